@@ -1,0 +1,702 @@
+/*
+ * ORACLE TEST INFRASTRUCTURE -- not product code.
+ *
+ * CPU restatement (plain C, fp64, scalar, single thread) of the reference's
+ * live multigrid path: the mode-9 driver `Semi_implicit_iterative`
+ * (transport_tri_semi.F90:14-891, selected by main.F90:16,46-47) with its
+ * internal smoother / get_residual / get_A_x / get_RHS / get_diagonal /
+ * solve_* subroutines, the inter-level transfers restrictor / prolongator /
+ * element_conversion (splitting.F90:10-151), the halo update_overlaps
+ * (splitting.F90:1210-1397), the sub-element numbering and geometry
+ * get_str_info / get_splitting (Msh2Tri.F90:32-107), the gmsh reader and the
+ * neighbour search ReadMSH / CheckNeig / getNeigDataMesh
+ * (Msh2Tri.F90:132-334,454-548,776-963) and the per-level shape-function
+ * scaling tri_det_nlx / semi_tri_det_nlx_multigrid (ShapFun.F90:1389-1454,
+ * 1661-1684) plus get_un_ele_mass_stiff_diffvol (ShapFun_unstruc.F90:304-335).
+ *
+ * It is the parity checker for the HIP path and the "port" CPU baseline.
+ * It follows the reference's structure literally -- stencils re-derived per
+ * un_ele per pass, source term and level-1 RHS re-evaluated at every
+ * sub-element visit, halo rewritten at the start of every sweep, the
+ * tnew / tnew_nonlin state machine of transport_tri_semi.F90:299-381 -- and
+ * its floating-point operation order (compile with -ffp-contract=off).
+ * Pinned against the instrumented reference build (oracle/build_ref.py) by
+ * tests/test_oracle_golden.py.
+ *
+ * Data layout = the reference's Fortran arrays: a level field
+ * tracer(l)%x(3, nsub_l, U) column-major is a C array [U][nsub_l][3].
+ * Quantities the reference leaves uninitialised are defined as zero (see
+ * oracle/build_ref.py for the matching patches).
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define NLOC 3
+#define NGI 3
+
+typedef struct {
+    int n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid;
+    double dt, k, omega, theta;
+} orc_cfg;
+
+typedef struct {
+    orc_cfg c;
+    int U;
+    double *X;      /* (2,3,U) */
+    int *region;    /* U */
+    int *neig;      /* (3,U), 1-based, 0 = boundary */
+    int *fneig;     /* (3,U) */
+    int *dir;       /* (3,U) 0/1 */
+    int nsub[16];   /* 4^(S-l+1), index l-1 */
+    double *tnew[16], *told[16], *rhs[16], *res[16], *source[16];
+    double *tnn;    /* tnew_nonlin, shape of level tnn_level */
+    int tnn_level;
+    double *detwei[16]; /* (3,U) per level */
+    double *nx[16];     /* (ngi,2,3,U) per level */
+    double *t_overlap, *t_overlap_old; /* (2^S*3, 3, U) */
+    int slots;
+} orc_state;
+
+/* ---------------------------------------------------------------- helpers */
+
+/* Msh2Tri.F90:32-60 get_str_info */
+static void get_str_info(int n_split, int ele, int *irow, int *ipos, int *orientation) {
+    int i = ele, row = 1, ele_row = (1 << (n_split + 1)) - 1;
+    while (i >= 1) {
+        if (i > ele_row) { i -= ele_row; row += 1; ele_row -= 2; }
+        else { *ipos = i; *irow = row; break; }
+    }
+    *orientation = *ipos % 2;
+}
+
+/* Msh2Tri.F90:69-107 get_splitting; un_x is (2,3) column-major */
+static void get_splitting(const double *un_x, int n_split, int str_ele, double str_x[3][2]) {
+    double p = (double)(1 << n_split);
+    double v1[2], v2[2];
+    int irow, ipos, orient;
+    v1[0] = (un_x[0] - un_x[4]) / p;
+    v1[1] = (un_x[1] - un_x[5]) / p;
+    v2[0] = (un_x[2] - un_x[4]) / p;
+    v2[1] = (un_x[3] - un_x[5]) / p;
+    get_str_info(n_split, str_ele, &irow, &ipos, &orient);
+    for (int d = 0; d < 2; ++d) {
+        double x3 = un_x[4 + d];
+        if (ipos % 2 != 0) {
+            str_x[2][d] = x3 + (irow - 1) * v2[d] + (ipos / 2) * v1[d];
+            str_x[1][d] = x3 + irow * v2[d] + (ipos / 2) * v1[d];
+            str_x[0][d] = x3 + (irow - 1) * v2[d] + v1[d] * (ipos / 2 + 1);
+        } else {
+            str_x[0][d] = x3 + irow * v2[d] + v1[d] * (ipos / 2 - 1);
+            str_x[1][d] = x3 + (irow - 1) * v2[d] + v1[d] * (ipos / 2);
+            str_x[2][d] = x3 + irow * v2[d] + v1[d] * (ipos / 2);
+        }
+    }
+}
+
+/* splitting.F90:1401-1405 boundary */
+static double boundary(double a, double b) { return sin(a + b); }
+
+/* splitting.F90:97-140 element_conversion; fin_ele 1-based */
+static void element_conversion(int fin[4], int coarse_ele, int i_split) {
+    int irow, ipos, orient, counter, tot_fine = 0;
+    int rowx = (1 << (i_split + 1)) * 2 - 1;
+    get_str_info(i_split, coarse_ele, &irow, &ipos, &orient);
+    if (orient == 1) {
+        counter = 2;
+        while (counter < irow * 2) { tot_fine += rowx; rowx -= 2; counter += 1; }
+        fin[0] = ipos * 2 - 1 + tot_fine;
+        fin[1] = fin[0] + 1;
+        fin[2] = fin[0] + 2;
+        tot_fine += rowx;
+        fin[3] = ipos * 2 - 1 + tot_fine;
+    } else {
+        counter = 1;
+        while (counter < irow * 2) { tot_fine += rowx; rowx -= 2; counter += 1; }
+        fin[2] = (ipos / 2 - 1) * 3 + ipos / 2 + tot_fine + 1;
+        fin[1] = fin[2] + 1;
+        fin[0] = fin[2] + 2;
+        fin[3] = fin[0] - rowx - 2;
+    }
+}
+
+/* splitting.F90:427-451 loc_surf_ele_multigrid; surf is (2^n, 3) column-major, 1-based values */
+static void loc_surf_ele(int n, int *surf) {
+    int m = 1 << n, ele, counter;
+    surf[0 + 0 * m] = 1;
+    for (ele = 2; ele <= m; ++ele) surf[(ele - 1) + 0 * m] = surf[(ele - 2) + 0 * m] + 2;
+    surf[0 + 2 * m] = 1;
+    counter = surf[(ele - 2) + 0 * m];
+    surf[0 + 1 * m] = counter;
+    for (ele = 2; ele <= m; ++ele) {
+        surf[(ele - 1) + 1 * m] = surf[(ele - 2) + 1 * m] + counter - 2;
+        surf[(ele - 1) + 2 * m] = surf[(ele - 2) + 1 * m] + 1;
+        counter -= 2;
+    }
+}
+
+/* --------------------------------------------------------- mesh ingest */
+
+typedef struct { int nodes; double *vx, *vy; } vtx_t;
+
+static int next_line(FILE *f, char *buf, int n) { return fgets(buf, n, f) != NULL; }
+
+static int trim_eq(const char *line, const char *tok) {
+    size_t n = strlen(tok);
+    while (*line == ' ' || *line == '\t') ++line;
+    if (strncmp(line, tok, n)) return 0;
+    line += n;
+    while (*line == ' ' || *line == '\t' || *line == '\r' || *line == '\n') ++line;
+    return *line == 0;
+}
+
+/* Generic.F90:50-58 AreEqual2: |X-Y|_2 < epsilon(double) */
+static int are_equal(double ax, double ay, double bx, double by) {
+    double dx = ax - bx, dy = ay - by;
+    return sqrt(dx * dx + dy * dy) < 2.220446049250313e-16;
+}
+
+static int check_vector(const int v[4], int num) {
+    for (int i = 0; i < 4; ++i) if (v[i] == num) return 1;
+    return 0;
+}
+
+static double length2d(double x1, double y1, double x2, double y2) {
+    return sqrt((x2 - x1) * (x2 - x1) + (y2 - y1) * (y2 - y1));
+}
+
+/* Msh2Tri.F90:776-963 CheckNeig (literal, including the l_d pre-filter) */
+static void check_neig(orc_state *s, int i, int j, int *no_neig, double l_d) {
+    const double *Xi = s->X + 6 * (i - 1), *Xj = s->X + 6 * (j - 1);
+    int vertex[4] = {0, 0, 0, 0}, counter = 0;
+    int one = 0, two = 0, three = 0, one2 = 0, two2 = 0, three2 = 0;
+    for (int a = 0; a < 3; ++a) {
+        for (int b = 0; b < 3; ++b) {
+            double d = length2d(Xi[2 * a], Xi[2 * a + 1], Xj[2 * b], Xj[2 * b + 1]);
+            if (d > l_d) counter += 1;
+            if (counter > 2) break;
+        }
+        if (counter > 2) break;
+    }
+    if (counter >= 2) return;
+    /* vertex codes as assigned at Msh2Tri.F90:820-871 */
+    static const int code[3][3] = {{1, 2, 3}, {2, 5, 6}, {3, 6, 9}};
+    for (int a = 0; a < 3; ++a) {
+        for (int b = 0; b < 3; ++b) {
+            if (are_equal(Xi[2 * a], Xi[2 * a + 1], Xj[2 * b], Xj[2 * b + 1])) {
+                vertex[a] = code[a][b];
+                if (a == 0) one = 1; else if (a == 1) two = 1; else three = 1;
+                if (b == 0) one2 = 1; else if (b == 1) two2 = 1; else three2 = 1;
+                break;
+            }
+        }
+    }
+    int *ni = s->neig + 3 * (i - 1), *nj = s->neig + 3 * (j - 1);
+    int *di = s->dir + 3 * (i - 1), *dj = s->dir + 3 * (j - 1);
+    if (one && three) {
+        ni[0] = j; *no_neig += 1;
+        if (check_vector(vertex, 1) || (check_vector(vertex, 2) && check_vector(vertex, 9))) di[0] = 1;
+        three = 0;
+    } else if (one && two) {
+        ni[1] = j; *no_neig += 1;
+        if (check_vector(vertex, 1) || (check_vector(vertex, 6) && check_vector(vertex, 2))) di[1] = 1;
+        one = 0;
+    } else if (three && two) {
+        ni[2] = j; *no_neig += 1;
+        if (check_vector(vertex, 9) || (check_vector(vertex, 6) && check_vector(vertex, 2))) di[2] = 1;
+        two = 0;
+    }
+    int jf = -1;
+    if (one2 && three2) jf = 0;
+    else if (one2 && two2) jf = 1;
+    else if (three2 && two2) jf = 2;
+    if (jf >= 0) {
+        nj[jf] = i;
+        if (one) dj[jf] = di[0];
+        else if (two) dj[jf] = di[1];
+        else if (three) dj[jf] = di[2];
+    }
+}
+
+/* Msh2Tri.F90:132-334 ReadMSH (gmsh 2.2 ascii). Returns number of triangles
+ * or <0 on error; if s != NULL also fills s->X, region, neig, dir, fneig. */
+static int read_msh(const char *path, orc_state *s) {
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    char line[4096];
+    int nodes = 0, nel = 0;
+    double *vx = NULL, *vy = NULL;
+    while (next_line(f, line, sizeof line)) if (trim_eq(line, "$Nodes")) break;
+    if (!next_line(f, line, sizeof line)) { fclose(f); return -2; }
+    nodes = atoi(line);
+    vx = calloc(nodes + 1, sizeof(double)); vy = calloc(nodes + 1, sizeof(double));
+    for (int i = 0; i < nodes; ++i) {
+        int id; double x, y, z;
+        if (!next_line(f, line, sizeof line) || sscanf(line, "%d %lf %lf %lf", &id, &x, &y, &z) != 4 ||
+            id < 1 || id > nodes) { fclose(f); free(vx); free(vy); return -3; }
+        vx[id] = x; vy[id] = y;
+    }
+    while (next_line(f, line, sizeof line)) if (trim_eq(line, "$Elements")) break;
+    if (!next_line(f, line, sizeof line)) { fclose(f); free(vx); free(vy); return -4; }
+    nel = atoi(line);
+    int *pos_of = calloc(nel + 1, sizeof(int)), *reg = calloc(nel + 1, sizeof(int));
+    int (*xp)[3] = calloc(nel + 1, sizeof *xp);
+    int j = 0;
+    double l_d = 0.0;
+    for (int i = 0; i < nel; ++i) {
+        if (!next_line(f, line, sizeof line)) { fclose(f); return -5; }
+        int tok[64], nt = 0;
+        char *p = line, *end;
+        while (nt < 64) { long v = strtol(p, &end, 10); if (end == p) break; tok[nt++] = (int)v; p = end; }
+        int pos = tok[0], type = tok[1];
+        if (!(type == 23 || type == 21 || type == 20 || type == 9 || type == 2 || type == 24 || type == 25)) {
+            j += 1; continue;
+        }
+        int ntag = tok[2];
+        reg[pos] = tok[3];
+        xp[pos][0] = tok[3 + ntag]; xp[pos][1] = tok[4 + ntag]; xp[pos][2] = tok[5 + ntag];
+        int a = xp[pos][0], b = xp[pos][1], c = xp[pos][2];
+        double d1 = length2d(vx[a], vy[a], vx[c], vy[c]);
+        double d2 = length2d(vx[a], vy[a], vx[b], vy[b]);
+        double d3 = length2d(vx[b], vy[b], vx[c], vy[c]);
+        if (d1 > l_d) l_d = d1;
+        if (d2 > l_d) l_d = d2;
+        if (d3 > l_d) l_d = d3;
+    }
+    fclose(f);
+    int U = nel - j;
+    if (s) {
+        s->U = U;
+        s->X = calloc(6 * (size_t)U, sizeof(double));
+        s->region = calloc(U, sizeof(int));
+        s->neig = calloc(3 * (size_t)U, sizeof(int));
+        s->fneig = calloc(3 * (size_t)U, sizeof(int));
+        s->dir = calloc(3 * (size_t)U, sizeof(int));
+        for (int i = j + 1; i <= nel; ++i) {   /* meshList(i-j) = meshList2(i) */
+            int e = i - j - 1;
+            s->region[e] = reg[i];
+            for (int k = 0; k < 3; ++k) {
+                s->X[6 * e + 2 * k] = vx[xp[i][k]];
+                s->X[6 * e + 2 * k + 1] = vy[xp[i][k]];
+            }
+        }
+        for (int a = 1; a <= U; ++a) {
+            int no_neig = 0;
+            for (int b = a + 1; b <= U; ++b) {
+                check_neig(s, a, b, &no_neig, l_d);
+                if (no_neig == 3) break;
+            }
+        }
+        /* transport_tri_semi.F90:222-228 + Msh2Tri.F90:463-468 getNeigDataMesh: fNeig = NumLoc(Neig(Npos), Mpos) */
+        for (int e = 0; e < U; ++e)
+            for (int fc = 0; fc < 3; ++fc) {
+                int np = s->neig[3 * e + fc], ns = 0;
+                if (np != 0) {
+                    for (int q = 0; q < 3; ++q) if (s->neig[3 * (np - 1) + q] == e + 1) { ns = q + 1; break; }
+                }
+                s->fneig[3 * e + fc] = ns;
+            }
+    }
+    free(vx); free(vy); free(pos_of); free(reg); free(xp);
+    return U;
+}
+
+/* ------------------------------------------------------- geometry/stencils */
+
+static const double N_gl[NGI][NLOC] = {{0.5, 0.5, 0.0}, {0.0, 0.5, 0.5}, {0.5, 0.0, 0.5}};  /* TRIQUAold :554-563, SHATRIold :1036-1040 */
+static const double NLX[2][NLOC] = {{1.0, 0.0, -1.0}, {0.0, 1.0, -1.0}};                    /* SHATRIold :1042-1048 */
+
+/* ShapFun.F90:1389-1454 tri_det_nlx + :1678-1683 per-level scaling */
+static void level_geometry(const double *X, int i_split, double detwei[NGI], double nx[NGI][2][NLOC]) {
+    const double weight = 1.0 / 3.0;
+    for (int g = 0; g < NGI; ++g) {
+        double agi = 0, bgi = 0, cgi = 0, dgi = 0;
+        for (int L = 0; L < NLOC; ++L) {
+            agi = agi + NLX[0][L] * X[2 * L];
+            bgi = bgi + NLX[0][L] * X[2 * L + 1];
+            cgi = cgi + NLX[1][L] * X[2 * L];
+            dgi = dgi + NLX[1][L] * X[2 * L + 1];
+        }
+        double detj = agi * dgi - bgi * cgi;
+        detwei[g] = 0.5 * fabs(detj) * weight;
+        double a11 = dgi / detj, a21 = -(cgi / detj), a12 = -(bgi / detj), a22 = agi / detj;
+        for (int L = 0; L < NLOC; ++L) {
+            nx[g][0][L] = a11 * NLX[0][L] + a12 * NLX[1][L];
+            nx[g][1][L] = a21 * NLX[0][L] + a22 * NLX[1][L];
+        }
+        detwei[g] = detwei[g] / (double)(1 << (2 * i_split));
+        for (int d = 0; d < 2; ++d)
+            for (int L = 0; L < NLOC; ++L) nx[g][d][L] = nx[g][d][L] * (double)(1 << i_split);
+    }
+}
+
+/* ShapFun_unstruc.F90:304-335 + transport_tri_semi.F90:602-606 (diff_vol1 reduction) */
+static void stencil(const double detwei[NGI], double nx[NGI][2][NLOC], double k,
+                    double M[3][3], double Kd[3][3], double ml[3]) {
+    for (int j = 0; j < NLOC; ++j) {
+        double s = 0;
+        for (int g = 0; g < NGI; ++g) s = s + N_gl[g][j] * detwei[g];
+        ml[j] = s;
+        for (int i = 0; i < NLOC; ++i) {
+            double m = 0;
+            for (int g = 0; g < NGI; ++g) m = m + N_gl[g][i] * detwei[g] * N_gl[g][j];
+            M[i][j] = m;
+        }
+    }
+    for (int i = 0; i < NLOC; ++i)
+        for (int j = 0; j < NLOC; ++j) {
+            double acc = 0.0;
+            for (int d = 0; d < 2; ++d) {
+                double s = 0;
+                for (int g = 0; g < NGI; ++g) s = s + k * nx[g][d][i] * detwei[g] * nx[g][d][j];
+                acc = acc + s;
+            }
+            Kd[i][j] = acc;
+        }
+}
+
+/* ------------------------------------------------------------ the state */
+
+static size_t lvl_len(orc_state *s, int l) { return (size_t)3 * s->nsub[l - 1] * s->U; }
+
+static void copy_to_tnn(orc_state *s, int l) {   /* :325-327 realloc + copy */
+    free(s->tnn);
+    s->tnn = malloc(lvl_len(s, l) * sizeof(double));
+    memcpy(s->tnn, s->tnew[l - 1], lvl_len(s, l) * sizeof(double));
+    s->tnn_level = l;
+}
+
+/* splitting.F90:1210-1397 update_overlaps (faces in the order 1, 3, 2) */
+static void update_overlaps(orc_state *s, int l) {
+    int i_split = s->c.n_split - l + 1, m = 1 << i_split, sl = s->slots;
+    int *surf = malloc(sizeof(int) * 3 * m);
+    loc_surf_ele(i_split, surf);
+    const double *T = s->tnew[l - 1], *To = s->told[l - 1];
+    int nsub = s->nsub[l - 1];
+    static const int face_order[3] = {1, 3, 2};
+    for (int u = 0; u < s->U; ++u) {
+        for (int fo = 0; fo < 3; ++fo) {
+            int f = face_order[fo];
+            for (int i = 1; i <= m; ++i) {
+                int se = surf[(i - 1) + (f - 1) * m], irow, ipos, orient;
+                get_str_info(i_split, se, &irow, &ipos, &orient);
+                int npos = s->neig[3 * u + f - 1];
+                double xl[3][2];
+                get_splitting(s->X + 6 * u, i_split, se, xl);
+                const double *tv = T + (size_t)3 * ((size_t)u * nsub + se - 1);
+                const double *tov = To + (size_t)3 * ((size_t)u * nsub + se - 1);
+                if (npos == 0) {
+                    double *ov = s->t_overlap + (size_t)u * sl * 3 + (size_t)(f - 1) * sl;
+                    double *oo = s->t_overlap_old + (size_t)u * sl * 3 + (size_t)(f - 1) * sl;
+                    int a, b, na, nb;   /* 1-based slots and local nodes */
+                    if (f == 1) { a = (ipos / 2) * 3 + 1; b = (ipos / 2) * 3 + 3; na = 0; nb = 2; }
+                    else if (f == 3) { a = (irow - 1) * 3 + 2; b = (irow - 1) * 3 + 3; na = 1; nb = 2; }
+                    else { a = (irow - 1) * 3 + 1; b = (irow - 1) * 3 + 2; na = 0; nb = 1; }
+                    double t1 = boundary(xl[na][0], xl[na][1]), t2 = boundary(xl[nb][0], xl[nb][1]);
+                    ov[a - 1] = t1; ov[b - 1] = t2; oo[a - 1] = t1; oo[b - 1] = t2;
+                } else {
+                    int nside = s->fneig[3 * u + f - 1], dir = s->dir[3 * u + f - 1], kslot;
+                    int fwd, rev;
+                    if (f == 1) { fwd = ipos / 2 + 1; rev = m - (ipos / 2 + 1) + 1; }
+                    else { fwd = irow; rev = m - irow + 1; }
+                    if (f == 2) { int t = fwd; fwd = rev; rev = t; }   /* face 2 is mirrored (:1354-1391) */
+                    if (nside == 2) kslot = dir ? rev : fwd;
+                    else kslot = dir ? fwd : rev;
+                    double *ov = s->t_overlap + (size_t)(npos - 1) * sl * 3 + (size_t)(nside - 1) * sl;
+                    double *oo = s->t_overlap_old + (size_t)(npos - 1) * sl * 3 + (size_t)(nside - 1) * sl;
+                    for (int q = 0; q < 3; ++q) { ov[kslot * 3 - 3 + q] = tv[q]; oo[kslot * 3 - 3 + q] = tov[q]; }
+                }
+            }
+        }
+    }
+    free(surf);
+}
+
+/* One sub-element visit of the smoother / residual: stencil products.
+ * get_A_x :412-448 with theta, zero advection / flux / surface terms. */
+static void get_A_x(const orc_state *s, const double M[3][3], const double Kd[3][3], double rdt,
+                    const double *x, const double *xo, double A[3], double mo[3]) {
+    double theta = s->c.theta;
+    for (int i = 0; i < 3; ++i) {
+        mo[i] = rdt * (M[i][0] * xo[0] + M[i][1] * xo[1] + M[i][2] * xo[2]);
+        double mn = rdt * (M[i][0] * x[0] + M[i][1] * x[1] + M[i][2] * x[2]);
+        double dv = Kd[i][0] * x[0] + Kd[i][1] * x[1] + Kd[i][2] * x[2];
+        double sn = 0.0, fn = 0.0, ds = 0.0;
+        A[i] = theta * (mn - sn + fn + dv + ds) + (1. - theta) * (mn);
+    }
+}
+
+/* source (:593) + get_RHS (:452-464), level 1 only; writes rhs[3] and source */
+static void get_rhs_l1(const orc_state *s, const double M[3][3], const double xl[3][2],
+                       const double mo[3], double *src, double *rhs) {
+    double theta = s->c.theta, k = s->c.k;
+    for (int i = 0; i < 3; ++i) src[i] = -(2 * k * boundary(xl[i][0], xl[i][1]));
+    for (int i = 0; i < 3; ++i) {
+        src[i] = M[i][0] * src[0] + M[i][1] * src[1] + M[i][2] * src[2];
+        rhs[i] = theta * (mo[i] + src[i]) + (1. - theta) * (mo[i] + src[i]);
+    }
+}
+
+/* transport_tri_semi.F90:543-722 smoother */
+static void smoother(orc_state *s, int l) {
+    int i_split = s->c.n_split - l + 1, nsub = s->nsub[l - 1];
+    double rdt = 1 / s->c.dt, om = s->c.omega;
+    double *T = s->tnew[l - 1], *To = s->told[l - 1], *R = s->rhs[l - 1], *Src = s->source[l - 1];
+    for (int sm = 0; sm < s->c.n_smooth; ++sm) {
+        memcpy(T, s->tnn, lvl_len(s, l) * sizeof(double));     /* :550 */
+        update_overlaps(s, l);                                  /* :555 */
+        for (int u = 0; u < s->U; ++u) {
+            double M[3][3], Kd[3][3], ml[3];
+            stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+            for (int se = 1; se <= nsub; ++se) {
+                size_t o = (size_t)3 * ((size_t)u * nsub + se - 1);
+                double xl[3][2];
+                get_splitting(s->X + 6 * u, i_split, se, xl);
+                double *tnn = s->tnn + o;
+                if (s->c.solver == 2) {   /* solve_Richardson :511-518, mass/stiff/flux reset to 0 at :585-612 */
+                    for (int i = 0; i < 3; ++i) Src[o + i] = -(2 * s->c.k * boundary(xl[i][0], xl[i][1]));
+                    for (int i = 0; i < 3; ++i) tnn[i] = tnn[i] + om * (R[o + i] - (0.0 - 0.0 + 0.0));
+                    continue;
+                }
+                double A[3], mo[3], D[3];
+                const double *xin = (s->c.solver == 3) ? tnn : T + o;   /* get_A_x(.true./.false.) */
+                get_A_x(s, M, Kd, rdt, xin, To + o, A, mo);
+                if (l == 1) get_rhs_l1(s, M, xl, mo, Src + o, R + o);
+                else for (int i = 0; i < 3; ++i) Src[o + i] = -(2 * s->c.k * boundary(xl[i][0], xl[i][1]));
+                for (int i = 0; i < 3; ++i) D[i] = rdt * ml[i] + Kd[i][i] + 0.0;   /* get_diagonal :481-486 */
+                for (int i = 0; i < 3; ++i) {
+                    double base = (s->c.solver == 3) ? tnn[i] : T[o + i];   /* :504 vs :494 */
+                    tnn[i] = base + om / D[i] * (R[o + i] - A[i]);
+                }
+            }
+        }
+    }
+}
+
+/* transport_tri_semi.F90:725-873 get_residual */
+static void get_residual(orc_state *s, int l) {
+    int i_split = s->c.n_split - l + 1, nsub = s->nsub[l - 1];
+    double rdt = 1 / s->c.dt;
+    double *T = s->tnew[l - 1], *To = s->told[l - 1], *R = s->rhs[l - 1], *Src = s->source[l - 1];
+    for (int u = 0; u < s->U; ++u) {
+        double M[3][3], Kd[3][3], ml[3];
+        stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+        for (int se = 1; se <= nsub; ++se) {
+            size_t o = (size_t)3 * ((size_t)u * nsub + se - 1);
+            double xl[3][2], A[3], mo[3];
+            get_splitting(s->X + 6 * u, i_split, se, xl);
+            get_A_x(s, M, Kd, rdt, T + o, To + o, A, mo);
+            if (l == 1) get_rhs_l1(s, M, xl, mo, Src + o, R + o);
+            else for (int i = 0; i < 3; ++i) Src[o + i] = -(2 * s->c.k * boundary(xl[i][0], xl[i][1]));
+            for (int i = 0; i < 3; ++i) s->res[l - 1][o + i] = A[i] - R[o + i];
+        }
+    }
+}
+
+/* splitting.F90:10-32 restrictor */
+static void restrictor(orc_state *s, int l) {
+    if (l >= s->c.levels) return;
+    int i_split = s->c.n_split - l + 1, nf = s->nsub[l - 1], nc = s->nsub[l];
+    const double *r = s->res[l - 1];
+    double *b = s->rhs[l];
+    for (int u = 0; u < s->U; ++u)
+        for (int c = 1; c <= nc; ++c) {
+            int fin[4];
+            element_conversion(fin, c, i_split - 1);
+            const int pick[3] = {fin[2], fin[3], fin[0]};
+            for (int i = 0; i < 3; ++i) {
+                const double *rv = r + (size_t)3 * ((size_t)u * nf + pick[i] - 1);
+                b[(size_t)3 * ((size_t)u * nc + c - 1) + i] = (rv[0] + rv[1] + rv[2]) / 3.;
+            }
+        }
+}
+
+/* splitting.F90:38-91 prolongator */
+static void prolongator(orc_state *s, int l) {
+    int i_split = s->c.n_split - l + 1, nf = s->nsub[l - 1], nc = s->nsub[l];
+    double *F = s->tnew[l - 1];
+    const double *Y = s->tnew[l];
+    for (int u = 0; u < s->U; ++u)
+        for (int c = 1; c <= nc; ++c) {
+            int fin[4];
+            element_conversion(fin, c, i_split - 1);
+            const double *y = Y + (size_t)3 * ((size_t)u * nc + c - 1);
+            double *f1 = F + (size_t)3 * ((size_t)u * nf + fin[0] - 1);
+            double *f2 = F + (size_t)3 * ((size_t)u * nf + fin[1] - 1);
+            double *f3 = F + (size_t)3 * ((size_t)u * nf + fin[2] - 1);
+            double *f4 = F + (size_t)3 * ((size_t)u * nf + fin[3] - 1);
+            f1[0] = f1[0] + 0.5 * y[2] + 0.5 * y[0];
+            f1[1] = f1[1] + 0.5 * y[1] + 0.5 * y[2];
+            f1[2] = f1[2] + y[2];
+            f2[0] = f2[0] + f1[1];
+            f2[1] = f2[1] + f1[0];
+            f2[2] = f2[2] + 0.5 * y[0] + 0.5 * y[1];
+            f3[0] = f3[0] + y[0];
+            f3[1] = f3[1] + f2[2];
+            f3[2] = f3[2] + f2[1];
+            f4[0] = f4[0] + f2[2];
+            f4[1] = f4[1] + y[1];
+            f4[2] = f4[2] + f2[0];
+        }
+}
+
+/* ----------------------------------------------------------- public API */
+
+int orc_msh_count(const char *path) { return read_msh(path, NULL); }
+
+/* Mesh + topology exactly as the reference builds it (ReadMSH/CheckNeig/getNeigDataMesh). */
+int orc_msh_load(const char *path, int U, double *X, int *region, int *neig, int *fneig, int *dir) {
+    orc_state s;
+    memset(&s, 0, sizeof s);
+    int n = read_msh(path, &s);
+    if (n < 0) return n;
+    if (n != U) return -10;
+    memcpy(X, s.X, sizeof(double) * 6 * U);
+    memcpy(region, s.region, sizeof(int) * U);
+    memcpy(neig, s.neig, sizeof(int) * 3 * U);
+    memcpy(fneig, s.fneig, sizeof(int) * 3 * U);
+    memcpy(dir, s.dir, sizeof(int) * 3 * U);
+    free(s.X); free(s.region); free(s.neig); free(s.fneig); free(s.dir);
+    return 0;
+}
+
+orc_state *orc_create(const orc_cfg *cfg, int U, const double *X, const int *region, const int *neig,
+                      const int *fneig, const int *dir) {
+    if (cfg->levels < 1 || cfg->levels > cfg->n_split || cfg->n_split > 12) return NULL;  /* :120-123 */
+    if (cfg->theta != 1.0) return NULL;   /* theta hard-coded to 1 (:117); the theta<1 RHS is iterate-dependent */
+    orc_state *s = calloc(1, sizeof *s);
+    s->c = *cfg;
+    s->U = U;
+    s->X = malloc(sizeof(double) * 6 * U); memcpy(s->X, X, sizeof(double) * 6 * U);
+    s->region = malloc(sizeof(int) * U); memcpy(s->region, region, sizeof(int) * U);
+    s->neig = malloc(sizeof(int) * 3 * U); memcpy(s->neig, neig, sizeof(int) * 3 * U);
+    s->fneig = malloc(sizeof(int) * 3 * U); memcpy(s->fneig, fneig, sizeof(int) * 3 * U);
+    s->dir = malloc(sizeof(int) * 3 * U); memcpy(s->dir, dir, sizeof(int) * 3 * U);
+    for (int l = 1; l <= cfg->levels; ++l) {
+        int i_split = cfg->n_split - l + 1;
+        s->nsub[l - 1] = 1 << (2 * i_split);
+        size_t n = lvl_len(s, l);
+        s->tnew[l - 1] = calloc(n, sizeof(double));
+        s->told[l - 1] = calloc(n, sizeof(double));
+        s->rhs[l - 1] = calloc(n, sizeof(double));
+        s->res[l - 1] = calloc(n, sizeof(double));
+        s->source[l - 1] = calloc(n, sizeof(double));
+        s->detwei[l - 1] = calloc((size_t)3 * U, sizeof(double));
+        s->nx[l - 1] = calloc((size_t)18 * U, sizeof(double));
+        for (int u = 0; u < U; ++u)
+            level_geometry(s->X + 6 * u, i_split, s->detwei[l - 1] + 3 * u,
+                           (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u));
+    }
+    /* :249-251 region 4 => tnew(level 1) = 1 */
+    for (int u = 0; u < U; ++u)
+        if (s->region[u] == 4)
+            for (int q = 0; q < 3 * s->nsub[0]; ++q) s->tnew[0][(size_t)3 * s->nsub[0] * u + q] = 1.0;
+    s->slots = (1 << cfg->n_split) * 3;
+    s->t_overlap = calloc((size_t)s->slots * 3 * U, sizeof(double));
+    s->t_overlap_old = calloc((size_t)s->slots * 3 * U, sizeof(double));
+    copy_to_tnn(s, 1);
+    return s;
+}
+
+void orc_free(orc_state *s) {
+    if (!s) return;
+    for (int l = 0; l < s->c.levels; ++l) {
+        free(s->tnew[l]); free(s->told[l]); free(s->rhs[l]); free(s->res[l]); free(s->source[l]);
+        free(s->detwei[l]); free(s->nx[l]);
+    }
+    free(s->tnn); free(s->t_overlap); free(s->t_overlap_old);
+    free(s->X); free(s->region); free(s->neig); free(s->fneig); free(s->dir);
+    free(s);
+}
+
+/* what: 0 tnew, 1 told, 2 rhs, 3 res, 4 tnn (level ignored), 5 source */
+static double *field(orc_state *s, int what, int l, size_t *n) {
+    if (what == 4) { *n = lvl_len(s, s->tnn_level); return s->tnn; }
+    if (l < 1 || l > s->c.levels) return NULL;
+    *n = lvl_len(s, l);
+    switch (what) {
+        case 0: return s->tnew[l - 1];
+        case 1: return s->told[l - 1];
+        case 2: return s->rhs[l - 1];
+        case 3: return s->res[l - 1];
+        case 5: return s->source[l - 1];
+    }
+    return NULL;
+}
+
+long orc_get(orc_state *s, int what, int l, double *out) {
+    size_t n; double *p = field(s, what, l, &n);
+    if (!p) return -1;
+    if (out) memcpy(out, p, n * sizeof(double));
+    return (long)n;
+}
+
+int orc_set(orc_state *s, int what, int l, const double *in) {
+    size_t n; double *p = field(s, what, l, &n);
+    if (!p) return -1;
+    memcpy(p, in, n * sizeof(double));
+    return 0;
+}
+
+int orc_tnn_level(orc_state *s) { return s->tnn_level; }
+
+void orc_get_overlap(orc_state *s, double *tov, double *tovo) {
+    size_t n = (size_t)s->slots * 3 * s->U;
+    if (tov) memcpy(tov, s->t_overlap, n * sizeof(double));
+    if (tovo) memcpy(tovo, s->t_overlap_old, n * sizeof(double));
+}
+
+void orc_level_geometry(orc_state *s, int l, double *detwei, double *M, double *Kd, double *ml) {
+    for (int u = 0; u < s->U; ++u) {
+        double m[3][3], kd[3][3], l3[3];
+        stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, m, kd, l3);
+        for (int i = 0; i < 3; ++i) {
+            detwei[3 * u + i] = s->detwei[l - 1][3 * u + i];
+            ml[3 * u + i] = l3[i];
+            for (int j = 0; j < 3; ++j) {   /* Fortran (i,j,u) column-major */
+                M[9 * u + i + 3 * j] = m[i][j];
+                Kd[9 * u + i + 3 * j] = kd[i][j];
+            }
+        }
+    }
+}
+
+void orc_copy_to_tnn(orc_state *s, int l) { copy_to_tnn(s, l); }
+void orc_smoother(orc_state *s, int l) { smoother(s, l); }
+void orc_get_residual(orc_state *s, int l) { get_residual(s, l); }
+void orc_restrictor(orc_state *s, int l) { restrictor(s, l); }
+void orc_prolongator(orc_state *s, int l) { prolongator(s, l); }
+void orc_update_overlaps(orc_state *s, int l) { update_overlaps(s, l); }
+
+/* :316-317 */
+void orc_begin_timestep(orc_state *s) {
+    memcpy(s->told[0], s->tnew[0], lvl_len(s, 1) * sizeof(double));
+    copy_to_tnn(s, 1);
+}
+
+/* :319-379, one pass of the n_multigrid loop (one V-cycle) */
+void orc_vcycle(orc_state *s) {
+    int L = s->c.levels;
+    for (int l = 1; l <= L; ++l) {
+        copy_to_tnn(s, l);
+        smoother(s, l);
+        restrictor(s, l);
+        get_residual(s, l);
+    }
+    copy_to_tnn(s, L);
+    for (int i = 0; i < s->c.n_coarse; ++i) smoother(s, L);
+    for (int l = L - 1; l >= 1; --l) {
+        copy_to_tnn(s, l);
+        prolongator(s, l);
+        smoother(s, l);
+    }
+}
+
+/* :299-381 the time loop */
+void orc_run(orc_state *s) {
+    for (int it = 0; it < s->c.ntime; ++it) {
+        orc_begin_timestep(s);
+        for (int mg = 0; mg < s->c.n_multigrid; ++mg) orc_vcycle(s);
+    }
+}

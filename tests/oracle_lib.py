@@ -1,0 +1,147 @@
+"""ctypes binding of the C oracle (oracle/pamg_oracle.c -> oracle/_build/liborc.so).
+
+TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg use this module, and only as the checker / CPU baseline.
+Field arrays are returned in the reference's Fortran shape (3, nsub, U).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "_build", "liborc.so")
+
+TNEW, TOLD, RHS, RES, TNN, SOURCE = 0, 1, 2, 3, 4, 5
+
+
+class OrcCfg(C.Structure):
+    _fields_ = [("n_split", C.c_int), ("levels", C.c_int), ("n_smooth", C.c_int),
+                ("n_coarse", C.c_int), ("solver", C.c_int), ("ntime", C.c_int),
+                ("n_multigrid", C.c_int), ("dt", C.c_double), ("k", C.c_double),
+                ("omega", C.c_double), ("theta", C.c_double)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        ip = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+        L.orc_msh_count.argtypes = [C.c_char_p]
+        L.orc_msh_load.argtypes = [C.c_char_p, C.c_int, dp, ip, ip, ip, ip]
+        L.orc_create.restype = P
+        L.orc_create.argtypes = [C.POINTER(OrcCfg), C.c_int, dp, ip, ip, ip, ip]
+        L.orc_free.argtypes = [P]
+        L.orc_get.restype = C.c_long
+        L.orc_get.argtypes = [P, C.c_int, C.c_int, C.c_void_p]
+        L.orc_set.argtypes = [P, C.c_int, C.c_int, dp]
+        L.orc_tnn_level.argtypes = [P]
+        L.orc_get_overlap.argtypes = [P, dp, dp]
+        L.orc_level_geometry.argtypes = [P, C.c_int, dp, dp, dp, dp]
+        for name in ("orc_copy_to_tnn", "orc_smoother", "orc_get_residual", "orc_restrictor",
+                     "orc_prolongator", "orc_update_overlaps"):
+            getattr(L, name).argtypes = [P, C.c_int]
+        for name in ("orc_begin_timestep", "orc_vcycle", "orc_run"):
+            getattr(L, name).argtypes = [P]
+        _lib = L
+    return _lib
+
+
+class Mesh:
+    """Reference topology: X (2,3,U), region (U), Neig/fNeig/Dir (3,U), 1-based neighbours."""
+
+    def __init__(self, U, X, region, neig, fneig, dir_):
+        self.U, self.X, self.region, self.neig, self.fneig, self.dir = U, X, region, neig, fneig, dir_
+
+
+def read_msh(path):
+    L = lib()
+    U = L.orc_msh_count(path.encode())
+    if U < 0:
+        raise IOError(f"oracle could not read {path} ({U})")
+    X = np.zeros(6 * U, np.float64)
+    reg = np.zeros(U, np.int32)
+    ne, fn, di = (np.zeros(3 * U, np.int32) for _ in range(3))
+    rc = L.orc_msh_load(path.encode(), U, X, reg, ne, fn, di)
+    if rc != 0:
+        raise IOError(f"oracle msh load failed {rc}")
+    return Mesh(U, X, reg, ne, fn, di)
+
+
+class Oracle:
+    def __init__(self, mesh, n_split, levels, n_smooth=4, solver=3, ntime=2, n_multigrid=2,
+                 n_coarse=15, dt=1.25e-5, k=1.0, omega=0.8, theta=1.0):
+        self.L = lib()
+        self.mesh = mesh
+        self.cfg = OrcCfg(n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid, dt, k, omega, theta)
+        self.h = self.L.orc_create(C.byref(self.cfg), mesh.U, mesh.X, mesh.region, mesh.neig,
+                                   mesh.fneig, mesh.dir)
+        if not self.h:
+            raise ValueError("orc_create rejected the configuration")
+        self.n_split, self.levels = n_split, levels
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.orc_free(self.h)
+            self.h = None
+
+    def nsub(self, level):
+        return 4 ** (self.n_split - level + 1)
+
+    def get(self, what, level=1):
+        n = self.L.orc_get(self.h, what, level, None)
+        out = np.empty(n, np.float64)
+        self.L.orc_get(self.h, what, level, out.ctypes.data)
+        lv = self.L.orc_tnn_level(self.h) if what == TNN else level
+        return out.reshape((3, self.nsub(lv), self.mesh.U), order="F")
+
+    def set(self, what, level, arr):
+        a = np.ascontiguousarray(np.asarray(arr, np.float64).reshape(-1, order="F"))
+        assert self.L.orc_set(self.h, what, level, a) == 0
+
+    def overlap(self):
+        n = (2 ** self.n_split) * 3 * 3 * self.mesh.U
+        a, b = np.empty(n), np.empty(n)
+        self.L.orc_get_overlap(self.h, a, b)
+        shp = ((2 ** self.n_split) * 3, 3, self.mesh.U)
+        return a.reshape(shp, order="F"), b.reshape(shp, order="F")
+
+    def geometry(self, level):
+        U = self.mesh.U
+        dw, M, Kd, ml = np.empty(3 * U), np.empty(9 * U), np.empty(9 * U), np.empty(3 * U)
+        self.L.orc_level_geometry(self.h, level, dw, M, Kd, ml)
+        return (dw.reshape((3, U), order="F"), M.reshape((3, 3, U), order="F"),
+                Kd.reshape((3, 3, U), order="F"), ml.reshape((3, U), order="F"))
+
+    def copy_to_tnn(self, l): self.L.orc_copy_to_tnn(self.h, l)
+    def smoother(self, l): self.L.orc_smoother(self.h, l)
+    def get_residual(self, l): self.L.orc_get_residual(self.h, l)
+    def restrictor(self, l): self.L.orc_restrictor(self.h, l)
+    def prolongator(self, l): self.L.orc_prolongator(self.h, l)
+    def update_overlaps(self, l): self.L.orc_update_overlaps(self.h, l)
+    def begin_timestep(self): self.L.orc_begin_timestep(self.h)
+    def vcycle(self): self.L.orc_vcycle(self.h)
+    def run(self): self.L.orc_run(self.h)
+
+    def state(self):
+        d = {}
+        for l in range(1, self.levels + 1):
+            d[f"tnew_L{l}"] = self.get(TNEW, l)
+            d[f"told_L{l}"] = self.get(TOLD, l)
+            d[f"RHS_L{l}"] = self.get(RHS, l)
+            d[f"res_L{l}"] = self.get(RES, l)
+        d["tnew_nonlin"] = self.get(TNN)
+        return d
