@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Benchmark: multigrid V-cycles/s + level-1 smoother HBM GB/s vs roofline.
+
+Workload (BASELINE.json configs[2], the 8192-element metric): the reference
+mesh untitled8192.msh (128x32x2 triangles), n_split = 5 (8,388,608 fine
+sub-elements, 25.2 M DOF; every level lives in HBM, well past the 256 MiB
+Infinity Cache), multi_levels = 3, n_smooth = 4, solver = 3 (block
+Gauss-Seidel), the reference's mode-9 physics (dt = 1.25e-5, k = 1,
+omega = 0.8). One step = one V-cycle of transport_tri_semi.F90:319-379
+(restriction leg, 15 coarse smoother calls, prolongation leg, halo after
+every smoother call) over the whole mesh.
+
+N > 1 (python -m torch.distributed.run ... bench.py --gpus N): strong scaling
+of the same mesh, x-strip domain decomposition by unstructured element, one
+process per GPU, halo exchanged with RCCL (grouped ncclSend/ncclRecv over
+xGMI) after every smoother call. `value` = V-cycles of the whole mesh / max
+over ranks of the timed wall time.
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "p-a_multigrids_amd"))
+MESH = os.path.join(ROOT, "tests", "meshes", "untitled8192.msh")
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nsplit", type=int, default=5)
+    ap.add_argument("--levels", type=int, default=3)
+    ap.add_argument("--nsmooth", type=int, default=4)
+    ap.add_argument("--mesh", default=MESH)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the n_split=3 and sweep-kernel side measurements")
+    ap.add_argument("--halo-mode", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline():
+    """Reference CPU path on this host: the reference Fortran itself (fp64
+    build, oracle/_ref, 1 core, its own `cpu_time for time_loop` window) on a
+    bounded sample -- 1 V-cycle of untitled8192 at n_split = 3, which is 1/16 of
+    the n_split = 5 work on every level -- scaled to the benchmarked config."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "pamg_ref_fp64")
+    kind = "reference"
+    if not os.path.exists(exe):
+        return None
+    tmp = tempfile.mkdtemp(prefix="pamg_cpu_")
+    try:
+        shutil.copy(MESH, tmp)
+        with open(os.path.join(tmp, "pamg_ref.nml"), "w") as f:
+            f.write("&pamg_ref\n pamg_mesh='untitled8192.msh', pamg_dump_prefix='', pamg_nsplit=3, pamg_ntime=1,\n"
+                    " pamg_nmultigrid=1, pamg_solver=3, pamg_levels=3, pamg_nsmooth=4, pamg_vtk=100000\n/\n")
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        r = subprocess.run(["taskset", "-c", "0", exe] if shutil.which("taskset") else [exe], cwd=tmp,
+                           capture_output=True, text=True, timeout=900, env=env)
+        m = re.search(r"cpu_time for time_loop =\s*([0-9.Ee+-]+)", r.stdout)
+        if r.returncode != 0 or not m:
+            return None
+        t = float(m.group(1))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return dict(value=1.0 / (16.0 * t), unit="V-cycles/s", cores=1, kind=kind,
+                sample=f"reference fp64 build (flang -O2), 1 V-cycle of untitled8192 at n_split=3, multi_levels=3 "
+                       f"took {t:.2f} s in its time_loop window on 1 core; n_split=5 has 16x the sub-elements on "
+                       f"every level, value = 1/(16*{t:.2f} s)",
+                nsplit3_vcycles_per_s=1.0 / t)
+
+
+def pmc_traffic(nsplit):
+    """HBM bytes per level-1 smoother launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_smooth_l1.json), if one exists for this config."""
+    p = os.path.join(ROOT, "profiles", "pmc_smooth_l1.json")
+    try:
+        d = json.load(open(p))
+        if int(d.get("n_split", -1)) == nsplit:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    # torch first: libpamg then binds the same HIP / RCCL runtime (shared sonames)
+    import torch
+    import torch.distributed as dist
+    import pamg
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    mesh = pamg.Mesh.read(a.mesh)
+    comm = None
+    if world > 1:
+        obj = [pamg.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = (world, rank, obj[0], mesh.x_strip_owner(world))
+    s = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=local,
+                                   halo_mode=a.halo_mode, comm=comm)
+    s.begin_timestep()
+    s.vcycle(a.warmup)
+    s.synchronize()
+    s.timing_enable(0x7F)
+    s.timing_reset()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.vcycle(a.steps)
+    s.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    tm = s.timing()
+    value = a.steps / elapsed
+    # dominant kernel by total time inside the timed region
+    dom = max((k for k in tm if tm[k]["launches"] > 0 and k != "sweep_bench"), key=lambda k: tm[k]["ms"])
+    kinfo = tm["smooth_L1"]
+    ms_per_launch = kinfo["ms"] / max(1, kinfo["launches"])
+    bytes_per_launch = kinfo["bytes"] / max(1, kinfo["launches"])
+    achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
+    traffic = pmc_traffic(a.nsplit) if world == 1 else None
+    extra = {"kernels": {k: dict(ms_total=round(v["ms"], 4), launches=v["launches"],
+                                 gbs=round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None)
+                         for k, v in tm.items() if v["launches"]},
+             "dominant_kernel": dom, "fine_sub_elements_per_rank": s.U * 4 ** a.nsplit}
+    if rank == 0 and world == 1 and not a.no_extra:
+        for asm in (False, True):
+            ms, by = s.sweep_bench(20, asm)
+            extra["sweep_assembled" if asm else "sweep_stencil"] = dict(
+                ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
+                frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
+        s.close()
+        s3 = pamg.SemiImplicitIterative(mesh, 3, a.levels, n_smooth=a.nsmooth, solver=3, device=local)
+        s3.begin_timestep()
+        s3.vcycle(a.warmup)
+        s3.synchronize()
+        t0 = time.perf_counter()
+        s3.vcycle(max(a.steps, 200))
+        s3.synchronize()
+        extra["nsplit3_vcycles_per_s"] = round(max(a.steps, 200) / (time.perf_counter() - t0), 1)
+        s3.close()
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline()
+        if cpu and "nsplit3_vcycles_per_s" in extra:
+            extra["nsplit3_speedup_vs_cpu"] = round(extra["nsplit3_vcycles_per_s"] / cpu["nsplit3_vcycles_per_s"], 1)
+    if rank == 0:
+        line = {
+            "metric": "multigrid V-cycles/sec + smoother HBM GB/s vs roofline, 8192-ele tri mesh",
+            "value": round(value, 3),
+            "unit": "V-cycles/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * elapsed / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "reference mesh untitled8192.msh, deterministic mode-9 IC/source (no random data)",
+            "config": {"workload": f"untitled8192.msh n_split={a.nsplit} multi_levels={a.levels} "
+                                   f"n_smooth={a.nsmooth} GS, 1 V-cycle per step",
+                       "fine_sub_elements": mesh.U * 4 ** a.nsplit, "levels": a.levels,
+                       "parallelism": f"dd{world}", "halo_mode": a.halo_mode},
+            "roofline": {"bound": "hbm", "kernel": "k_smooth (level-1 smoother call, n_smooth sweeps fused)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "alg_bytes_per_launch": bytes_per_launch, "ms_per_launch": round(ms_per_launch, 4)},
+            "cpu_baseline": ({k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")} if cpu else None),
+            "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    s.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+/*
+ * pamg.h -- C-ABI of the MI355X-native multigrid hot path (libpamg.so).
+ *
+ * Drop-in boundary for the multigrid smoother / residual / restriction /
+ * prolongation / halo loop of the reference's semi-structured DG solver
+ * (Amin-Nadimy/P-A_multigrids). The reference has no FFI of its own: the path
+ * is a set of internal (`contains`) subroutines of `Semi_implicit_iterative`
+ * reached by host association. Each entry point below names the reference
+ * routine it replaces (file:line in the reference tree). The Fortran host
+ * binds these through iso_c_binding (p-a_multigrids_amd/fortran/pamg_mod.F90);
+ * the Python tests / bench bind them through ctypes (p-a_multigrids_amd/pamg).
+ *
+ * Conventions
+ *  - plain pointers and sizes only; every entry returns int (0 = PAMG_OK,
+ *    < 0 = error, message via pamg_last_error); no C++ exception crosses.
+ *  - host field arrays use the reference's Fortran layout
+ *    tracer(l)%x(3, nsub_l, U), column-major, fp64 (Structures.F90:185-188);
+ *    nsub_l = 4**(n_split - l + 1) (transport_tri_semi.F90:180).
+ *  - levels are 1-based as in the reference; neighbour ids are 1-based and 0
+ *    marks a domain boundary (Structures.F90:143-170 Mesh%Neig/fNeig/Dir).
+ *  - device memory is owned by the handle; host copies happen only in
+ *    upload / set_state / get_state / get_overlap, never per sweep.
+ *  - calls are ordered on the handle's HIP stream; getters synchronise.
+ */
+#ifndef PAMG_H
+#define PAMG_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PAMG_OK 0
+#define PAMG_ERR_ARG (-1)
+#define PAMG_ERR_HIP (-2)
+#define PAMG_ERR_IO (-3)
+#define PAMG_ERR_STATE (-4)
+#define PAMG_ERR_COMM (-5)
+#define PAMG_ERR_NODEV (-6)
+
+/* field selectors for pamg_set_state / pamg_get_state (Structures.F90:185-188) */
+#define PAMG_TNEW 0        /* tracer(l)%tnew */
+#define PAMG_TOLD 1        /* tracer(l)%told */
+#define PAMG_RHS 2         /* tracer(l)%RHS */
+#define PAMG_RESIDUAL 3    /* tracer(l)%residuale */
+#define PAMG_TNEW_NONLIN 4 /* tnew_nonlin (transport_tri_semi.F90:85), shape of its current level */
+
+/* timed kernel classes (pamg_timing_*) */
+#define PAMG_K_SMOOTH_L1 0
+#define PAMG_K_SMOOTH 1
+#define PAMG_K_RESIDUAL 2
+#define PAMG_K_RESTRICT 3
+#define PAMG_K_PROLONG 4
+#define PAMG_K_RHS 5
+#define PAMG_K_HALO 6
+#define PAMG_K_SWEEP_BENCH 7
+#define PAMG_K_COUNT 8
+
+typedef struct pamg_handle pamg_handle;
+typedef struct pamg_mesh pamg_mesh;
+
+typedef struct {
+    int n_split;      /* transport_tri_semi.F90:118 */
+    int multi_levels; /* main.F90:46-47 (multi_levels <= n_split, :120-123) */
+    int n_smooth;     /* sweeps per smoother call, main.F90:46-47 */
+    int n_coarse;     /* smoother calls on the coarsest level, :351 (15) */
+    int solver;       /* 1 Jacobi, 2 Richardson, 3 Gauss-Seidel (:695-716) */
+    int device;       /* HIP device ordinal */
+    double dt;        /* CFL*dx, :133 */
+    double k;         /* diffusion coefficient, :136 */
+    double omega;     /* relaxation, :140 */
+    double theta;     /* time weighting, :117 (only 1.0 is accepted) */
+    int halo_mode;    /* 0: halo written once per smoother call (state-identical),
+                         1: one launch per sweep, halo at every sweep (reference timing) */
+    int reserved[7];
+} pamg_params;
+
+/* mode-9 defaults of the reference (main.F90:46-47, transport_tri_semi.F90:117-140) */
+void pamg_default_params(pamg_params *p);
+int pamg_version(void);
+
+/* ---- mesh ingest: replaces ReadMSH + CheckNeig + getNeigDataMesh
+ *      (Msh2Tri.F90:132-334, 776-963, 454-548) with an O(N) edge hash ---- */
+int pamg_msh_read(const char *path, pamg_mesh **m);
+/* structured strip of nx*ny*2 triangles on [0,lx]x[0,ly] (synthetic scaling meshes) */
+int pamg_msh_strip(int nx, int ny, double lx, double ly, pamg_mesh **m);
+int pamg_msh_size(const pamg_mesh *m, int *U);
+/* X(2,3,U) fp64, region(U), Neig/fNeig/Dir(3,U) */
+int pamg_msh_get(const pamg_mesh *m, double *X, int *region, int *neig, int *fneig, int *dir);
+void pamg_msh_free(pamg_mesh *m);
+
+/* ---- handle ---- */
+int pamg_create(const pamg_params *p, pamg_handle **h);
+/* mesh + topology; runs the setup of transport_tri_semi.F90:178-288 on the
+ * device side (per-level stencils, numbering tables, halo plan, initial
+ * condition tnew := 0, region 4 := 1 at level 1, :237-252) */
+int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, const int *neig,
+                     const int *fneig, const int *dir);
+int pamg_nsub(pamg_handle *h, int level);
+int pamg_set_state(pamg_handle *h, int level, int what, const double *host);
+int pamg_get_state(pamg_handle *h, int level, int what, double *host);
+/* halo buffers meshList(:)%t_overlap / t_overlap_old as (2**n_split*3, 3, U) */
+int pamg_get_overlap(pamg_handle *h, double *t_overlap, double *t_overlap_old);
+int pamg_tnn_level(pamg_handle *h);
+
+/* ---- the hot path, one entry per reference call site ---- */
+/* :316-317 told := tnew, tnew_nonlin := tnew, plus level-1 RHS (get_RHS :452-464) */
+int pamg_begin_timestep(pamg_handle *h);
+/* :325-327, :346-348, :365-367 tnew_nonlin := tracer(l)%tnew */
+int pamg_copy_to_nonlin(pamg_handle *h, int level);
+/* n_calls consecutive `call smoother` (:331, :352, :376; body :543-722) */
+int pamg_smoother(pamg_handle *h, int level, int n_calls);
+/* n_sweeps single sweeps with the smoother's tnew / tnew_nonlin semantics (one
+ * "iteration" of the LinearSolvers.F90 GSsolver_Mesh* facade, :632-848) */
+int pamg_sweep(pamg_handle *h, int level, int n_sweeps);
+/* `call restrictor` splitting.F90:10-32 (no-op on the coarsest level) */
+int pamg_restrictor(pamg_handle *h, int level);
+/* `call get_residual` :725-873 */
+int pamg_get_residual(pamg_handle *h, int level);
+/* `call prolongator` splitting.F90:38-91 */
+int pamg_prolongator(pamg_handle *h, int level);
+/* n passes of the n_multigrid loop body :319-379 */
+int pamg_vcycle(pamg_handle *h, int n);
+/* the time loop :299-381 */
+int pamg_run(pamg_handle *h, int ntime, int n_multigrid);
+int pamg_synchronize(pamg_handle *h);
+
+/* ---- measurement ---- */
+/* enable HIP-event timing of the kernel classes in `mask` (bit PAMG_K_*) */
+int pamg_timing_enable(pamg_handle *h, unsigned mask);
+int pamg_timing_reset(pamg_handle *h);
+/* total ms, launches and algorithmic HBM bytes of kernel class `kid` since reset */
+int pamg_timing_read(pamg_handle *h, int kid, double *ms_total, long *launches, double *bytes_total);
+/* the unfused level-1 roofline kernel: `sweeps` launches of one smoother sweep
+ * (assembled=0: per-un_ele stencils; assembled=1: per-sub-element 3x3 blocks,
+ * block-CSR with one block per block-row, the matrices.F90 format) */
+int pamg_sweep_bench(pamg_handle *h, int sweeps, int assembled, double *ms_avg, double *bytes_per_launch);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---- */
+int pamg_comm_unique_id(char out[128]);
+/* owner[U] = rank (0-based) owning each un_ele; call before pamg_upload_mesh.
+ * nranks == 1 needs no id. The halo (update_overlaps) towards un_eles owned by
+ * other ranks is exchanged with grouped ncclSend/ncclRecv after every halo write. */
+int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int U, const int *owner);
+int pamg_owned_count(pamg_handle *h);
+/* single-process exchange of the packed halo of `level` between n partition
+ * handles (created with pamg_comm_init(id = NULL)): the same send/recv
+ * segments RCCL would carry, copied device to device, then unpacked */
+int pamg_halo_loopback(pamg_handle *const *hs, int n, int level);
+
+/* ---- host-only halo plan (tooling / CPU tests of the partitioned exchange) ---- */
+typedef struct pamg_plan pamg_plan;
+int pamg_plan_build(int U, const double *X, const int *neig, const int *fneig, const int *dir, int n_split,
+                    int level, int nranks, int rank, const int *owner, pamg_plan **out);
+/* sizes[6] = n_owned, n_local, n_bc, n_remote, n_recv, n_peers */
+int pamg_plan_sizes(const pamg_plan *p, int *sizes);
+/* any pointer may be NULL; bc_dst / bc_val hold (a, b) pairs; offsets have n_peers + 1 entries */
+int pamg_plan_get(const pamg_plan *p, int *owned, int *local_src, int *local_dst, int *bc_dst, double *bc_val,
+                  int *remote_src, int *peers, int *send_off, int *recv_dst, int *recv_off);
+void pamg_plan_free(pamg_plan *p);
+
+int pamg_last_error(pamg_handle *h, char *buf, int len);
+int pamg_destroy(pamg_handle *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PAMG_H */

@@ -1,0 +1,633 @@
+// C-ABI of libpamg: handle, setup, state transfer, the hot-path entry points
+// (one per reference call site) and the V-cycle driver of
+// transport_tri_semi.F90:299-381.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pamg_internal.h"
+
+using namespace pamg;
+
+namespace pamg {
+struct Comm {
+    ncclComm_t nccl = nullptr;
+};
+}  // namespace pamg
+
+#define HIPCHK(h, expr)                                                                   \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            (h)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                 \
+            return PAMG_ERR_HIP;                                                          \
+        }                                                                                 \
+    } while (0)
+
+#define NCCLCHK(h, expr)                                                                  \
+    do {                                                                                  \
+        ncclResult_t r_ = (expr);                                                         \
+        if (r_ != ncclSuccess) {                                                          \
+            (h)->err = std::string(#expr) + ": " + ncclGetErrorString(r_);                \
+            return PAMG_ERR_COMM;                                                         \
+        }                                                                                 \
+    } while (0)
+
+#define CHK(expr)                    \
+    do {                             \
+        int rc_ = (expr);            \
+        if (rc_ != PAMG_OK) return rc_; \
+    } while (0)
+
+namespace {
+
+template <class T>
+int dev_alloc(pamg_handle *h, T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return PAMG_OK;
+    HIPCHK(h, hipMalloc((void **)p, count * sizeof(T)));
+    return PAMG_OK;
+}
+
+template <class T>
+int dev_upload(pamg_handle *h, T **p, const std::vector<T> &v) {
+    CHK(dev_alloc(h, p, v.size()));
+    if (!v.empty()) HIPCHK(h, hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return PAMG_OK;
+}
+
+void dev_free(void *p) {
+    if (p) (void)hipFree(p);
+}
+
+int check_level(pamg_handle *h, int l) {
+    if (!h->mesh_ready) { h->err = "mesh not uploaded"; return PAMG_ERR_STATE; }
+    if (l < 1 || l > h->p.multi_levels) { h->err = "level out of range"; return PAMG_ERR_ARG; }
+    return PAMG_OK;
+}
+
+// ---- timing -------------------------------------------------------------
+hipEvent_t take_event(pamg_handle *h) {
+    auto &pool = h->timing.pool;
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct Span {
+    pamg_handle *h; int kid; double bytes; hipEvent_t a = nullptr;
+    Span(pamg_handle *h_, int kid_, double bytes_) : h(h_), kid(kid_), bytes(bytes_) {
+        if (h->timing.mask & (1u << kid)) { a = take_event(h); (void)hipEventRecord(a, h->stream); }
+    }
+    ~Span() {
+        if (!a) return;
+        hipEvent_t b = take_event(h);
+        (void)hipEventRecord(b, h->stream);
+        h->timing.pending.push_back(Timing::Rec{kid, a, b, bytes});
+    }
+};
+
+int drain_timing(pamg_handle *h) {
+    auto &T = h->timing;
+    if (T.pending.empty()) return PAMG_OK;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (auto &r : T.pending) {
+        float ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&ms, r.a, r.b));
+        T.ms[r.kid] += ms;
+        T.count[r.kid] += 1;
+        T.bytes[r.kid] += r.bytes;
+        T.pool.push_back(r.a);
+        T.pool.push_back(r.b);
+    }
+    T.pending.clear();
+    return PAMG_OK;
+}
+
+// ---- scratch ------------------------------------------------------------
+int ensure_scratch(pamg_handle *h, size_t bytes) {
+    if (h->scratch_bytes >= bytes) return PAMG_OK;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    dev_free(h->scratch);
+    h->scratch = nullptr;
+    h->scratch_bytes = 0;
+    HIPCHK(h, hipMalloc((void **)&h->scratch, bytes));
+    h->scratch_bytes = bytes;
+    return PAMG_OK;
+}
+
+double *field_ptr(pamg_handle *h, int l, int what) {
+    Level &L = h->lv[l];
+    switch (what) {
+        case PAMG_TNEW: return L.T;
+        case PAMG_TOLD: return L.TOLD;
+        case PAMG_RHS: return L.RHS;
+        case PAMG_RESIDUAL: return L.RES;
+        case PAMG_TNEW_NONLIN: return L.TNN;
+    }
+    return nullptr;
+}
+
+// ---- halo exchange --------------------------------------------------------
+int halo(pamg_handle *h, int l) {
+    Level &L = h->lv[l];
+    const HaloPlan &P = L.halo;
+    {
+        Span sp(h, PAMG_K_HALO, (double)(P.local.size() + P.remote.size()) * 72.0 + P.bc.size() * 48.0);
+        HIPCHK(h, launch_halo(h->stream, L, h->tov, h->tovo));
+    }
+    if (h->comm && !P.peers.empty()) {
+        NCCLCHK(h, ncclGroupStart());
+        for (size_t q = 0; q < P.peers.size(); ++q) {
+            const int peer = P.peers[q];
+            const size_t ns = (size_t)(P.send_peer_off[q + 1] - P.send_peer_off[q]);
+            const size_t nr = (size_t)(P.recv_peer_off[q + 1] - P.recv_peer_off[q]);
+            if (ns) NCCLCHK(h, ncclSend(P.d_send + 6 * (size_t)P.send_peer_off[q], 6 * ns, ncclDouble, peer,
+                                        h->comm->nccl, h->stream));
+            if (nr) NCCLCHK(h, ncclRecv(P.d_recv + 6 * (size_t)P.recv_peer_off[q], 6 * nr, ncclDouble, peer,
+                                        h->comm->nccl, h->stream));
+        }
+        NCCLCHK(h, ncclGroupEnd());
+        HIPCHK(h, launch_halo_unpack(h->stream, L, h->tov, h->tovo));
+    }
+    return PAMG_OK;
+}
+
+// `sweeps` sweeps on level l reading the iterate from T (src_is_T: the leg
+// copy tnew_nonlin := tnew is folded into the launch) or from TNN.
+int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
+    Level &L = h->lv[l];
+    h->tnn_level = l;
+    if (sweeps <= 0) {
+        if (src_is_T) HIPCHK(h, hipMemcpyAsync(L.TNN, L.T, 3 * L.pitch * sizeof(double), hipMemcpyDeviceToDevice,
+                                               h->stream));
+        return PAMG_OK;
+    }
+    const double rdt = 1 / h->p.dt;
+    const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
+    const double bytes = 96.0 * (double)L.N + 168.0 * h->U;
+    if (h->p.halo_mode == 1) {
+        for (int s = 0; s < sweeps; ++s) {
+            {
+                Span sp(h, kid, bytes);
+                HIPCHK(h, launch_smooth(h->stream, L, (s == 0 && src_is_T) ? L.T : L.TNN, 1, h->p.solver, rdt,
+                                        h->p.omega));
+            }
+            CHK(halo(h, l));
+        }
+        return PAMG_OK;
+    }
+    {
+        Span sp(h, kid, bytes);
+        HIPCHK(h, launch_smooth(h->stream, L, src_is_T ? L.T : L.TNN, sweeps, h->p.solver, rdt, h->p.omega));
+    }
+    return halo(h, l);
+}
+
+int rhs_level1(pamg_handle *h, bool start_of_step) {
+    Level &L = h->lv[1];
+    Span sp(h, PAMG_K_RHS, 96.0 * (double)L.N);
+    HIPCHK(h, launch_rhs(h->stream, L, h->geo1, 1 / h->p.dt, h->p.k, start_of_step));
+    return PAMG_OK;
+}
+
+int residual(pamg_handle *h, int l) {
+    Level &L = h->lv[l];
+    if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, false));   // get_RHS inside get_residual (:865-867)
+    Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)L.N + 168.0 * h->U);
+    HIPCHK(h, launch_residual(h->stream, L, 1 / h->p.dt));
+    return PAMG_OK;
+}
+
+int restrict_(pamg_handle *h, int l) {
+    if (l >= h->p.multi_levels) return PAMG_OK;   // splitting.F90:18
+    Span sp(h, PAMG_K_RESTRICT, 96.0 * (double)h->lv[l + 1].N);
+    HIPCHK(h, launch_restrict(h->stream, h->lv[l], h->lv[l + 1], h->U));
+    return PAMG_OK;
+}
+
+int prolong(pamg_handle *h, int l, bool fused_copy) {
+    if (l >= h->p.multi_levels) { h->err = "prolongator needs a coarser level"; return PAMG_ERR_ARG; }
+    if (fused_copy) h->tnn_level = l;
+    Span sp(h, PAMG_K_PROLONG, (fused_copy ? 312.0 : 216.0) * (double)h->lv[l + 1].N);
+    HIPCHK(h, launch_prolong(h->stream, h->lv[l], h->lv[l + 1], fused_copy));
+    return PAMG_OK;
+}
+
+int vcycle_once(pamg_handle *h) {
+    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    for (int l = 1; l <= L; ++l) {           // :323-340
+        CHK(smooth(h, l, true, ns));
+        CHK(restrict_(h, l));
+        CHK(residual(h, l));
+    }
+    CHK(smooth(h, L, true, ns * h->p.n_coarse));   // :344-359
+    for (int l = L - 1; l >= 1; --l) {             // :363-378
+        CHK(prolong(h, l, true));
+        CHK(smooth(h, l, false, ns));
+    }
+    return PAMG_OK;
+}
+
+void free_levels(pamg_handle *h) {
+    for (int l = 1; l <= kMaxLevels; ++l) {
+        Level &L = h->lv[l];
+        dev_free(L.T); dev_free(L.stc); dev_free(L.subinfo); dev_free(L.children); dev_free(L.blocks);
+        dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
+        dev_free(L.halo.d_send); dev_free(L.halo.d_recv);
+        L = Level();
+    }
+    dev_free(h->geo1); dev_free(h->tov); dev_free(h->tovo);
+    h->geo1 = h->tov = h->tovo = nullptr;
+    h->mesh_ready = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pamg_version(void) { return 100; }
+
+void pamg_default_params(pamg_params *p) {
+    std::memset(p, 0, sizeof *p);
+    p->n_split = 1;          // :118
+    p->multi_levels = 1;     // main.F90:46-47
+    p->n_smooth = 4;
+    p->n_coarse = 15;        // :351
+    p->solver = 3;
+    p->device = 0;
+    p->dt = 1. * 0.0000125;  // CFL*dx, :133
+    p->k = 1.;               // :136
+    p->omega = 0.8;          // :140
+    p->theta = 1.;           // :117
+    p->halo_mode = 0;
+}
+
+int pamg_create(const pamg_params *p, pamg_handle **out) {
+    if (!p || !out) return PAMG_ERR_ARG;
+    *out = nullptr;
+    if (p->multi_levels < 1 || p->multi_levels > p->n_split || p->n_split > kMaxLevels || p->n_split < 1 ||
+        p->n_smooth < 0 || p->n_coarse < 0 || (p->solver < 1 || p->solver > 3) || !(p->dt > 0) ||
+        p->theta != 1.0 || (p->halo_mode != 0 && p->halo_mode != 1))
+        return PAMG_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PAMG_ERR_NODEV;
+    if (p->device < 0 || p->device >= ndev) return PAMG_ERR_NODEV;
+    auto *h = new pamg_handle;
+    h->p = *p;
+    h->device = p->device;
+    if (hipSetDevice(h->device) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return PAMG_ERR_HIP;
+    }
+    *out = h;
+    return PAMG_OK;
+}
+
+int pamg_comm_unique_id(char out[128]) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return PAMG_ERR_COMM;
+    static_assert(sizeof(id) == 128, "ncclUniqueId size");
+    std::memcpy(out, &id, 128);
+    return PAMG_OK;
+}
+
+int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int U, const int *owner) {
+    if (!h || nranks < 1 || rank < 0 || rank >= nranks || !owner || U < 1) return PAMG_ERR_ARG;
+    if (h->mesh_ready) { h->err = "pamg_comm_init must precede pamg_upload_mesh"; return PAMG_ERR_STATE; }
+    h->nranks = nranks;
+    h->rank = rank;
+    h->owner.assign(owner, owner + U);
+    if (nranks > 1 && id) {   // id == NULL: detached partition (pamg_halo_loopback exchanges)
+        HIPCHK(h, hipSetDevice(h->device));
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, 128);
+        h->comm = new Comm;
+        NCCLCHK(h, ncclCommInitRank(&h->comm->nccl, nranks, uid, rank));
+    }
+    return PAMG_OK;
+}
+
+int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, const int *neig, const int *fneig,
+                     const int *dir) {
+    if (!h || U < 1 || !X || !region || !neig || !fneig || !dir) return PAMG_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    free_levels(h);
+    h->U_global = U;
+    h->owned.clear();
+    if (!h->owner.empty() && (int)h->owner.size() != U) {
+        h->err = "owner map size differs from the uploaded mesh";
+        return PAMG_ERR_ARG;
+    }
+    if (!h->owner.empty()) {
+        for (int g = 0; g < U; ++g) {
+            if (h->owner[g] < 0 || h->owner[g] >= h->nranks) { h->err = "owner out of range"; return PAMG_ERR_ARG; }
+            if (h->owner[g] == h->rank) h->owned.push_back(g);
+        }
+    } else {
+        for (int g = 0; g < U; ++g) h->owned.push_back(g);
+    }
+    h->U = (int)h->owned.size();
+    for (int g = 0; g < U; ++g)
+        for (int f = 0; f < 3; ++f) {
+            const int n = neig[3 * g + f];
+            if (n < 0 || n > U || (n && (fneig[3 * g + f] < 1 || fneig[3 * g + f] > 3))) {
+                h->err = "inconsistent neighbour table at un_ele " + std::to_string(g + 1);
+                return PAMG_ERR_ARG;
+            }
+        }
+    const int S = h->p.n_split, Lc = h->p.multi_levels, Ul = h->U;
+    h->slots = (1 << S) * 3;
+    CHK(dev_alloc(h, &h->tov, (size_t)h->slots * 3 * std::max(Ul, 1)));
+    CHK(dev_alloc(h, &h->tovo, (size_t)h->slots * 3 * std::max(Ul, 1)));
+    HIPCHK(h, hipMemsetAsync(h->tov, 0, (size_t)h->slots * 3 * std::max(Ul, 1) * sizeof(double), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->tovo, 0, (size_t)h->slots * 3 * std::max(Ul, 1) * sizeof(double), h->stream));
+    // level-1 geometry for the source term
+    {
+        std::vector<double> geo((size_t)std::max(Ul, 1) * kGeoStride, 0.0);
+        const double pw = (double)(1 << S);
+        for (int q = 0; q < Ul; ++q) {
+            const double *x = X + 6 * (size_t)h->owned[q];
+            double *g = &geo[(size_t)q * kGeoStride];
+            g[0] = x[4]; g[1] = x[5];
+            g[2] = (x[0] - x[4]) / pw; g[3] = (x[1] - x[5]) / pw;
+            g[4] = (x[2] - x[4]) / pw; g[5] = (x[3] - x[5]) / pw;
+        }
+        CHK(dev_upload(h, &h->geo1, geo));
+    }
+    for (int l = 1; l <= Lc; ++l) {
+        Level &L = h->lv[l];
+        L.isplit = S - l + 1;
+        L.nsub = 1 << (2 * L.isplit);
+        L.N = (int64_t)L.nsub * Ul;
+        L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64);
+        double *base = nullptr;
+        CHK(dev_alloc(h, &base, 15 * (size_t)L.pitch));
+        HIPCHK(h, hipMemsetAsync(base, 0, 15 * (size_t)L.pitch * sizeof(double), h->stream));
+        L.T = base; L.TNN = base + 3 * L.pitch; L.RHS = base + 6 * L.pitch; L.RES = base + 9 * L.pitch;
+        L.TOLD = base + 12 * L.pitch;
+        std::vector<double> stc((size_t)std::max(Ul, 1) * kStcStride, 0.0);
+        for (int q = 0; q < Ul; ++q)
+            level_stencil(X + 6 * (size_t)h->owned[q], L.isplit, h->p.k, h->p.dt, h->p.omega,
+                          &stc[(size_t)q * kStcStride]);
+        CHK(dev_upload(h, &L.stc, stc));
+        std::vector<int2> sub(L.nsub);
+        for (int e = 1; e <= L.nsub; ++e) {
+            int irow, ipos, o;
+            get_str_info(L.isplit, e, &irow, &ipos, &o);
+            sub[e - 1] = make_int2(irow, ipos);
+        }
+        CHK(dev_upload(h, &L.subinfo, sub));
+        if (l < Lc) {
+            std::vector<int4> ch(L.nsub / 4);
+            for (int c = 1; c <= L.nsub / 4; ++c) {
+                int fin[4];
+                element_conversion(fin, c, L.isplit - 1);
+                for (int q = 0; q < 4; ++q)
+                    if (fin[q] < 1 || fin[q] > L.nsub) { h->err = "element_conversion out of range"; return PAMG_ERR_STATE; }
+                ch[c - 1] = make_int4(fin[0] - 1, fin[1] - 1, fin[2] - 1, fin[3] - 1);
+            }
+            CHK(dev_upload(h, &L.children, ch));
+        }
+        CHK(build_halo(h, l, X, neig, fneig, dir));
+        HaloPlan &P = L.halo;
+        CHK(dev_upload(h, &P.d_local, P.local));
+        CHK(dev_upload(h, &P.d_bc, P.bc));
+        CHK(dev_upload(h, &P.d_remote, P.remote));
+        CHK(dev_upload(h, &P.d_recv_dst, P.recv_dst));
+        CHK(dev_alloc(h, &P.d_send, 6 * P.remote.size()));
+        CHK(dev_alloc(h, &P.d_recv, 6 * P.recv_dst.size()));
+    }
+    // initial condition (:237-252): tnew = 0, region 4 => 1 on level 1
+    {
+        Level &L1 = h->lv[1];
+        bool any = false;
+        for (int q = 0; q < Ul; ++q) any |= region[h->owned[q]] == 4;
+        if (any) {
+            std::vector<double> t(3 * (size_t)L1.pitch, 0.0);
+            for (int q = 0; q < Ul; ++q)
+                if (region[h->owned[q]] == 4)
+                    for (int c = 0; c < 3; ++c)
+                        for (int e = 0; e < L1.nsub; ++e) t[c * L1.pitch + (size_t)q * L1.nsub + e] = 1.0;
+            HIPCHK(h, hipMemcpy(L1.T, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+        }
+        HIPCHK(h, hipMemcpyAsync(L1.TNN, L1.T, 3 * L1.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+        h->tnn_level = 1;
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->mesh_ready = true;
+    return PAMG_OK;
+}
+
+int pamg_owned_count(pamg_handle *h) { return h ? h->U : PAMG_ERR_ARG; }
+
+int pamg_nsub(pamg_handle *h, int level) {
+    if (!h) return PAMG_ERR_ARG;
+    CHK(check_level(h, level));
+    return h->lv[level].nsub;
+}
+
+int pamg_tnn_level(pamg_handle *h) { return h ? h->tnn_level : PAMG_ERR_ARG; }
+
+int pamg_set_state(pamg_handle *h, int level, int what, const double *host) {
+    if (!h || !host) return PAMG_ERR_ARG;
+    if (what == PAMG_TNEW_NONLIN) { CHK(check_level(h, level)); h->tnn_level = level; }
+    CHK(check_level(h, level));
+    Level &L = h->lv[level];
+    double *dst = field_ptr(h, level, what);
+    if (!dst) return PAMG_ERR_ARG;
+    CHK(ensure_scratch(h, 3 * (size_t)L.N * sizeof(double)));
+    HIPCHK(h, hipMemcpyAsync(h->scratch, host, 3 * (size_t)L.N * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, launch_to_soa(h->stream, h->scratch, dst, L.N, L.pitch));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PAMG_OK;
+}
+
+int pamg_get_state(pamg_handle *h, int level, int what, double *host) {
+    if (!h || !host) return PAMG_ERR_ARG;
+    if (what == PAMG_TNEW_NONLIN) level = h->tnn_level;
+    CHK(check_level(h, level));
+    Level &L = h->lv[level];
+    double *src = field_ptr(h, level, what);
+    if (!src) return PAMG_ERR_ARG;
+    CHK(ensure_scratch(h, 3 * (size_t)L.N * sizeof(double)));
+    HIPCHK(h, launch_to_aos(h->stream, src, h->scratch, L.N, L.pitch));
+    HIPCHK(h, hipMemcpyAsync(host, h->scratch, 3 * (size_t)L.N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PAMG_OK;
+}
+
+int pamg_get_overlap(pamg_handle *h, double *tov, double *tovo) {
+    if (!h || !h->mesh_ready) return PAMG_ERR_STATE;
+    const size_t n = (size_t)h->slots * 3 * h->U * sizeof(double);
+    if (tov) HIPCHK(h, hipMemcpyAsync(tov, h->tov, n, hipMemcpyDeviceToHost, h->stream));
+    if (tovo) HIPCHK(h, hipMemcpyAsync(tovo, h->tovo, n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PAMG_OK;
+}
+
+int pamg_begin_timestep(pamg_handle *h) {
+    if (!h) return PAMG_ERR_ARG;
+    CHK(check_level(h, 1));
+    h->tnn_level = 1;
+    if (h->p.solver == 2) {   // solve_Richardson never calls get_RHS inside the smoother
+        Level &L = h->lv[1];
+        HIPCHK(h, hipMemcpyAsync(L.TOLD, L.T, 3 * L.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(L.TNN, L.T, 3 * L.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+        return PAMG_OK;
+    }
+    return rhs_level1(h, true);
+}
+
+int pamg_copy_to_nonlin(pamg_handle *h, int level) {
+    if (!h) return PAMG_ERR_ARG;
+    CHK(check_level(h, level));
+    Level &L = h->lv[level];
+    HIPCHK(h, hipMemcpyAsync(L.TNN, L.T, 3 * L.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    h->tnn_level = level;
+    return PAMG_OK;
+}
+
+int pamg_smoother(pamg_handle *h, int level, int n_calls) {
+    if (!h || n_calls < 0) return PAMG_ERR_ARG;
+    CHK(check_level(h, level));
+    if (h->tnn_level != level) {
+        h->err = "smoother: tnew_nonlin holds another level (call pamg_copy_to_nonlin first)";
+        return PAMG_ERR_STATE;
+    }
+    return smooth(h, level, false, h->p.n_smooth * n_calls);
+}
+
+int pamg_sweep(pamg_handle *h, int level, int n_sweeps) {
+    if (!h || n_sweeps < 0) return PAMG_ERR_ARG;
+    CHK(check_level(h, level));
+    if (h->tnn_level != level) {
+        h->err = "sweep: tnew_nonlin holds another level (call pamg_copy_to_nonlin first)";
+        return PAMG_ERR_STATE;
+    }
+    return smooth(h, level, false, n_sweeps);
+}
+
+int pamg_restrictor(pamg_handle *h, int level) {
+    if (!h) return PAMG_ERR_ARG;
+    CHK(check_level(h, level));
+    return restrict_(h, level);
+}
+
+int pamg_get_residual(pamg_handle *h, int level) {
+    if (!h) return PAMG_ERR_ARG;
+    CHK(check_level(h, level));
+    return residual(h, level);
+}
+
+int pamg_prolongator(pamg_handle *h, int level) {
+    if (!h) return PAMG_ERR_ARG;
+    CHK(check_level(h, level));
+    return prolong(h, level, false);
+}
+
+int pamg_vcycle(pamg_handle *h, int n) {
+    if (!h || n < 0) return PAMG_ERR_ARG;
+    CHK(check_level(h, 1));
+    for (int c = 0; c < n; ++c) CHK(vcycle_once(h));
+    return PAMG_OK;
+}
+
+int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
+    if (!h || ntime < 0 || n_multigrid < 0) return PAMG_ERR_ARG;
+    for (int t = 0; t < ntime; ++t) {
+        CHK(pamg_begin_timestep(h));
+        CHK(pamg_vcycle(h, n_multigrid));
+    }
+    return PAMG_OK;
+}
+
+int pamg_synchronize(pamg_handle *h) {
+    if (!h) return PAMG_ERR_ARG;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PAMG_OK;
+}
+
+int pamg_timing_enable(pamg_handle *h, unsigned mask) {
+    if (!h) return PAMG_ERR_ARG;
+    h->timing.mask = mask;
+    return PAMG_OK;
+}
+
+int pamg_timing_reset(pamg_handle *h) {
+    if (!h) return PAMG_ERR_ARG;
+    CHK(drain_timing(h));
+    for (int k = 0; k < PAMG_K_COUNT; ++k) { h->timing.ms[k] = 0; h->timing.count[k] = 0; h->timing.bytes[k] = 0; }
+    return PAMG_OK;
+}
+
+int pamg_timing_read(pamg_handle *h, int kid, double *ms_total, long *launches, double *bytes_total) {
+    if (!h || kid < 0 || kid >= PAMG_K_COUNT) return PAMG_ERR_ARG;
+    CHK(drain_timing(h));
+    if (ms_total) *ms_total = h->timing.ms[kid];
+    if (launches) *launches = h->timing.count[kid];
+    if (bytes_total) *bytes_total = h->timing.bytes[kid];
+    return PAMG_OK;
+}
+
+int pamg_sweep_bench(pamg_handle *h, int sweeps, int assembled, double *ms_avg, double *bytes_per_launch) {
+    if (!h || sweeps < 1) return PAMG_ERR_ARG;
+    CHK(check_level(h, 1));
+    Level &L = h->lv[1];
+    const double rdt = 1 / h->p.dt;
+    CHK(ensure_scratch(h, 3 * (size_t)L.pitch * sizeof(double)));
+    if (assembled && !L.blocks) {
+        CHK(dev_alloc(h, &L.blocks, 12 * (size_t)L.pitch));
+        HIPCHK(h, launch_build_blocks(h->stream, L, rdt));
+    }
+    const double bytes = assembled ? 168.0 * (double)L.N : 72.0 * (double)L.N + 168.0 * h->U;
+    const unsigned saved = h->timing.mask;
+    CHK(drain_timing(h));
+    const double ms0 = h->timing.ms[PAMG_K_SWEEP_BENCH];
+    const long n0 = h->timing.count[PAMG_K_SWEEP_BENCH];
+    h->timing.mask |= 1u << PAMG_K_SWEEP_BENCH;
+    for (int s = 0; s < sweeps; ++s) {
+        Span sp(h, PAMG_K_SWEEP_BENCH, bytes);
+        if (assembled) HIPCHK(h, launch_sweep_assembled(h->stream, L, h->scratch, rdt));
+        else HIPCHK(h, launch_sweep_stencil(h->stream, L, h->scratch, rdt));
+    }
+    h->timing.mask = saved;
+    CHK(drain_timing(h));
+    const long n = h->timing.count[PAMG_K_SWEEP_BENCH] - n0;
+    if (ms_avg) *ms_avg = (h->timing.ms[PAMG_K_SWEEP_BENCH] - ms0) / std::max(1L, n);
+    if (bytes_per_launch) *bytes_per_launch = bytes;
+    return PAMG_OK;
+}
+
+int pamg_last_error(pamg_handle *h, char *buf, int len) {
+    if (!h || !buf || len <= 0) return PAMG_ERR_ARG;
+    std::strncpy(buf, h->err.c_str(), (size_t)len - 1);
+    buf[len - 1] = 0;
+    return PAMG_OK;
+}
+
+int pamg_destroy(pamg_handle *h) {
+    if (!h) return PAMG_OK;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    free_levels(h);
+    dev_free(h->scratch);
+    for (auto e : h->timing.pool) (void)hipEventDestroy(e);
+    for (auto &r : h->timing.pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    if (h->comm) {
+        if (h->comm->nccl) ncclCommDestroy(h->comm->nccl);
+        delete h->comm;
+    }
+    (void)hipStreamDestroy(h->stream);
+    delete h;
+    return PAMG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+// Internal structures of libpamg (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/pamg.h"
+
+namespace pamg {
+
+constexpr int kMaxLevels = 12;
+
+// Per (un_ele, level) operator record, fp64, 32 doubles = 256 B (two 128-B lines):
+// M (3x3 row-major) | Kd (3x3 row-major) | w = omega / D (3) | pad.
+// M and Kd are get_un_ele_mass_stiff_diffvol (ShapFun_unstruc.F90:304-335) reduced as
+// transport_tri_semi.F90:592-607; D is get_diagonal (:481-486).
+constexpr int kStcM = 0, kStcK = 9, kStcW = 18, kStcStride = 32;
+
+// Level-1 geometry record per un_ele (get_splitting, Msh2Tri.F90:69-107):
+// x3, y3, v1x, v1y, v2x, v2y (v = edge / 2**i_split), pad to 8 doubles.
+constexpr int kGeoStride = 8;
+
+struct HaloCopy {     // update_overlaps copy entry (splitting.F90:1256-1391)
+    int32_t src;      // global sub-element index (local numbering) on this rank
+    int32_t dst;      // element offset in t_overlap (local) or in the send buffer
+};
+struct HaloBC {       // boundary entry (splitting.F90:1243-1252, :1287-1295, :1345-1353)
+    int32_t dst_a, dst_b;
+    double val_a, val_b;
+};
+
+struct HaloPlan {
+    std::vector<HaloCopy> local;          // destination on this rank
+    std::vector<HaloBC> bc;
+    std::vector<HaloCopy> remote;         // dst = entry index in the packed send buffer
+    std::vector<int> send_peer_off;       // per peer: first entry in `remote` (size npeers+1)
+    std::vector<int> recv_dst;            // per received entry: t_overlap offset
+    std::vector<int> recv_peer_off;       // per peer: first entry in recv (size npeers+1)
+    std::vector<int> peers;               // peer ranks
+    // device copies
+    HaloCopy *d_local = nullptr, *d_remote = nullptr;
+    HaloBC *d_bc = nullptr;
+    int *d_recv_dst = nullptr;
+    double *d_send = nullptr, *d_recv = nullptr;   // 6 doubles per entry (tnew 3, told 3)
+};
+
+struct Level {
+    int isplit = 0;       // n_split - l + 1
+    int nsub = 0;         // 4**isplit
+    int64_t N = 0;        // nsub * U_local
+    int64_t pitch = 0;    // plane stride (>= N, multiple of 64)
+    // SoA planes [3][pitch]
+    double *T = nullptr, *TNN = nullptr, *RHS = nullptr, *RES = nullptr, *TOLD = nullptr;
+    double *stc = nullptr;            // U_local * kStcStride
+    int2 *subinfo = nullptr;          // nsub: (irow, ipos) of get_str_info
+    int4 *children = nullptr;         // nsub/4 (children of the next coarser level's sub-elements)
+    double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
+    HaloPlan halo;
+};
+
+struct Timing {
+    unsigned mask = 0;
+    struct Rec { int kid; hipEvent_t a, b; double bytes; };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    double ms[PAMG_K_COUNT] = {0};
+    long count[PAMG_K_COUNT] = {0};
+    double bytes[PAMG_K_COUNT] = {0};
+};
+
+struct Comm;  // pamg_comm.cpp
+
+}  // namespace pamg
+
+struct pamg_handle {
+    pamg_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int U = 0;                 // local un_ele count
+    int U_global = 0;
+    std::vector<int> owned;    // global ids (0-based) of local un_eles, ascending
+    pamg::Level lv[pamg::kMaxLevels + 1];   // 1-based
+    double *geo1 = nullptr;    // U * kGeoStride
+    double *tov = nullptr, *tovo = nullptr; // (slots, 3, U) t_overlap / t_overlap_old
+    int slots = 0;
+    int tnn_level = 1;
+    bool mesh_ready = false;
+    std::string err;
+    pamg::Timing timing;
+    // multi-GPU
+    int nranks = 1, rank = 0;
+    std::vector<int> owner;    // global owner map (empty = all local)
+    pamg::Comm *comm = nullptr;
+    double *scratch = nullptr; size_t scratch_bytes = 0;
+};
+
+// ---- setup (pamg_setup.cpp) ----
+namespace pamg {
+void get_str_info(int n_split, int ele, int *irow, int *ipos, int *orientation);
+void element_conversion(int fin[4], int coarse_ele, int i_split);
+void loc_surf_ele(int n, std::vector<int> &surf);
+void get_splitting(const double *un_x, int n_split, int str_ele, double str_x[3][2]);
+void level_stencil(const double *X, int i_split, double k, double dt, double omega, double *rec);
+int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const int *fneig, const int *dir);
+}  // namespace pamg
+
+// ---- kernels (pamg_kernels.hip) ----
+namespace pamg {
+hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int sweeps, int solver,
+                         double rdt, double omega);
+hipError_t launch_residual(hipStream_t s, const Level &L, double rdt);
+hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U);
+hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn);
+hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, bool start_of_step);
+hipError_t launch_halo(hipStream_t s, const Level &L, double *tov, double *tovo);
+hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
+hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
+hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch);
+hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt);
+hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
+hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
+}  // namespace pamg

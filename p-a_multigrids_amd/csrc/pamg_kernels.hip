@@ -1,0 +1,467 @@
+// HIP kernels of the multigrid hot path, written for CDNA4 (gfx950).
+//
+// Data layout in HBM: every level field is three fp64 planes [3][pitch]
+// (structure of arrays, sub-element index s = u * nsub + str_ele - 1), so a
+// wave64 moves 1 KiB per plane per instruction with 16-B (double2) lanes.
+// Each thread owns two consecutive sub-elements, which always belong to the
+// same un_ele (nsub = 4**i_split >= 4), so the 256-B operator record of that
+// un_ele is read once per thread and served from L1/L2 to all lanes of the
+// un_ele. The arithmetic is the reference's, in its order and without FMA
+// contraction (built with -ffp-contract=off): results are bit-identical to
+// the reference's fp64 build except where the device sine enters (level-1
+// source term).
+//
+// The operator is block diagonal (3x3 per sub-element): the
+// work per sub-element per sweep is ~30 flop on 72-168 B, far left of the
+// fp64 ridge, so these are HBM-bound streaming kernels; MFMA has no role.
+#include <hip/hip_runtime.h>
+
+#include "pamg_internal.h"
+
+namespace pamg {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ double2 ld2(const double *p) { return *reinterpret_cast<const double2 *>(p); }
+__device__ __forceinline__ void st2(double *p, double2 v) { *reinterpret_cast<double2 *>(p) = v; }
+
+struct Stc {
+    double M[9], K[9], w[3];
+};
+
+__device__ __forceinline__ void load_stc(const double *__restrict__ rec, Stc &S) {
+#pragma unroll
+    for (int q = 0; q < 9; q += 1) S.M[q] = rec[kStcM + q];
+#pragma unroll
+    for (int q = 0; q < 9; q += 1) S.K[q] = rec[kStcK + q];
+#pragma unroll
+    for (int q = 0; q < 3; q += 1) S.w[q] = rec[kStcW + q];
+}
+
+// get_A_x (transport_tri_semi.F90:412-448) with theta = 1 and the zero
+// advection / flux / surface terms folded: A_i = rdt*(M x)_i + (Kd x)_i.
+__device__ __forceinline__ void apply_A(const Stc &S, double rdt, const double x[3], double A[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double mx = S.M[3 * i] * x[0] + S.M[3 * i + 1] * x[1] + S.M[3 * i + 2] * x[2];
+        double kx = S.K[3 * i] * x[0] + S.K[3 * i + 1] * x[1] + S.K[3 * i + 2] * x[2];
+        A[i] = rdt * mx + kx;
+    }
+}
+
+// One sweep of solve_Gauss_Seidel / solve_Jacobi (:491-507), which coincide
+// for the block-diagonal operator: x_i += (omega / D_i) * (b_i - A_i).
+__device__ __forceinline__ void sweep(const Stc &S, double rdt, const double b[3], double x[3]) {
+    double A[3];
+    apply_A(S, rdt, x, A);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = x[i] + S.w[i] * (b[i] - A[i]);
+}
+
+// Fused smoother call(s): `sweeps` consecutive sweeps kept in registers.
+// `src` may alias T or TNN (each thread reads its own words before writing them).
+// Reference semantics (:548-550): each sweep starts with tnew := tnew_nonlin,
+// so after the call tnew holds the iterate before the last sweep and
+// tnew_nonlin the last one.
+template <bool RICHARDSON>
+__global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T, double *TNN,
+                                                   const double *__restrict__ RHS,
+                                                   const double *__restrict__ stc, int64_t pitch,
+                                                   int64_t npairs, int nsub_log2, int sweeps, double rdt,
+                                                   double omega) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npairs) return;
+    const int64_t s = 2 * p;
+    double2 xv[3], bv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        xv[c] = ld2(src + c * pitch + s);
+        bv[c] = ld2(RHS + c * pitch + s);
+    }
+    double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
+    const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
+    double p0[3] = {x0[0], x0[1], x0[2]}, p1[3] = {x1[0], x1[1], x1[2]};
+    if (RICHARDSON) {
+        // solve_Richardson (:511-518): mass/stiff/flux terms are reset to 0 (:585-612)
+        for (int it = 0; it < sweeps; ++it) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                p0[i] = x0[i]; p1[i] = x1[i];
+                x0[i] = x0[i] + omega * (b0[i] - (0.0 - 0.0 + 0.0));
+                x1[i] = x1[i] + omega * (b1[i] - (0.0 - 0.0 + 0.0));
+            }
+        }
+    } else {
+        Stc S;
+        load_stc(stc + (s >> nsub_log2) * kStcStride, S);
+        for (int it = 0; it < sweeps; ++it) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { p0[i] = x0[i]; p1[i] = x1[i]; }
+            sweep(S, rdt, b0, x0);
+            sweep(S, rdt, b1, x1);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        st2(T + c * pitch + s, make_double2(p0[c], p1[c]));
+        st2(TNN + c * pitch + s, make_double2(x0[c], x1[c]));
+    }
+}
+
+// get_residual (:725-873): residuale = A x - RHS (note the sign, :869).
+__global__ __launch_bounds__(kBlock) void k_residual(const double *__restrict__ T, const double *__restrict__ RHS,
+                                                     double *__restrict__ RES, const double *__restrict__ stc,
+                                                     int64_t pitch, int64_t npairs, int nsub_log2, double rdt) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npairs) return;
+    const int64_t s = 2 * p;
+    double2 xv[3], bv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        xv[c] = ld2(T + c * pitch + s);
+        bv[c] = ld2(RHS + c * pitch + s);
+    }
+    Stc S;
+    load_stc(stc + (s >> nsub_log2) * kStcStride, S);
+    const double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
+    double A0[3], A1[3];
+    apply_A(S, rdt, x0, A0);
+    apply_A(S, rdt, x1, A1);
+    const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) st2(RES + c * pitch + s, make_double2(A0[c] - b0[c], A1[c] - b1[c]));
+}
+
+// Level-1 right-hand side + time-step start (:316-317, :593, get_RHS :452-464):
+// told := tnew, tnew_nonlin := tnew, source s_j = -2k sin(x_j + y_j) at the
+// sub-element nodes (get_splitting coordinates), cascaded in place through M,
+// RHS_i = rdt (M told)_i + s'_i.
+__global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, double *TOLD,
+                                                double *__restrict__ TNN, double *__restrict__ RHS,
+                                                const double *__restrict__ stc, const double *__restrict__ geo,
+                                                const int2 *__restrict__ subinfo, int64_t pitch, int64_t N,
+                                                int nsub_log2, double rdt, double k, int start_of_step) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= N) return;
+    const int64_t u = s >> nsub_log2;
+    const int sub = (int)(s & ((1ll << nsub_log2) - 1));
+    double t[3];
+    if (start_of_step) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            t[c] = T[c * pitch + s];
+            TOLD[c * pitch + s] = t[c];
+            TNN[c * pitch + s] = t[c];
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) t[c] = TOLD[c * pitch + s];
+    }
+    const double *g = geo + u * kGeoStride;
+    const int2 ri = subinfo[sub];
+    const int irow = ri.x, ipos = ri.y;
+    double xl[3][2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        const double x3 = g[d], v1 = g[2 + d], v2 = g[4 + d];
+        if (ipos % 2 != 0) {
+            xl[2][d] = x3 + (double)(irow - 1) * v2 + (double)(ipos / 2) * v1;
+            xl[1][d] = x3 + (double)irow * v2 + (double)(ipos / 2) * v1;
+            xl[0][d] = x3 + (double)(irow - 1) * v2 + v1 * (double)(ipos / 2 + 1);
+        } else {
+            xl[0][d] = x3 + (double)irow * v2 + v1 * (double)(ipos / 2 - 1);
+            xl[1][d] = x3 + (double)(irow - 1) * v2 + v1 * (double)(ipos / 2);
+            xl[2][d] = x3 + (double)irow * v2 + v1 * (double)(ipos / 2);
+        }
+    }
+    const double *M = stc + u * kStcStride + kStcM;
+    double src[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) src[i] = -(2 * k * sin(xl[i][0] + xl[i][1]));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        src[i] = M[3 * i] * src[0] + M[3 * i + 1] * src[1] + M[3 * i + 2] * src[2];
+        const double mo = rdt * (M[3 * i] * t[0] + M[3 * i + 1] * t[1] + M[3 * i + 2] * t[2]);
+        RHS[i * pitch + s] = mo + src[i];
+    }
+}
+
+// restrictor (splitting.F90:10-32): RHS_{l+1}(:, c) = averages of the fine
+// residuals of children 3, 4, 1 (element_conversion, :97-140).
+__global__ __launch_bounds__(kBlock) void k_restrict(const double *__restrict__ RES, double *__restrict__ RHSc,
+                                                     const int4 *__restrict__ children, int64_t pitch_f,
+                                                     int64_t pitch_c, int64_t Nc, int nsubc_log2) {
+    const int64_t cg = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (cg >= Nc) return;
+    const int64_t u = cg >> nsubc_log2;
+    const int c = (int)(cg & ((1ll << nsubc_log2) - 1));
+    const int4 ch = children[c];
+    const int64_t base = u << (nsubc_log2 + 2);
+    const int64_t pick[3] = {base + ch.z, base + ch.w, base + ch.x};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int64_t f = pick[i];
+        RHSc[i * pitch_c + cg] = (RES[f] + RES[pitch_f + f] + RES[2 * pitch_f + f]) / 3.;
+    }
+}
+
+// prolongator (splitting.F90:38-91), fused with the preceding
+// tnew_nonlin := tnew copy of the prolongation leg (:365-367).
+__global__ __launch_bounds__(kBlock) void k_prolong(double *__restrict__ T, double *__restrict__ TNN,
+                                                    const double *__restrict__ Tc, const int4 *__restrict__ children,
+                                                    int64_t pitch_f, int64_t pitch_c, int64_t Nc, int nsubc_log2,
+                                                    int write_tnn) {
+    const int64_t cg = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (cg >= Nc) return;
+    const int64_t u = cg >> nsubc_log2;
+    const int c = (int)(cg & ((1ll << nsubc_log2) - 1));
+    const int4 ch = children[c];
+    const int64_t base = u << (nsubc_log2 + 2);
+    const int64_t fi[4] = {base + ch.x, base + ch.y, base + ch.z, base + ch.w};
+    const double y[3] = {Tc[cg], Tc[pitch_c + cg], Tc[2 * pitch_c + cg]};
+    double f[4][3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            f[q][i] = T[i * pitch_f + fi[q]];
+            if (write_tnn) TNN[i * pitch_f + fi[q]] = f[q][i];
+        }
+    f[0][0] = f[0][0] + 0.5 * y[2] + 0.5 * y[0];
+    f[0][1] = f[0][1] + 0.5 * y[1] + 0.5 * y[2];
+    f[0][2] = f[0][2] + y[2];
+    f[1][0] = f[1][0] + f[0][1];
+    f[1][1] = f[1][1] + f[0][0];
+    f[1][2] = f[1][2] + 0.5 * y[0] + 0.5 * y[1];
+    f[2][0] = f[2][0] + y[0];
+    f[2][1] = f[2][1] + f[1][2];
+    f[2][2] = f[2][2] + f[1][1];
+    f[3][0] = f[3][0] + f[1][2];
+    f[3][1] = f[3][1] + y[1];
+    f[3][2] = f[3][2] + f[1][0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) T[i * pitch_f + fi[q]] = f[q][i];
+}
+
+// update_overlaps (splitting.F90:1210-1397): boundary writes and neighbour
+// copies of (tnew, told) into t_overlap / t_overlap_old (one writer per word),
+// plus the packed send buffer for neighbours owned by other ranks.
+__global__ __launch_bounds__(kBlock) void k_halo(const double *__restrict__ T, const double *__restrict__ TOLD,
+                                                 int64_t pitch, double *__restrict__ tov, double *__restrict__ tovo,
+                                                 const HaloCopy *__restrict__ loc, int nloc,
+                                                 const HaloBC *__restrict__ bc, int nbc,
+                                                 const HaloCopy *__restrict__ rem, int nrem,
+                                                 double *__restrict__ send) {
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    if (e < nloc) {
+        const HaloCopy h = loc[e];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            tov[h.dst + q] = T[q * pitch + h.src];
+            tovo[h.dst + q] = TOLD[q * pitch + h.src];
+        }
+    } else if (e < nloc + nbc) {
+        const HaloBC b = bc[e - nloc];
+        tov[b.dst_a] = b.val_a;
+        tov[b.dst_b] = b.val_b;
+        tovo[b.dst_a] = b.val_a;
+        tovo[b.dst_b] = b.val_b;
+    } else if (e < nloc + nbc + nrem) {
+        const HaloCopy h = rem[e - nloc - nbc];
+        double *o = send + 6 * (int64_t)h.dst;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            o[q] = T[q * pitch + h.src];
+            o[3 + q] = TOLD[q * pitch + h.src];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_halo_unpack(const double *__restrict__ recv, const int *__restrict__ dst,
+                                                        int n, double *__restrict__ tov, double *__restrict__ tovo) {
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const int d = dst[e];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        tov[d + q] = recv[6 * (int64_t)e + q];
+        tovo[d + q] = recv[6 * (int64_t)e + 3 + q];
+    }
+}
+
+// layout converters between the reference's (3, nsub, U) and the planes
+__global__ __launch_bounds__(kBlock) void k_to_soa(const double *__restrict__ aos, double *__restrict__ soa,
+                                                   int64_t N, int64_t pitch) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= N) return;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) soa[c * pitch + s] = aos[3 * s + c];
+}
+__global__ __launch_bounds__(kBlock) void k_to_aos(const double *__restrict__ soa, double *__restrict__ aos,
+                                                   int64_t N, int64_t pitch) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= N) return;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) aos[3 * s + c] = soa[c * pitch + s];
+}
+
+// ---- roofline kernels: one unfused level-1 sweep -------------------------
+// Assembled operator (the north star's "element-block-sparse" matrix in the
+// block-CSR layout of matrices.F90:997-1198 with its single non-zero block per
+// block-row): per sub-element A = rdt*M + Kd (9 planes) and w = omega/D
+// (3 planes). Traffic per sub-element: x 24 + b 24 + out 24 + A 72 + w 24 = 168 B.
+__global__ __launch_bounds__(kBlock) void k_build_blocks(const double *__restrict__ stc, double *__restrict__ blk,
+                                                         int64_t pitch, int64_t N, int nsub_log2, double rdt) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= N) return;
+    const double *r = stc + (s >> nsub_log2) * kStcStride;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) blk[q * pitch + s] = rdt * r[kStcM + q] + r[kStcK + q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) blk[(9 + q) * pitch + s] = r[kStcW + q];
+}
+
+__global__ __launch_bounds__(kBlock) void k_sweep_assembled(const double *__restrict__ x, const double *__restrict__ b,
+                                                            const double *__restrict__ blk, double *__restrict__ out,
+                                                            int64_t pitch, int64_t npairs) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npairs) return;
+    const int64_t s = 2 * p;
+    double2 xv[3], bv[3], a[12];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { xv[c] = ld2(x + c * pitch + s); bv[c] = ld2(b + c * pitch + s); }
+#pragma unroll
+    for (int q = 0; q < 12; ++q) a[q] = ld2(blk + q * pitch + s);
+    const double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
+    const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double A0 = a[3 * i].x * x0[0] + a[3 * i + 1].x * x0[1] + a[3 * i + 2].x * x0[2];
+        const double A1 = a[3 * i].y * x1[0] + a[3 * i + 1].y * x1[1] + a[3 * i + 2].y * x1[2];
+        st2(out + i * pitch + s, make_double2(x0[i] + a[9 + i].x * (b0[i] - A0), x1[i] + a[9 + i].y * (b1[i] - A1)));
+    }
+}
+
+// Matrix-free form of the same sweep (the reference's own structure: one
+// stencil per un_ele, ShapFun_unstruc.F90:304-335): 72 B per sub-element.
+__global__ __launch_bounds__(kBlock) void k_sweep_stencil(const double *__restrict__ x, const double *__restrict__ b,
+                                                          const double *__restrict__ stc, double *__restrict__ out,
+                                                          int64_t pitch, int64_t npairs, int nsub_log2, double rdt) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npairs) return;
+    const int64_t s = 2 * p;
+    double2 xv[3], bv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { xv[c] = ld2(x + c * pitch + s); bv[c] = ld2(b + c * pitch + s); }
+    Stc S;
+    load_stc(stc + (s >> nsub_log2) * kStcStride, S);
+    double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
+    const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
+    sweep(S, rdt, b0, x0);
+    sweep(S, rdt, b1, x1);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) st2(out + c * pitch + s, make_double2(x0[c], x1[c]));
+}
+
+inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+inline int log2i(int v) { int r = 0; while ((1 << r) < v) ++r; return r; }
+
+}  // namespace
+
+hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int sweeps, int solver, double rdt,
+                         double omega) {
+    const int64_t npairs = L.N / 2;
+    if (npairs == 0 || sweeps <= 0) return hipSuccess;
+    if (solver == 2)
+        hipLaunchKernelGGL(k_smooth<true>, dim3(grid_for(npairs)), dim3(kBlock), 0, s, src, L.T, L.TNN, L.RHS,
+                           L.stc, L.pitch, npairs, log2i(L.nsub), sweeps, rdt, omega);
+    else
+        hipLaunchKernelGGL(k_smooth<false>, dim3(grid_for(npairs)), dim3(kBlock), 0, s, src, L.T, L.TNN, L.RHS,
+                           L.stc, L.pitch, npairs, log2i(L.nsub), sweeps, rdt, omega);
+    return hipGetLastError();
+}
+
+hipError_t launch_residual(hipStream_t s, const Level &L, double rdt) {
+    const int64_t npairs = L.N / 2;
+    if (npairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_residual, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.RHS, L.RES, L.stc, L.pitch,
+                       npairs, log2i(L.nsub), rdt);
+    return hipGetLastError();
+}
+
+hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U) {
+    (void)U;
+    if (coarse.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_restrict, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.RES, coarse.RHS,
+                       fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub));
+    return hipGetLastError();
+}
+
+hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn) {
+    if (coarse.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prolong, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.T, fine.TNN, coarse.T,
+                       fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub), write_tnn ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, bool start_of_step) {
+    if (L.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rhs, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.T, L.TOLD, L.TNN, L.RHS, L.stc, geo1,
+                       L.subinfo, L.pitch, L.N, log2i(L.nsub), rdt, k, start_of_step ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_halo(hipStream_t s, const Level &L, double *tov, double *tovo) {
+    const HaloPlan &P = L.halo;
+    const int n = (int)(P.local.size() + P.bc.size() + P.remote.size());
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_halo, dim3(grid_for(n)), dim3(kBlock), 0, s, L.T, L.TOLD, L.pitch, tov, tovo, P.d_local,
+                       (int)P.local.size(), P.d_bc, (int)P.bc.size(), P.d_remote, (int)P.remote.size(), P.d_send);
+    return hipGetLastError();
+}
+
+hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo) {
+    const HaloPlan &P = L.halo;
+    const int n = (int)P.recv_dst.size();
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_halo_unpack, dim3(grid_for(n)), dim3(kBlock), 0, s, P.d_recv, P.d_recv_dst, n, tov, tovo);
+    return hipGetLastError();
+}
+
+hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_to_soa, dim3(grid_for(N)), dim3(kBlock), 0, s, aos, soa, N, pitch);
+    return hipGetLastError();
+}
+
+hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_to_aos, dim3(grid_for(N)), dim3(kBlock), 0, s, soa, aos, N, pitch);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt) {
+    hipLaunchKernelGGL(k_build_blocks, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.stc, L.blocks, L.pitch, L.N,
+                       log2i(L.nsub), rdt);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt) {
+    (void)rdt;
+    const int64_t npairs = L.N / 2;
+    hipLaunchKernelGGL(k_sweep_assembled, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
+                       L.pitch, npairs);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt) {
+    const int64_t npairs = L.N / 2;
+    hipLaunchKernelGGL(k_sweep_stencil, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.TNN, L.RHS, L.stc, out,
+                       L.pitch, npairs, log2i(L.nsub), rdt);
+    return hipGetLastError();
+}
+
+}  // namespace pamg

@@ -1,0 +1,270 @@
+// One-time setup of libpamg (host, fp64): sub-element numbering tables, the
+// per-(un_ele, level) 3x3 operator records and the halo plan.
+//
+// Compiled with -ffp-contract=off so every quantity is formed with the
+// reference's operation order (see oracle/pamg_oracle.c for the literal
+// restatement these mirror); the device kernels then reproduce the
+// reference's arithmetic bit for bit except the sine of the source term.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "pamg_internal.h"
+
+namespace pamg {
+
+// Msh2Tri.F90:32-60 get_str_info
+void get_str_info(int n_split, int ele, int *irow, int *ipos, int *orientation) {
+    int i = ele, row = 1, ele_row = (1 << (n_split + 1)) - 1;
+    *ipos = 1; *irow = 1;
+    while (i >= 1) {
+        if (i > ele_row) { i -= ele_row; row += 1; ele_row -= 2; }
+        else { *ipos = i; *irow = row; break; }
+    }
+    *orientation = *ipos % 2;
+}
+
+// splitting.F90:97-140 element_conversion (1-based fine ids)
+void element_conversion(int fin[4], int coarse_ele, int i_split) {
+    int irow, ipos, orient, counter, tot = 0;
+    int rowx = (1 << (i_split + 1)) * 2 - 1;
+    get_str_info(i_split, coarse_ele, &irow, &ipos, &orient);
+    if (orient == 1) {
+        counter = 2;
+        while (counter < irow * 2) { tot += rowx; rowx -= 2; counter += 1; }
+        fin[0] = ipos * 2 - 1 + tot;
+        fin[1] = fin[0] + 1;
+        fin[2] = fin[0] + 2;
+        tot += rowx;
+        fin[3] = ipos * 2 - 1 + tot;
+    } else {
+        counter = 1;
+        while (counter < irow * 2) { tot += rowx; rowx -= 2; counter += 1; }
+        fin[2] = (ipos / 2 - 1) * 3 + ipos / 2 + tot + 1;
+        fin[1] = fin[2] + 1;
+        fin[0] = fin[2] + 2;
+        fin[3] = fin[0] - rowx - 2;
+    }
+}
+
+// splitting.F90:427-451 loc_surf_ele_multigrid; surf(2**n, 3) column-major, 1-based values
+void loc_surf_ele(int n, std::vector<int> &surf) {
+    int m = 1 << n, ele, counter;
+    surf.assign(3 * (size_t)m, 0);
+    surf[0] = 1;
+    for (ele = 2; ele <= m; ++ele) surf[ele - 1] = surf[ele - 2] + 2;
+    surf[2 * m] = 1;
+    counter = surf[ele - 2];
+    surf[m] = counter;
+    for (ele = 2; ele <= m; ++ele) {
+        surf[(ele - 1) + m] = surf[(ele - 2) + m] + counter - 2;
+        surf[(ele - 1) + 2 * m] = surf[(ele - 2) + m] + 1;
+        counter -= 2;
+    }
+}
+
+// Msh2Tri.F90:69-107 get_splitting; un_x (2,3) column-major
+void get_splitting(const double *un_x, int n_split, int str_ele, double str_x[3][2]) {
+    double p = (double)(1 << n_split), v1[2], v2[2];
+    int irow, ipos, orient;
+    v1[0] = (un_x[0] - un_x[4]) / p;
+    v1[1] = (un_x[1] - un_x[5]) / p;
+    v2[0] = (un_x[2] - un_x[4]) / p;
+    v2[1] = (un_x[3] - un_x[5]) / p;
+    get_str_info(n_split, str_ele, &irow, &ipos, &orient);
+    for (int d = 0; d < 2; ++d) {
+        double x3 = un_x[4 + d];
+        if (ipos % 2 != 0) {
+            str_x[2][d] = x3 + (irow - 1) * v2[d] + (ipos / 2) * v1[d];
+            str_x[1][d] = x3 + irow * v2[d] + (ipos / 2) * v1[d];
+            str_x[0][d] = x3 + (irow - 1) * v2[d] + v1[d] * (ipos / 2 + 1);
+        } else {
+            str_x[0][d] = x3 + irow * v2[d] + v1[d] * (ipos / 2 - 1);
+            str_x[1][d] = x3 + (irow - 1) * v2[d] + v1[d] * (ipos / 2);
+            str_x[2][d] = x3 + irow * v2[d] + v1[d] * (ipos / 2);
+        }
+    }
+}
+
+// Operator record of one (un_ele, level): tri_det_nlx (ShapFun.F90:1389-1454) scaled by
+// semi_tri_det_nlx_multigrid (:1678-1683), get_un_ele_mass_stiff_diffvol
+// (ShapFun_unstruc.F90:304-335), the diff_vol1 reduction (transport_tri_semi.F90:602-606)
+// and get_diagonal (:481-486). The quadrature is TRIQUAold's ngi=3 edge-midpoint rule
+// (ShapFun.F90:554-563) with SHATRIold's P1 functions (:1036-1048).
+void level_stencil(const double *X, int i_split, double k, double dt, double omega, double *rec) {
+    static const double N[3][3] = {{0.5, 0.5, 0.0}, {0.0, 0.5, 0.5}, {0.5, 0.0, 0.5}};
+    static const double NLX[2][3] = {{1.0, 0.0, -1.0}, {0.0, 1.0, -1.0}};
+    const double weight = 1.0 / 3.0;
+    double detwei[3], nx[3][2][3];
+    for (int g = 0; g < 3; ++g) {
+        double agi = 0, bgi = 0, cgi = 0, dgi = 0;
+        for (int L = 0; L < 3; ++L) {
+            agi = agi + NLX[0][L] * X[2 * L];
+            bgi = bgi + NLX[0][L] * X[2 * L + 1];
+            cgi = cgi + NLX[1][L] * X[2 * L];
+            dgi = dgi + NLX[1][L] * X[2 * L + 1];
+        }
+        double detj = agi * dgi - bgi * cgi;
+        detwei[g] = 0.5 * std::fabs(detj) * weight;
+        double a11 = dgi / detj, a21 = -(cgi / detj), a12 = -(bgi / detj), a22 = agi / detj;
+        for (int L = 0; L < 3; ++L) {
+            nx[g][0][L] = a11 * NLX[0][L] + a12 * NLX[1][L];
+            nx[g][1][L] = a21 * NLX[0][L] + a22 * NLX[1][L];
+        }
+        detwei[g] = detwei[g] / (double)(1 << (2 * i_split));
+        for (int d = 0; d < 2; ++d)
+            for (int L = 0; L < 3; ++L) nx[g][d][L] = nx[g][d][L] * (double)(1 << i_split);
+    }
+    double ml[3], M[3][3], Kd[3][3];
+    for (int j = 0; j < 3; ++j) {
+        double s = 0;
+        for (int g = 0; g < 3; ++g) s = s + N[g][j] * detwei[g];
+        ml[j] = s;
+        for (int i = 0; i < 3; ++i) {
+            double m = 0;
+            for (int g = 0; g < 3; ++g) m = m + N[g][i] * detwei[g] * N[g][j];
+            M[i][j] = m;
+        }
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double acc = 0.0;
+            for (int d = 0; d < 2; ++d) {
+                double s = 0;
+                for (int g = 0; g < 3; ++g) s = s + k * nx[g][d][i] * detwei[g] * nx[g][d][j];
+                acc = acc + s;
+            }
+            Kd[i][j] = acc;
+        }
+    std::memset(rec, 0, sizeof(double) * kStcStride);
+    double rdt = 1 / dt;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) {
+            rec[kStcM + 3 * i + j] = M[i][j];
+            rec[kStcK + 3 * i + j] = Kd[i][j];
+        }
+        double D = rdt * ml[i] + Kd[i][i] + 0.0;
+        rec[kStcW + i] = omega / D;
+    }
+}
+
+// Halo plan of update_overlaps (splitting.F90:1210-1397) for level l:
+// for every owned un_ele u, faces in the order 1, 3, 2, and the 2**i boundary
+// sub-elements surf_ele(:, f): either a boundary-condition write of
+// sin(x+y) at two nodes into u's own t_overlap(:, f), or a copy of
+// (tnew, told)(:, s, u) into t_overlap(slot, Nside) of the neighbour.
+// Each destination word has exactly one writer, so the plan is order-free.
+int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const int *fneig, const int *dir) {
+    Level &L = h->lv[l];
+    HaloPlan &P = L.halo;
+    P.local.clear(); P.bc.clear(); P.remote.clear(); P.recv_dst.clear();
+    P.peers.clear(); P.send_peer_off.clear(); P.recv_peer_off.clear();
+    const int is = L.isplit, m = 1 << is, sl = h->slots;
+    std::vector<int> surf;
+    loc_surf_ele(is, surf);
+    const bool dist = !h->owner.empty();
+    std::vector<int> g2l;   // global -> local index (or -1)
+    if (dist) {
+        g2l.assign(h->U_global, -1);
+        for (int q = 0; q < h->U; ++q) g2l[h->owned[q]] = q;
+    }
+    // remote entries grouped by destination rank, in (sender u, face, i) order
+    std::vector<std::vector<HaloCopy>> by_peer(h->nranks);
+    static const int face_order[3] = {1, 3, 2};
+    for (int q = 0; q < h->U; ++q) {
+        const int ug = dist ? h->owned[q] : q;
+        const double *X = Xg + 6 * (size_t)ug;
+        for (int fo = 0; fo < 3; ++fo) {
+            const int f = face_order[fo];
+            for (int i = 1; i <= m; ++i) {
+                const int se = surf[(i - 1) + (f - 1) * m];
+                int irow, ipos, orient;
+                get_str_info(is, se, &irow, &ipos, &orient);
+                const int npos = neig[3 * (size_t)ug + f - 1];
+                const int src = q * L.nsub + se - 1;
+                if (npos == 0) {
+                    double xl[3][2];
+                    get_splitting(X, is, se, xl);
+                    int a, b, na, nb;
+                    if (f == 1) { a = (ipos / 2) * 3 + 1; b = (ipos / 2) * 3 + 3; na = 0; nb = 2; }
+                    else if (f == 3) { a = (irow - 1) * 3 + 2; b = (irow - 1) * 3 + 3; na = 1; nb = 2; }
+                    else { a = (irow - 1) * 3 + 1; b = (irow - 1) * 3 + 2; na = 0; nb = 1; }
+                    const int base = q * sl * 3 + (f - 1) * sl;
+                    HaloBC e;
+                    e.dst_a = base + a - 1;
+                    e.dst_b = base + b - 1;
+                    e.val_a = std::sin(xl[na][0] + xl[na][1]);   // boundary(), splitting.F90:1401-1405
+                    e.val_b = std::sin(xl[nb][0] + xl[nb][1]);
+                    P.bc.push_back(e);
+                } else {
+                    const int nside = fneig[3 * (size_t)ug + f - 1];
+                    const int dr = dir[3 * (size_t)ug + f - 1];
+                    if (nside < 1 || nside > 3) {
+                        h->err = "halo: asymmetric neighbour table (fNeig = 0) at un_ele " + std::to_string(ug + 1);
+                        return PAMG_ERR_ARG;
+                    }
+                    int fwd, rev;
+                    if (f == 1) { fwd = ipos / 2 + 1; rev = m - (ipos / 2 + 1) + 1; }
+                    else { fwd = irow; rev = m - irow + 1; }
+                    if (f == 2) std::swap(fwd, rev);   // face 2 branches are mirrored (:1354-1391)
+                    const int kslot = (nside == 2) ? (dr ? rev : fwd) : (dr ? fwd : rev);
+                    const int ng = npos - 1;
+                    const int off_in_elem = (nside - 1) * sl + kslot * 3 - 3;
+                    if (!dist || h->owner[ng] == h->rank) {
+                        const int nl = dist ? g2l[ng] : ng;
+                        P.local.push_back(HaloCopy{src, nl * sl * 3 + off_in_elem});
+                    } else {
+                        by_peer[h->owner[ng]].push_back(HaloCopy{src, off_in_elem});
+                    }
+                }
+            }
+        }
+    }
+    if (dist) {
+        // send side: peers in ascending rank order
+        P.send_peer_off.push_back(0);
+        for (int r = 0; r < h->nranks; ++r) {
+            if (r == h->rank) continue;
+            bool has_send = !by_peer[r].empty();
+            // receive side from r: enumerate r's owned elements in the same order
+            std::vector<int> rd;
+            for (int ug = 0; ug < h->U_global; ++ug) {
+                if (h->owner[ug] != r) continue;
+                for (int fo = 0; fo < 3; ++fo) {
+                    const int f = face_order[fo];
+                    const int npos = neig[3 * (size_t)ug + f - 1];
+                    if (npos == 0 || h->owner[npos - 1] != h->rank) continue;
+                    const int nside = fneig[3 * (size_t)ug + f - 1];
+                    const int dr = dir[3 * (size_t)ug + f - 1];
+                    for (int i = 1; i <= m; ++i) {
+                        const int se = surf[(i - 1) + (f - 1) * m];
+                        int irow, ipos, orient;
+                        get_str_info(is, se, &irow, &ipos, &orient);
+                        int fwd, rev;
+                        if (f == 1) { fwd = ipos / 2 + 1; rev = m - (ipos / 2 + 1) + 1; }
+                        else { fwd = irow; rev = m - irow + 1; }
+                        if (f == 2) std::swap(fwd, rev);
+                        const int kslot = (nside == 2) ? (dr ? rev : fwd) : (dr ? fwd : rev);
+                        const int nl = g2l[npos - 1];
+                        rd.push_back(nl * sl * 3 + (nside - 1) * sl + kslot * 3 - 3);
+                    }
+                }
+            }
+            if (!has_send && rd.empty()) continue;
+            P.peers.push_back(r);
+            for (auto &e : by_peer[r]) {
+                HaloCopy c{e.src, (int)P.remote.size()};
+                (void)c;
+                P.remote.push_back(HaloCopy{e.src, (int)P.remote.size()});
+            }
+            P.send_peer_off.push_back((int)P.remote.size());
+            if (P.recv_peer_off.empty()) P.recv_peer_off.push_back(0);
+            P.recv_dst.insert(P.recv_dst.end(), rd.begin(), rd.end());
+            P.recv_peer_off.push_back((int)P.recv_dst.size());
+        }
+        if (P.recv_peer_off.empty()) P.recv_peer_off.push_back(0);
+    }
+    return PAMG_OK;
+}
+
+}  // namespace pamg

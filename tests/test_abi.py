@@ -1,0 +1,69 @@
+"""CPU checks of the C-ABI boundary: libpamg.so loads, exports every entry point
+include/pamg.h declares, and refuses to run without a GPU instead of falling
+back to a CPU path."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import pamg
+from pamg import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pamg.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pamg_\w+)\s*\(", text)))
+
+
+def test_header_declares_the_hot_path():
+    fns = header_functions()
+    for name in ("pamg_smoother", "pamg_restrictor", "pamg_get_residual", "pamg_prolongator",
+                 "pamg_vcycle", "pamg_begin_timestep", "pamg_upload_mesh", "pamg_comm_init"):
+        assert name in fns
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    missing = [f for f in header_functions() if not hasattr(L, f)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_every_declared_symbol():
+    src = open(os.path.join(ROOT, "p-a_multigrids_amd", "pamg", "_lib.py")).read()
+    missing = [f for f in header_functions() if f'"{f}"' not in src]
+    assert not missing, missing
+
+
+def test_version_and_defaults_match_reference_mode9():
+    L = _lib.lib()
+    assert L.pamg_version() >= 100
+    p = pamg.default_params()
+    # main.F90:46-47 and transport_tri_semi.F90:117-140
+    assert (p.n_split, p.multi_levels, p.n_smooth, p.n_coarse, p.solver) == (1, 1, 4, 15, 3)
+    assert p.dt == 1.0 * 0.0000125 and p.k == 1.0 and p.omega == 0.8 and p.theta == 1.0
+
+
+def test_parameter_validation():
+    L = _lib.lib()
+    h = C.c_void_p()
+    bad = [dict(multi_levels=3, n_split=2), dict(theta=0.5), dict(solver=4), dict(dt=0.0)]
+    for kw in bad:
+        p = pamg.default_params(**kw)
+        assert L.pamg_create(C.byref(p), C.byref(h)) == -1, kw
+
+
+@pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") is None and os.path.exists("/dev/kfd"),
+                    reason="a GPU may be present")
+def test_no_gpu_fails_loudly():
+    """Without a device the product path refuses to run (no CPU fallback)."""
+    p = pamg.default_params()
+    h = C.c_void_p()
+    rc = _lib.lib().pamg_create(C.byref(p), C.byref(h))
+    assert rc == -6   # PAMG_ERR_NODEV
+    with pytest.raises(pamg.PamgError):
+        pamg.SemiImplicitIterative(pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "untitled8.msh")), 1, 1)
