@@ -11,7 +11,7 @@ import sys
 def rows_from_db(path):
     con = sqlite3.connect(path)
     cur = con.cursor()
-    return [(r[0], int(r[1]), float(r[2]) * 1e-3, float(r[3]) * 1e-3, float(r[4]))
+    return [(r[0], int(r[1]), float(r[2]), float(r[3]), float(r[4]))   # top_kernels view: microseconds
             for r in cur.execute("select name, total_calls, total_duration, average, percentage from top_kernels")]
 
 
@@ -31,7 +31,7 @@ def main():
     rows = rows_from_csv(csvs[0]) if csvs else rows_from_db(dbs[0])
     lines = [f"{'kernel':70s} {'calls':>6s} {'total_us':>11s} {'avg_us':>9s} {'pct':>6s}"]
     for name, n, tot, avg, pct in rows:
-        short = name.split("(")[0].replace("pamg::(anonymous namespace)::", "").replace("void ", "")
+        short = name.replace("pamg::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         lines.append(f"{short[:70]:70s} {n:6d} {tot:11.1f} {avg:9.2f} {pct:6.2f}")
     text = "\n".join(lines) + "\n"
     if len(sys.argv) > 2:
