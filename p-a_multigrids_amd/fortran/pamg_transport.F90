@@ -8,7 +8,7 @@
 ! Run-time configuration (the reference hard-codes these, :99,:118,:135 and
 ! main.F90:46-47) comes from the namelist file given as the first argument
 ! (default pamg_run.nml):
-!   &pamg_run mesh='untitled8.msh', n_split=3, multi_levels=3, n_smooth=4,
+!   &transport mesh_file='untitled8.msh', n_split=3, multi_levels=3, n_smooth=4,
 !             solver=3, ntime=2, n_multigrid=2, device=0, dump='out.bin',
 !             call_sites=1 /
 ! call_sites=1 drives the fine-grained entry points exactly at the reference
@@ -16,13 +16,13 @@
 program pamg_transport
   use iso_c_binding
   use pamg
-  use LinearSolvers, only: Mesh, pamg_bind_handle, GSsolver_MeshSD
+  use LinearSolvers, only: MeshRec => Mesh, pamg_bind_handle, GSsolver_MeshSD
   implicit none
 
-  character(len=512) :: mesh = 'untitled8.msh', dump = ''
+  character(len=512) :: mesh_file = 'untitled8.msh', dump = ''
   integer :: n_split = 1, multi_levels = 1, n_smooth = 4, solver = 3, ntime = 2, n_multigrid = 2
   integer :: device = 0, call_sites = 1, facade_sweeps = 0
-  namelist /pamg_run/ mesh, n_split, multi_levels, n_smooth, solver, ntime, n_multigrid, device, dump, &
+  namelist /transport/ mesh_file, n_split, multi_levels, n_smooth, solver, ntime, n_multigrid, device, dump, &
        call_sites, facade_sweeps
 
   character(len=512) :: cfg
@@ -33,18 +33,18 @@ program pamg_transport
   integer(c_int), allocatable :: region(:), neig(:), fneig(:), dir(:)
   integer :: u_, itime, multigrid, ilevel, i
   integer(8) :: c0, c1, crate
-  type(Mesh), allocatable :: meshList(:)
+  type(MeshRec), allocatable :: meshList(:)
 
   cfg = 'pamg_run.nml'
   if (command_argument_count() >= 1) call get_command_argument(1, cfg)
   open(10, file=trim(cfg), status='old', action='read')
-  read(10, nml=pamg_run)
+  read(10, nml=transport)
   close(10)
 
   print *, '---------------------------------------------------------'
   print *, '|       Reading the .msh file     |'
-  rc = pamg_msh_read(c_path(mesh), m)                       ! ReadMSH (:99)
-  call pamg_check(rc, c_null_ptr, 'pamg_msh_read '//trim(mesh))
+  rc = pamg_msh_read(c_path(mesh_file), m)                       ! ReadMSH (:99)
+  call pamg_check(rc, c_null_ptr, 'pamg_msh_read '//trim(mesh_file))
   call pamg_check(pamg_msh_size(m, U), c_null_ptr, 'pamg_msh_size')
   allocate(X(6*U), region(U), neig(3*U), fneig(3*U), dir(3*U))
   call pamg_check(pamg_msh_get(m, X, region, neig, fneig, dir), c_null_ptr, 'pamg_msh_get')
