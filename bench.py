@@ -114,7 +114,9 @@ def main():
         obj = [pamg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = (world, rank, obj[0], mesh.x_strip_owner(world))
-    s = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=local,
+    ndev = max(1, torch.cuda.device_count())
+    device = local % ndev
+    s = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
                                    halo_mode=a.halo_mode, comm=comm)
     s.begin_timestep()
     s.vcycle(a.warmup)
@@ -160,7 +162,7 @@ def main():
                 ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
                 frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
         s.close()
-        s3 = pamg.SemiImplicitIterative(mesh, 3, a.levels, n_smooth=a.nsmooth, solver=3, device=local)
+        s3 = pamg.SemiImplicitIterative(mesh, 3, a.levels, n_smooth=a.nsmooth, solver=3, device=device)
         s3.begin_timestep()
         s3.vcycle(a.warmup)
         s3.synchronize()

@@ -5,6 +5,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -135,14 +137,14 @@ double *field_ptr(pamg_handle *h, int l, int what) {
 }
 
 // ---- halo exchange --------------------------------------------------------
+// The halo words of a smoother call are written by the smoother kernel itself
+// (local neighbours and boundary values into t_overlap, remote neighbours into
+// the packed send buffer); what remains here is the exchange with other ranks.
 int halo(pamg_handle *h, int l) {
     Level &L = h->lv[l];
     const HaloPlan &P = L.halo;
-    {
-        Span sp(h, PAMG_K_HALO, (double)(P.local.size() + P.remote.size()) * 72.0 + P.bc.size() * 48.0);
-        HIPCHK(h, launch_halo(h->stream, L, h->tov, h->tovo));
-    }
     if (h->comm && !P.peers.empty()) {
+        Span sp(h, PAMG_K_HALO, 2.0 * 48.0 * (double)(P.remote.size() + P.recv_dst.size()));
         NCCLCHK(h, ncclGroupStart());
         for (size_t q = 0; q < P.peers.size(); ++q) {
             const int peer = P.peers[q];
@@ -165,8 +167,7 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
     Level &L = h->lv[l];
     h->tnn_level = l;
     if (sweeps <= 0) {
-        if (src_is_T) HIPCHK(h, hipMemcpyAsync(L.TNN, L.T, 3 * L.pitch * sizeof(double), hipMemcpyDeviceToDevice,
-                                               h->stream));
+        if (src_is_T) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
         return PAMG_OK;
     }
     const double rdt = 1 / h->p.dt;
@@ -177,7 +178,7 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
             {
                 Span sp(h, kid, bytes);
                 HIPCHK(h, launch_smooth(h->stream, L, (s == 0 && src_is_T) ? L.T : L.TNN, 1, h->p.solver, rdt,
-                                        h->p.omega));
+                                        h->p.omega, h->tov, h->tovo));
             }
             CHK(halo(h, l));
         }
@@ -185,7 +186,8 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
     }
     {
         Span sp(h, kid, bytes);
-        HIPCHK(h, launch_smooth(h->stream, L, src_is_T ? L.T : L.TNN, sweeps, h->p.solver, rdt, h->p.omega));
+        HIPCHK(h, launch_smooth(h->stream, L, src_is_T ? L.T : L.TNN, sweeps, h->p.solver, rdt, h->p.omega, h->tov,
+                                h->tovo));
     }
     return halo(h, l);
 }
@@ -241,6 +243,7 @@ void free_levels(pamg_handle *h) {
         dev_free(L.T); dev_free(L.stc); dev_free(L.subinfo); dev_free(L.children); dev_free(L.blocks);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_recv);
+        dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
         L = Level();
     }
     dev_free(h->geo1); dev_free(h->tov); dev_free(h->tovo);
@@ -402,6 +405,9 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         CHK(dev_upload(h, &P.d_bc, P.bc));
         CHK(dev_upload(h, &P.d_remote, P.remote));
         CHK(dev_upload(h, &P.d_recv_dst, P.recv_dst));
+        CHK(dev_upload(h, &P.d_hface, P.hface));
+        CHK(dev_upload(h, &P.d_hsub, P.hsub));
+        CHK(dev_upload(h, &P.d_bcv, P.bcv));
         CHK(dev_alloc(h, &P.d_send, 6 * P.remote.size()));
         CHK(dev_alloc(h, &P.d_recv, 6 * P.recv_dst.size()));
     }
@@ -418,7 +424,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
                         for (int e = 0; e < L1.nsub; ++e) t[c * L1.pitch + (size_t)q * L1.nsub + e] = 1.0;
             HIPCHK(h, hipMemcpy(L1.T, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
         }
-        HIPCHK(h, hipMemcpyAsync(L1.TNN, L1.T, 3 * L1.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, launch_copy(h->stream, L1.T, L1.TNN, 3 * L1.pitch));
         h->tnn_level = 1;
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -479,8 +485,8 @@ int pamg_begin_timestep(pamg_handle *h) {
     h->tnn_level = 1;
     if (h->p.solver == 2) {   // solve_Richardson never calls get_RHS inside the smoother
         Level &L = h->lv[1];
-        HIPCHK(h, hipMemcpyAsync(L.TOLD, L.T, 3 * L.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
-        HIPCHK(h, hipMemcpyAsync(L.TNN, L.T, 3 * L.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, launch_copy(h->stream, L.T, L.TOLD, 3 * L.pitch));
+        HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
         return PAMG_OK;
     }
     return rhs_level1(h, true);
@@ -490,7 +496,7 @@ int pamg_copy_to_nonlin(pamg_handle *h, int level) {
     if (!h) return PAMG_ERR_ARG;
     CHK(check_level(h, level));
     Level &L = h->lv[level];
-    HIPCHK(h, hipMemcpyAsync(L.TNN, L.T, 3 * L.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
     h->tnn_level = level;
     return PAMG_OK;
 }

@@ -40,6 +40,14 @@ struct HaloPlan {
     std::vector<int> recv_dst;            // per received entry: t_overlap offset
     std::vector<int> recv_peer_off;       // per peer: first entry in recv (size npeers+1)
     std::vector<int> peers;               // peer ranks
+    // fused form used by the smoother kernel (one record per owned un_ele and face, one
+    // entry per sub-element of the level): the smoother threads that hold a boundary
+    // sub-element write its halo words themselves.
+    std::vector<int4> hface;              // (U*3) {mode | rev << 2, dst base, aux, 0}; mode 0 BC, 1 local, 2 remote
+    std::vector<int4> hsub;               // (nsub) position i (1-based, 0 = none) along faces 1, 2, 3
+    std::vector<double2> bcv;             // BC values sin(x+y) at the two face nodes, (u, f, i) order
+    int4 *d_hface = nullptr, *d_hsub = nullptr;
+    double2 *d_bcv = nullptr;
     // device copies
     HaloCopy *d_local = nullptr, *d_remote = nullptr;
     HaloBC *d_bc = nullptr;
@@ -110,13 +118,13 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
 // ---- kernels (pamg_kernels.hip) ----
 namespace pamg {
 hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int sweeps, int solver,
-                         double rdt, double omega);
+                         double rdt, double omega, double *tov, double *tovo);
 hipError_t launch_residual(hipStream_t s, const Level &L, double rdt);
 hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U);
 hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn);
 hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, bool start_of_step);
-hipError_t launch_halo(hipStream_t s, const Level &L, double *tov, double *tovo);
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
+hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch);
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt);

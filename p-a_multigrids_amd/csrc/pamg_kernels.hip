@@ -16,6 +16,8 @@
 // fp64 ridge, so these are HBM-bound streaming kernels; MFMA has no role.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "pamg_internal.h"
 
 namespace pamg {
@@ -59,17 +61,71 @@ __device__ __forceinline__ void sweep(const Stc &S, double rdt, const double b[3
     for (int i = 0; i < 3; ++i) x[i] = x[i] + S.w[i] * (b[i] - A[i]);
 }
 
+// Halo words written by the smoother (update_overlaps, splitting.F90:1210-1397).
+struct HaloArgs {
+    const int4 *hsub;     // per sub-element: position along faces 1, 2, 3 (0 = none)
+    const int4 *hface;    // per (un_ele, face): {mode | rev << 2, dst base, aux, 0}
+    const double2 *bcv;   // boundary values sin(x + y) at the two face nodes
+    const double *TOLD;
+    double *tov, *tovo, *send;
+    int m;                // 2**i_split sub-elements per face
+};
+
+// The reference rewrites the halo at the start of every sweep from the then
+// current tnew (:550-556); the last write of a smoother call therefore carries
+// the iterate before the last sweep, which is what these threads hold in p[].
+__device__ __forceinline__ void halo_face(const HaloArgs &H, int64_t u, int f, int i, double t0, double t1,
+                                          double t2, int64_t s, int64_t pitch) {
+    const double t[3] = {t0, t1, t2};
+    const int4 rec = H.hface[3 * u + f - 1];
+    const int mode = rec.x & 3;
+    if (mode == 0) {   // domain boundary: BC values into the own column (:1243-1252, :1287-1295, :1345-1353)
+        const int a = (i - 1) * 3 + (f == 3 ? 1 : 0);
+        const int b = (i - 1) * 3 + (f == 2 ? 1 : 2);
+        const double2 v = H.bcv[rec.z + i - 1];
+        H.tov[rec.y + a] = v.x;
+        H.tov[rec.y + b] = v.y;
+        H.tovo[rec.y + a] = v.x;
+        H.tovo[rec.y + b] = v.y;
+        return;
+    }
+    double to[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) to[c] = H.TOLD[c * pitch + s];
+    if (mode == 1) {   // neighbour on this rank: t_overlap(slot, Nside) of the neighbour
+        const int k = (rec.x >> 2) ? (H.m - i + 1) : i;
+        const int64_t d = rec.y + (int64_t)(k - 1) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { H.tov[d + c] = t[c]; H.tovo[d + c] = to[c]; }
+    } else {           // neighbour on another rank: packed send buffer (RCCL)
+        double *o = H.send + 6 * (int64_t)(rec.z + i - 1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { o[c] = t[c]; o[3 + c] = to[c]; }
+    }
+}
+
+__device__ __forceinline__ void halo_sub(const HaloArgs &H, int64_t s, int nsub_log2, double t0, double t1,
+                                         double t2, int64_t pitch) {
+    const int4 hs = H.hsub[s & ((1ll << nsub_log2) - 1)];
+    if ((hs.x | hs.y | hs.z) == 0) return;
+    const int64_t u = s >> nsub_log2;
+    if (hs.x) halo_face(H, u, 1, hs.x, t0, t1, t2, s, pitch);
+    if (hs.y) halo_face(H, u, 2, hs.y, t0, t1, t2, s, pitch);
+    if (hs.z) halo_face(H, u, 3, hs.z, t0, t1, t2, s, pitch);
+}
+
 // Fused smoother call(s): `sweeps` consecutive sweeps kept in registers.
-// `src` may alias T or TNN (each thread reads its own words before writing them).
 // Reference semantics (:548-550): each sweep starts with tnew := tnew_nonlin,
 // so after the call tnew holds the iterate before the last sweep and
-// tnew_nonlin the last one.
-template <bool RICHARDSON>
+// tnew_nonlin the last one. `src` may alias T or TNN (each thread reads its
+// own words before writing them). UNIFORM: every wave lies inside one un_ele
+// (nsub >= 128), so the operator record is read through the scalar unit.
+template <bool RICHARDSON, bool UNIFORM>
 __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T, double *TNN,
                                                    const double *__restrict__ RHS,
                                                    const double *__restrict__ stc, int64_t pitch,
                                                    int64_t npairs, int nsub_log2, int sweeps, double rdt,
-                                                   double omega) {
+                                                   double omega, HaloArgs H) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= npairs) return;
     const int64_t s = 2 * p;
@@ -93,8 +149,10 @@ __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T,
             }
         }
     } else {
+        int64_t u = s >> nsub_log2;
+        if (UNIFORM) u = __builtin_amdgcn_readfirstlane((int)u);
         Stc S;
-        load_stc(stc + (s >> nsub_log2) * kStcStride, S);
+        load_stc(stc + u * kStcStride, S);
         for (int it = 0; it < sweeps; ++it) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) { p0[i] = x0[i]; p1[i] = x1[i]; }
@@ -106,6 +164,10 @@ __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T,
     for (int c = 0; c < 3; ++c) {
         st2(T + c * pitch + s, make_double2(p0[c], p1[c]));
         st2(TNN + c * pitch + s, make_double2(x0[c], x1[c]));
+    }
+    if (H.hsub) {
+        halo_sub(H, s, nsub_log2, p0[0], p0[1], p0[2], pitch);
+        halo_sub(H, s + 1, nsub_log2, p1[0], p1[1], p1[2], pitch);
     }
 }
 
@@ -246,40 +308,91 @@ __global__ __launch_bounds__(kBlock) void k_prolong(double *__restrict__ T, doub
         for (int i = 0; i < 3; ++i) T[i * pitch_f + fi[q]] = f[q][i];
 }
 
-// update_overlaps (splitting.F90:1210-1397): boundary writes and neighbour
-// copies of (tnew, told) into t_overlap / t_overlap_old (one writer per word),
-// plus the packed send buffer for neighbours owned by other ranks.
-__global__ __launch_bounds__(kBlock) void k_halo(const double *__restrict__ T, const double *__restrict__ TOLD,
-                                                 int64_t pitch, double *__restrict__ tov, double *__restrict__ tovo,
-                                                 const HaloCopy *__restrict__ loc, int nloc,
-                                                 const HaloBC *__restrict__ bc, int nbc,
-                                                 const HaloCopy *__restrict__ rem, int nrem,
-                                                 double *__restrict__ send) {
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    if (e < nloc) {
-        const HaloCopy h = loc[e];
+// LDS-tiled inter-level transfers. A workgroup owns a tile of whole un_eles
+// (TF fine sub-elements, TF >= nsub_f): the fine fields of the tile are
+// streamed into LDS with coalesced double2 loads, the children of each coarse
+// sub-element (element_conversion, splitting.F90:97-140) are then addressed in
+// LDS, and the tile is streamed back. This replaces per-thread gathers of four
+// children spread over two rows of the un_ele.
+__global__ __launch_bounds__(kBlock) void k_prolong_tile(double *T, double *TNN, const double *__restrict__ Tc,
+                                                         const int4 *__restrict__ children, int64_t pitch_f,
+                                                         int64_t pitch_c, int64_t Nf, int nsubf_log2, int tile_log2,
+                                                         int write_tnn) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int TF = 1 << tile_log2;
+    const int64_t f0 = (int64_t)blockIdx.x << tile_log2;
+    const int nf = (int)min((int64_t)TF, Nf - f0);
+    for (int j = 2 * threadIdx.x; j < nf; j += 2 * kBlock) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            tov[h.dst + q] = T[q * pitch + h.src];
-            tovo[h.dst + q] = TOLD[q * pitch + h.src];
+        for (int c = 0; c < 3; ++c) {
+            const double2 v = ld2(T + c * pitch_f + f0 + j);
+            *reinterpret_cast<double2 *>(&lds[c * TF + j]) = v;
+            if (write_tnn) st2(TNN + c * pitch_f + f0 + j, v);   // tnew_nonlin := tnew (:365-367)
         }
-    } else if (e < nloc + nbc) {
-        const HaloBC b = bc[e - nloc];
-        tov[b.dst_a] = b.val_a;
-        tov[b.dst_b] = b.val_b;
-        tovo[b.dst_a] = b.val_a;
-        tovo[b.dst_b] = b.val_b;
-    } else if (e < nloc + nbc + nrem) {
-        const HaloCopy h = rem[e - nloc - nbc];
-        double *o = send + 6 * (int64_t)h.dst;
+    }
+    __syncthreads();
+    const int nsubc_log2 = nsubf_log2 - 2;
+    const int64_t c0 = f0 >> 2;
+    for (int cc = threadIdx.x; cc < (nf >> 2); cc += kBlock) {
+        const int c = (int)((c0 + cc) & ((1ll << nsubc_log2) - 1));
+        const int base = (cc >> nsubc_log2) << nsubf_log2;
+        const int4 ch = children[c];
+        const int fi[4] = {base + ch.x, base + ch.y, base + ch.z, base + ch.w};
+        const double y[3] = {Tc[c0 + cc], Tc[pitch_c + c0 + cc], Tc[2 * pitch_c + c0 + cc]};
+        double f[4][3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            o[q] = T[q * pitch + h.src];
-            o[3 + q] = TOLD[q * pitch + h.src];
-        }
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) f[q][i] = lds[i * TF + fi[q]];
+        f[0][0] = f[0][0] + 0.5 * y[2] + 0.5 * y[0];
+        f[0][1] = f[0][1] + 0.5 * y[1] + 0.5 * y[2];
+        f[0][2] = f[0][2] + y[2];
+        f[1][0] = f[1][0] + f[0][1];
+        f[1][1] = f[1][1] + f[0][0];
+        f[1][2] = f[1][2] + 0.5 * y[0] + 0.5 * y[1];
+        f[2][0] = f[2][0] + y[0];
+        f[2][1] = f[2][1] + f[1][2];
+        f[2][2] = f[2][2] + f[1][1];
+        f[3][0] = f[3][0] + f[1][2];
+        f[3][1] = f[3][1] + y[1];
+        f[3][2] = f[3][2] + f[1][0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) lds[i * TF + fi[q]] = f[q][i];
+    }
+    __syncthreads();
+    for (int j = 2 * threadIdx.x; j < nf; j += 2 * kBlock)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) st2(T + c * pitch_f + f0 + j, *reinterpret_cast<const double2 *>(&lds[c * TF + j]));
+}
+
+__global__ __launch_bounds__(kBlock) void k_restrict_tile(const double *__restrict__ RES, double *__restrict__ RHSc,
+                                                          const int4 *__restrict__ children, int64_t pitch_f,
+                                                          int64_t pitch_c, int64_t Nf, int nsubf_log2, int tile_log2) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int TF = 1 << tile_log2;
+    const int64_t f0 = (int64_t)blockIdx.x << tile_log2;
+    const int nf = (int)min((int64_t)TF, Nf - f0);
+    for (int j = 2 * threadIdx.x; j < nf; j += 2 * kBlock)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            *reinterpret_cast<double2 *>(&lds[c * TF + j]) = ld2(RES + c * pitch_f + f0 + j);
+    __syncthreads();
+    const int nsubc_log2 = nsubf_log2 - 2;
+    const int64_t c0 = f0 >> 2;
+    for (int cc = threadIdx.x; cc < (nf >> 2); cc += kBlock) {
+        const int c = (int)((c0 + cc) & ((1ll << nsubc_log2) - 1));
+        const int base = (cc >> nsubc_log2) << nsubf_log2;
+        const int4 ch = children[c];
+        const int pick[3] = {base + ch.z, base + ch.w, base + ch.x};   // children 3, 4, 1 (splitting.F90:26-28)
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            RHSc[i * pitch_c + c0 + cc] = (lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]) / 3.;
     }
 }
 
+// Unpack of the halo words received from other ranks (RCCL) into t_overlap.
 __global__ __launch_bounds__(kBlock) void k_halo_unpack(const double *__restrict__ recv, const int *__restrict__ dst,
                                                         int n, double *__restrict__ tov, double *__restrict__ tovo) {
     const int e = blockIdx.x * kBlock + threadIdx.x;
@@ -290,6 +403,12 @@ __global__ __launch_bounds__(kBlock) void k_halo_unpack(const double *__restrict
         tov[d + q] = recv[6 * (int64_t)e + q];
         tovo[d + q] = recv[6 * (int64_t)e + 3 + q];
     }
+}
+
+// device-to-device copy of whole planes (tnew_nonlin := tnew, told := tnew)
+__global__ __launch_bounds__(kBlock) void k_copy(const double *__restrict__ a, double *__restrict__ b, int64_t n2) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (int64_t)gridDim.x * kBlock)
+        st2(b + 2 * i, ld2(a + 2 * i));
 }
 
 // layout converters between the reference's (3, nsub, U) and the planes
@@ -372,15 +491,22 @@ inline int log2i(int v) { int r = 0; while ((1 << r) < v) ++r; return r; }
 }  // namespace
 
 hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int sweeps, int solver, double rdt,
-                         double omega) {
+                         double omega, double *tov, double *tovo) {
     const int64_t npairs = L.N / 2;
     if (npairs == 0 || sweeps <= 0) return hipSuccess;
+    const HaloPlan &P = L.halo;
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, L.TOLD, tov, tovo, P.d_send, 1 << L.isplit};
+    const int lg = log2i(L.nsub);
+    const dim3 g(grid_for(npairs)), b(kBlock);
     if (solver == 2)
-        hipLaunchKernelGGL(k_smooth<true>, dim3(grid_for(npairs)), dim3(kBlock), 0, s, src, L.T, L.TNN, L.RHS,
-                           L.stc, L.pitch, npairs, log2i(L.nsub), sweeps, rdt, omega);
+        hipLaunchKernelGGL((k_smooth<true, false>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg,
+                           sweeps, rdt, omega, H);
+    else if (L.nsub >= 128)
+        hipLaunchKernelGGL((k_smooth<false, true>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg,
+                           sweeps, rdt, omega, H);
     else
-        hipLaunchKernelGGL(k_smooth<false>, dim3(grid_for(npairs)), dim3(kBlock), 0, s, src, L.T, L.TNN, L.RHS,
-                           L.stc, L.pitch, npairs, log2i(L.nsub), sweeps, rdt, omega);
+        hipLaunchKernelGGL((k_smooth<false, false>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg,
+                           sweeps, rdt, omega, H);
     return hipGetLastError();
 }
 
@@ -392,18 +518,36 @@ hipError_t launch_residual(hipStream_t s, const Level &L, double rdt) {
     return hipGetLastError();
 }
 
+// tile of whole un_eles with at least 1024 fine sub-elements; LDS = 3 * TF * 8 B (<= 96 KiB)
+inline int tile_log2_for(int nsub_f) { const int lg = log2i(nsub_f); return lg > 10 ? lg : 10; }
+
 hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U) {
     (void)U;
     if (coarse.N == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_restrict, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.RES, coarse.RHS,
-                       fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub));
+    if (fine.nsub <= 4096) {
+        const int tl = tile_log2_for(fine.nsub);
+        const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
+        hipLaunchKernelGGL(k_restrict_tile, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.RES, coarse.RHS,
+                           fine.children, fine.pitch, coarse.pitch, fine.N, log2i(fine.nsub), tl);
+    } else {
+        hipLaunchKernelGGL(k_restrict, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.RES, coarse.RHS,
+                           fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub));
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn) {
     if (coarse.N == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prolong, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.T, fine.TNN, coarse.T,
-                       fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub), write_tnn ? 1 : 0);
+    if (fine.nsub <= 4096) {
+        const int tl = tile_log2_for(fine.nsub);
+        const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
+        hipLaunchKernelGGL(k_prolong_tile, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.T, fine.TNN,
+                           coarse.T, fine.children, fine.pitch, coarse.pitch, fine.N, log2i(fine.nsub), tl,
+                           write_tnn ? 1 : 0);
+    } else {
+        hipLaunchKernelGGL(k_prolong, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.T, fine.TNN, coarse.T,
+                           fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub), write_tnn ? 1 : 0);
+    }
     return hipGetLastError();
 }
 
@@ -414,20 +558,19 @@ hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double 
     return hipGetLastError();
 }
 
-hipError_t launch_halo(hipStream_t s, const Level &L, double *tov, double *tovo) {
-    const HaloPlan &P = L.halo;
-    const int n = (int)(P.local.size() + P.bc.size() + P.remote.size());
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_halo, dim3(grid_for(n)), dim3(kBlock), 0, s, L.T, L.TOLD, L.pitch, tov, tovo, P.d_local,
-                       (int)P.local.size(), P.d_bc, (int)P.bc.size(), P.d_remote, (int)P.remote.size(), P.d_send);
-    return hipGetLastError();
-}
-
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo) {
     const HaloPlan &P = L.halo;
     const int n = (int)P.recv_dst.size();
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_halo_unpack, dim3(grid_for(n)), dim3(kBlock), 0, s, P.d_recv, P.d_recv_dst, n, tov, tovo);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n) {
+    const int64_t n2 = n / 2;   // planes are multiples of 64 doubles
+    if (n2 == 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>((n2 + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(k_copy, dim3(g), dim3(kBlock), 0, s, src, dst, n2);
     return hipGetLastError();
 }
 

@@ -159,9 +159,18 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
     HaloPlan &P = L.halo;
     P.local.clear(); P.bc.clear(); P.remote.clear(); P.recv_dst.clear();
     P.peers.clear(); P.send_peer_off.clear(); P.recv_peer_off.clear();
+    P.hface.assign((size_t)h->U * 3, make_int4(0, 0, 0, 0));
+    P.bcv.clear();
     const int is = L.isplit, m = 1 << is, sl = h->slots;
     std::vector<int> surf;
     loc_surf_ele(is, surf);
+    P.hsub.assign(L.nsub, make_int4(0, 0, 0, 0));
+    for (int f = 1; f <= 3; ++f)
+        for (int i = 1; i <= m; ++i) {
+            int4 &e = P.hsub[surf[(i - 1) + (f - 1) * m] - 1];
+            (f == 1 ? e.x : f == 2 ? e.y : e.z) = i;
+        }
+    std::vector<std::pair<int, int>> remote_block((size_t)h->U * 3, std::make_pair(-1, -1));   // (peer, first index)
     const bool dist = !h->owner.empty();
     std::vector<int> g2l;   // global -> local index (or -1)
     if (dist) {
@@ -180,6 +189,10 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
                 const int se = surf[(i - 1) + (f - 1) * m];
                 int irow, ipos, orient;
                 get_str_info(is, se, &irow, &ipos, &orient);
+                if ((f == 1 && (irow != 1 || ipos != 2 * i - 1)) || (f != 1 && irow != i)) {
+                    h->err = "halo: unexpected boundary sub-element numbering";
+                    return PAMG_ERR_STATE;
+                }
                 const int npos = neig[3 * (size_t)ug + f - 1];
                 const int src = q * L.nsub + se - 1;
                 if (npos == 0) {
@@ -195,7 +208,9 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
                     e.dst_b = base + b - 1;
                     e.val_a = std::sin(xl[na][0] + xl[na][1]);   // boundary(), splitting.F90:1401-1405
                     e.val_b = std::sin(xl[nb][0] + xl[nb][1]);
+                    if (i == 1) P.hface[3 * (size_t)q + f - 1] = make_int4(0, base, (int)P.bc.size(), 0);
                     P.bc.push_back(e);
+                    P.bcv.push_back(make_double2(e.val_a, e.val_b));
                 } else {
                     const int nside = fneig[3 * (size_t)ug + f - 1];
                     const int dr = dir[3 * (size_t)ug + f - 1];
@@ -210,10 +225,19 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
                     const int kslot = (nside == 2) ? (dr ? rev : fwd) : (dr ? fwd : rev);
                     const int ng = npos - 1;
                     const int off_in_elem = (nside - 1) * sl + kslot * 3 - 3;
+                    // kslot is i or m - i + 1 (surf_ele(i, f) sits at ipos = 2i-1 on face 1 and in row i on faces 2, 3)
+                    const int rev_flag = (kslot == i) ? 0 : 1;
+                    if (kslot != i && kslot != m - i + 1) { h->err = "halo: slot map"; return PAMG_ERR_STATE; }
                     if (!dist || h->owner[ng] == h->rank) {
                         const int nl = dist ? g2l[ng] : ng;
+                        if (i == 1)
+                            P.hface[3 * (size_t)q + f - 1] = make_int4(1 | (rev_flag << 2), nl * sl * 3 + (nside - 1) * sl, 0, 0);
                         P.local.push_back(HaloCopy{src, nl * sl * 3 + off_in_elem});
                     } else {
+                        if (i == 1) {
+                            remote_block[3 * (size_t)q + f - 1] = std::make_pair(h->owner[ng], (int)by_peer[h->owner[ng]].size());
+                            P.hface[3 * (size_t)q + f - 1] = make_int4(2, 0, 0, 0);
+                        }
                         by_peer[h->owner[ng]].push_back(HaloCopy{src, off_in_elem});
                     }
                 }
@@ -252,11 +276,10 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
             }
             if (!has_send && rd.empty()) continue;
             P.peers.push_back(r);
-            for (auto &e : by_peer[r]) {
-                HaloCopy c{e.src, (int)P.remote.size()};
-                (void)c;
-                P.remote.push_back(HaloCopy{e.src, (int)P.remote.size()});
-            }
+            const int first = (int)P.remote.size();
+            for (size_t b = 0; b < remote_block.size(); ++b)
+                if (remote_block[b].first == r) P.hface[b].z = first + remote_block[b].second;
+            for (auto &e : by_peer[r]) P.remote.push_back(HaloCopy{e.src, (int)P.remote.size()});
             P.send_peer_off.push_back((int)P.remote.size());
             if (P.recv_peer_off.empty()) P.recv_peer_off.push_back(0);
             P.recv_dst.insert(P.recv_dst.end(), rd.begin(), rd.end());

@@ -17,6 +17,7 @@ program pamg_transport
   use iso_c_binding
   use pamg
   use LinearSolvers, only: MeshRec => Mesh, pamg_bind_handle, GSsolver_MeshSD
+  use pamg_dump, only: write_dump
   implicit none
 
   character(len=512) :: mesh_file = 'untitled8.msh', dump = ''
@@ -115,55 +116,7 @@ program pamg_transport
   print *, '|        cpu_time for time_loop = ', real(c1 - c0, 8) / real(crate, 8), '|'
   print *, '----------------------------------------------------------'
 
-  if (len_trim(dump) > 0) call write_dump(trim(dump))
+  if (len_trim(dump) > 0) call write_dump(h, trim(dump), int(U), n_split, multi_levels)
   call pamg_check(pamg_destroy(h), c_null_ptr, 'pamg_destroy')
-
-contains
-
-  ! PAMGREC1 records, same names and layout as oracle/ref_hooks/pamg_ref_hooks.F90
-  subroutine rec(u, name, a, dims)
-    integer, intent(in) :: u
-    character(len=*), intent(in) :: name
-    real(8), intent(in) :: a(:)
-    integer(8), intent(in) :: dims(:)
-    write(u) 'PAMGREC1'
-    write(u) int(len_trim(name), 4)
-    write(u) trim(name)
-    write(u) 1_4
-    write(u) int(size(dims), 4)
-    write(u) dims
-    write(u) a
-  end subroutine rec
-
-  subroutine write_dump(fn)
-    character(len=*), intent(in) :: fn
-    integer :: u, l, nsub
-    real(c_double), allocatable :: a(:), b(:)
-    character(len=32) :: nm
-    integer, parameter :: what(4) = [PAMG_TNEW, PAMG_TOLD, PAMG_RHS, PAMG_RESIDUAL]
-    character(len=4), parameter :: names(4) = ['tnew', 'told', 'RHS ', 'res ']
-    integer :: q
-    open(newunit=u, file=fn, access='stream', form='unformatted', status='replace')
-    do l = 1, multi_levels
-      nsub = 4**(n_split - l + 1)
-      allocate(a(3*nsub*U))
-      do q = 1, 4
-        call pamg_check(pamg_get_state(h, int(l, c_int), int(what(q), c_int), a), h, 'get_state')
-        write(nm, '(a,a,i0)') trim(names(q)), '_L', l
-        call rec(u, trim(nm), a, [3_8, int(nsub, 8), int(U, 8)])
-      end do
-      deallocate(a)
-    end do
-    ! at the end of the time loop tnew_nonlin holds level 1 (last smoother call, :376)
-    allocate(a(3*4**n_split*U))
-    call pamg_check(pamg_get_state(h, 1_c_int, int(PAMG_TNEW_NONLIN, c_int), a), h, 'get_state')
-    call rec(u, 'tnew_nonlin', a, [3_8, int(4**n_split, 8), int(U, 8)])
-    deallocate(a)
-    allocate(a(2**n_split*3*3*U), b(2**n_split*3*3*U))
-    call pamg_check(pamg_get_overlap(h, a, b), h, 'get_overlap')
-    call rec(u, 't_overlap', a, [int(2**n_split*3, 8), 3_8, int(U, 8)])
-    call rec(u, 't_overlap_old', b, [int(2**n_split*3, 8), 3_8, int(U, 8)])
-    close(u)
-  end subroutine write_dump
 
 end program pamg_transport
