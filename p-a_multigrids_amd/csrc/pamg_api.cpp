@@ -199,6 +199,28 @@ int rhs_level1(pamg_handle *h, bool start_of_step) {
     return PAMG_OK;
 }
 
+int residual(pamg_handle *h, int l);
+int restrict_(pamg_handle *h, int l);
+
+// told changed on level l: refresh the compact told copy the halo reads
+int refresh_told_halo(pamg_handle *h, int l) {
+    HIPCHK(h, launch_told_halo(h->stream, h->lv[l], h->U));
+    return PAMG_OK;
+}
+
+// restrictor(l) + get_residual(l) as one kernel (V-cycle driver)
+int restrict_residual(pamg_handle *h, int l) {
+    Level &L = h->lv[l];
+    if (l >= h->p.multi_levels || L.nsub > 4096) {
+        CHK(restrict_(h, l));
+        return residual(h, l);
+    }
+    if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, false));   // get_RHS inside get_residual (:865-867)
+    Span sp(h, PAMG_K_RESIDUAL, 102.0 * (double)L.N + 168.0 * h->U);
+    HIPCHK(h, launch_restrict_residual(h->stream, L, h->lv[l + 1], 1 / h->p.dt));
+    return PAMG_OK;
+}
+
 int residual(pamg_handle *h, int l) {
     Level &L = h->lv[l];
     if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, false));   // get_RHS inside get_residual (:865-867)
@@ -226,8 +248,7 @@ int vcycle_once(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     for (int l = 1; l <= L; ++l) {           // :323-340
         CHK(smooth(h, l, true, ns));
-        CHK(restrict_(h, l));
-        CHK(residual(h, l));
+        CHK(restrict_residual(h, l));
     }
     CHK(smooth(h, L, true, ns * h->p.n_coarse));   // :344-359
     for (int l = L - 1; l >= 1; --l) {             // :363-378
@@ -244,6 +265,7 @@ void free_levels(pamg_handle *h) {
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_recv);
         dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
+        dev_free(L.halo.d_surf); dev_free(L.halo.d_told_halo);
         L = Level();
     }
     dev_free(h->geo1); dev_free(h->tov); dev_free(h->tovo);
@@ -408,6 +430,9 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         CHK(dev_upload(h, &P.d_hface, P.hface));
         CHK(dev_upload(h, &P.d_hsub, P.hsub));
         CHK(dev_upload(h, &P.d_bcv, P.bcv));
+        CHK(dev_upload(h, &P.d_surf, P.surf));
+        CHK(dev_alloc(h, &P.d_told_halo, 3 * (size_t)P.n_told));
+        CHK(refresh_told_halo(h, l));
         CHK(dev_alloc(h, &P.d_send, 6 * P.remote.size()));
         CHK(dev_alloc(h, &P.d_recv, 6 * P.recv_dst.size()));
     }
@@ -452,6 +477,7 @@ int pamg_set_state(pamg_handle *h, int level, int what, const double *host) {
     CHK(ensure_scratch(h, 3 * (size_t)L.N * sizeof(double)));
     HIPCHK(h, hipMemcpyAsync(h->scratch, host, 3 * (size_t)L.N * sizeof(double), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, launch_to_soa(h->stream, h->scratch, dst, L.N, L.pitch));
+    if (what == PAMG_TOLD) CHK(refresh_told_halo(h, level));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return PAMG_OK;
 }
@@ -487,9 +513,10 @@ int pamg_begin_timestep(pamg_handle *h) {
         Level &L = h->lv[1];
         HIPCHK(h, launch_copy(h->stream, L.T, L.TOLD, 3 * L.pitch));
         HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
-        return PAMG_OK;
+        return refresh_told_halo(h, 1);
     }
-    return rhs_level1(h, true);
+    CHK(rhs_level1(h, true));
+    return refresh_told_halo(h, 1);
 }
 
 int pamg_copy_to_nonlin(pamg_handle *h, int level) {

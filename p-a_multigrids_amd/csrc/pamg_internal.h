@@ -46,8 +46,12 @@ struct HaloPlan {
     std::vector<int4> hface;              // (U*3) {mode | rev << 2, dst base, aux, 0}; mode 0 BC, 1 local, 2 remote
     std::vector<int4> hsub;               // (nsub) position i (1-based, 0 = none) along faces 1, 2, 3
     std::vector<double2> bcv;             // BC values sin(x+y) at the two face nodes, (u, f, i) order
+    std::vector<int> surf;                // surf_ele(i, f) of loc_surf_ele_multigrid, (m, 3), 1-based
+    int n_told = 0;                       // entries of the told halo (3 fp64 each); hface.w = first entry
     int4 *d_hface = nullptr, *d_hsub = nullptr;
     double2 *d_bcv = nullptr;
+    int *d_surf = nullptr;
+    double *d_told_halo = nullptr;        // told values of the copied sub-elements, refreshed when told changes
     // device copies
     HaloCopy *d_local = nullptr, *d_remote = nullptr;
     HaloBC *d_bc = nullptr;
@@ -125,6 +129,8 @@ hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse,
 hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, bool start_of_step);
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
 hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
+hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);
+hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch);
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt);

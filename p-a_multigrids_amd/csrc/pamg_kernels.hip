@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "pamg_internal.h"
 
@@ -66,7 +67,7 @@ struct HaloArgs {
     const int4 *hsub;     // per sub-element: position along faces 1, 2, 3 (0 = none)
     const int4 *hface;    // per (un_ele, face): {mode | rev << 2, dst base, aux, 0}
     const double2 *bcv;   // boundary values sin(x + y) at the two face nodes
-    const double *TOLD;
+    const double *told;   // told values of the copied sub-elements (3 per entry, hface.w = first entry)
     double *tov, *tovo, *send;
     int m;                // 2**i_split sub-elements per face
 };
@@ -74,10 +75,9 @@ struct HaloArgs {
 // The reference rewrites the halo at the start of every sweep from the then
 // current tnew (:550-556); the last write of a smoother call therefore carries
 // the iterate before the last sweep, which is what these threads hold in p[].
-__device__ __forceinline__ void halo_face(const HaloArgs &H, int64_t u, int f, int i, double t0, double t1,
-                                          double t2, int64_t s, int64_t pitch) {
-    const double t[3] = {t0, t1, t2};
-    const int4 rec = H.hface[3 * u + f - 1];
+// The halo metadata (face positions, face records, told) is fetched before the
+// sweeps so its latency hides under the arithmetic.
+__device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, int i, const double t[3]) {
     const int mode = rec.x & 3;
     if (mode == 0) {   // domain boundary: BC values into the own column (:1243-1252, :1287-1295, :1345-1353)
         const int a = (i - 1) * 3 + (f == 3 ? 1 : 0);
@@ -89,29 +89,65 @@ __device__ __forceinline__ void halo_face(const HaloArgs &H, int64_t u, int f, i
         H.tovo[rec.y + b] = v.y;
         return;
     }
-    double to[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) to[c] = H.TOLD[c * pitch + s];
+    // told is constant within a time step: its halo words come from a compact
+    // per-entry copy refreshed whenever told changes (k_told_halo)
+    const double *to = H.told + 3 * (int64_t)(rec.w + i - 1);
     if (mode == 1) {   // neighbour on this rank: t_overlap(slot, Nside) of the neighbour
         const int k = (rec.x >> 2) ? (H.m - i + 1) : i;
         const int64_t d = rec.y + (int64_t)(k - 1) * 3;
 #pragma unroll
         for (int c = 0; c < 3; ++c) { H.tov[d + c] = t[c]; H.tovo[d + c] = to[c]; }
-    } else {           // neighbour on another rank: packed send buffer (RCCL)
+    } else {                  // neighbour on another rank: packed send buffer (RCCL)
         double *o = H.send + 6 * (int64_t)(rec.z + i - 1);
 #pragma unroll
         for (int c = 0; c < 3; ++c) { o[c] = t[c]; o[3 + c] = to[c]; }
     }
 }
 
-__device__ __forceinline__ void halo_sub(const HaloArgs &H, int64_t s, int nsub_log2, double t0, double t1,
-                                         double t2, int64_t pitch) {
-    const int4 hs = H.hsub[s & ((1ll << nsub_log2) - 1)];
-    if ((hs.x | hs.y | hs.z) == 0) return;
-    const int64_t u = s >> nsub_log2;
-    if (hs.x) halo_face(H, u, 1, hs.x, t0, t1, t2, s, pitch);
-    if (hs.y) halo_face(H, u, 2, hs.y, t0, t1, t2, s, pitch);
-    if (hs.z) halo_face(H, u, 3, hs.z, t0, t1, t2, s, pitch);
+struct HaloPre {
+    int4 hs0, hs1;        // face positions of the two sub-elements
+    int4 rec[3];          // face records of the un_ele
+    bool any;
+};
+
+__device__ __forceinline__ void halo_prefetch(const HaloArgs &H, int64_t s, int64_t u, int nsub_log2, HaloPre &P) {
+    const int64_t sub = s & ((1ll << nsub_log2) - 1);
+    P.hs0 = H.hsub[sub];
+    P.hs1 = H.hsub[sub + 1];
+    P.any = (P.hs0.x | P.hs0.y | P.hs0.z | P.hs1.x | P.hs1.y | P.hs1.z) != 0;
+    if (P.any) {
+#pragma unroll
+        for (int f = 0; f < 3; ++f) P.rec[f] = H.hface[3 * u + f];
+    }
+}
+
+__device__ __forceinline__ void halo_write(const HaloArgs &H, const HaloPre &P, const double p0[3],
+                                           const double p1[3]) {
+    if (!P.any) return;
+    if (P.hs0.x) halo_face(H, P.rec[0], 1, P.hs0.x, p0);
+    if (P.hs0.y) halo_face(H, P.rec[1], 2, P.hs0.y, p0);
+    if (P.hs0.z) halo_face(H, P.rec[2], 3, P.hs0.z, p0);
+    if (P.hs1.x) halo_face(H, P.rec[0], 1, P.hs1.x, p1);
+    if (P.hs1.y) halo_face(H, P.rec[1], 2, P.hs1.y, p1);
+    if (P.hs1.z) halo_face(H, P.rec[2], 3, P.hs1.z, p1);
+}
+
+// Gather of told at the halo's copied sub-elements (entry order (u, f, i)),
+// run when told changes (time-step start, set_state), not per smoother call.
+__global__ __launch_bounds__(kBlock) void k_told_halo(const double *__restrict__ TOLD, int64_t pitch,
+                                                      const int4 *__restrict__ hface, const int *__restrict__ surf,
+                                                      double *__restrict__ out, int U, int m, int nsub_log2) {
+    const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= (int64_t)U * 3 * m) return;
+    const int i = (int)(idx % m) + 1;
+    const int f = (int)((idx / m) % 3) + 1;
+    const int64_t q = idx / (3 * m);
+    const int4 rec = hface[3 * q + f - 1];
+    if ((rec.x & 3) == 0) return;
+    const int64_t s = (q << nsub_log2) + surf[(i - 1) + (f - 1) * m] - 1;
+    double *o = out + 3 * (int64_t)(rec.w + i - 1);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = TOLD[c * pitch + s];
 }
 
 // Fused smoother call(s): `sweeps` consecutive sweeps kept in registers.
@@ -129,12 +165,17 @@ __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T,
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= npairs) return;
     const int64_t s = 2 * p;
+    int64_t u = s >> nsub_log2;
+    if (UNIFORM) u = __builtin_amdgcn_readfirstlane((int)u);
     double2 xv[3], bv[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         xv[c] = ld2(src + c * pitch + s);
         bv[c] = ld2(RHS + c * pitch + s);
     }
+    HaloPre hp;
+    hp.any = false;
+    if (H.hsub) halo_prefetch(H, s, u, nsub_log2, hp);
     double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
     const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
     double p0[3] = {x0[0], x0[1], x0[2]}, p1[3] = {x1[0], x1[1], x1[2]};
@@ -149,8 +190,6 @@ __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T,
             }
         }
     } else {
-        int64_t u = s >> nsub_log2;
-        if (UNIFORM) u = __builtin_amdgcn_readfirstlane((int)u);
         Stc S;
         load_stc(stc + u * kStcStride, S);
         for (int it = 0; it < sweeps; ++it) {
@@ -165,10 +204,7 @@ __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T,
         st2(T + c * pitch + s, make_double2(p0[c], p1[c]));
         st2(TNN + c * pitch + s, make_double2(x0[c], x1[c]));
     }
-    if (H.hsub) {
-        halo_sub(H, s, nsub_log2, p0[0], p0[1], p0[2], pitch);
-        halo_sub(H, s + 1, nsub_log2, p1[0], p1[1], p1[2], pitch);
-    }
+    halo_write(H, hp, p0, p1);
 }
 
 // get_residual (:725-873): residuale = A x - RHS (note the sign, :869).
@@ -392,6 +428,59 @@ __global__ __launch_bounds__(kBlock) void k_restrict_tile(const double *__restri
     }
 }
 
+// restrictor(l) followed by get_residual(l) (:336, :338) in one pass over a
+// tile of whole un_eles: the previous cycle's residual is staged in LDS and
+// restricted into RHS_{l+1}; then the new residual A tnew - RHS overwrites it.
+template <bool UNIFORM>
+__global__ __launch_bounds__(kBlock) void k_restrict_residual(const double *__restrict__ T,
+                                                              const double *__restrict__ RHS, double *RES,
+                                                              double *__restrict__ RHSc,
+                                                              const double *__restrict__ stc,
+                                                              const int4 *__restrict__ children, int64_t pitch_f,
+                                                              int64_t pitch_c, int64_t Nf, int nsubf_log2,
+                                                              int tile_log2, double rdt) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int TF = 1 << tile_log2;
+    const int64_t f0 = (int64_t)blockIdx.x << tile_log2;
+    const int nf = (int)min((int64_t)TF, Nf - f0);
+    for (int j = 2 * threadIdx.x; j < nf; j += 2 * kBlock)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            *reinterpret_cast<double2 *>(&lds[c * TF + j]) = ld2(RES + c * pitch_f + f0 + j);
+    __syncthreads();
+    const int nsubc_log2 = nsubf_log2 - 2;
+    const int64_t c0 = f0 >> 2;
+    for (int cc = threadIdx.x; cc < (nf >> 2); cc += kBlock) {
+        const int c = (int)((c0 + cc) & ((1ll << nsubc_log2) - 1));
+        const int base = (cc >> nsubc_log2) << nsubf_log2;
+        const int4 ch = children[c];
+        const int pick[3] = {base + ch.z, base + ch.w, base + ch.x};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            RHSc[i * pitch_c + c0 + cc] = (lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]) / 3.;
+    }
+    for (int j = 2 * threadIdx.x; j < nf; j += 2 * kBlock) {
+        const int64_t s = f0 + j;
+        int64_t u = s >> nsubf_log2;
+        if (UNIFORM) u = __builtin_amdgcn_readfirstlane((int)u);
+        double2 xv[3], bv[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            xv[c] = ld2(T + c * pitch_f + s);
+            bv[c] = ld2(RHS + c * pitch_f + s);
+        }
+        Stc S;
+        load_stc(stc + u * kStcStride, S);
+        const double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
+        double A0[3], A1[3];
+        apply_A(S, rdt, x0, A0);
+        apply_A(S, rdt, x1, A1);
+        const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
+#pragma unroll
+        for (int c = 0; c < 3; ++c) st2(RES + c * pitch_f + s, make_double2(A0[c] - b0[c], A1[c] - b1[c]));
+    }
+}
+
 // Unpack of the halo words received from other ranks (RCCL) into t_overlap.
 __global__ __launch_bounds__(kBlock) void k_halo_unpack(const double *__restrict__ recv, const int *__restrict__ dst,
                                                         int n, double *__restrict__ tov, double *__restrict__ tovo) {
@@ -495,13 +584,16 @@ hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int s
     const int64_t npairs = L.N / 2;
     if (npairs == 0 || sweeps <= 0) return hipSuccess;
     const HaloPlan &P = L.halo;
-    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, L.TOLD, tov, tovo, P.d_send, 1 << L.isplit};
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << L.isplit};
+    static const bool diag_nohalo = getenv("PAMG_DIAG_NOHALO") != nullptr;       // diagnostics only:
+    static const bool diag_nouniform = getenv("PAMG_DIAG_NOUNIFORM") != nullptr;  // A/B of the fused forms
+    if (diag_nohalo) H.hsub = nullptr;
     const int lg = log2i(L.nsub);
     const dim3 g(grid_for(npairs)), b(kBlock);
     if (solver == 2)
         hipLaunchKernelGGL((k_smooth<true, false>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg,
                            sweeps, rdt, omega, H);
-    else if (L.nsub >= 128)
+    else if (L.nsub >= 128 && !diag_nouniform)
         hipLaunchKernelGGL((k_smooth<false, true>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg,
                            sweeps, rdt, omega, H);
     else
@@ -533,6 +625,21 @@ hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse
         hipLaunchKernelGGL(k_restrict, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.RES, coarse.RHS,
                            fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub));
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt) {
+    if (fine.N == 0) return hipSuccess;
+    const int tl = tile_log2_for(fine.nsub);
+    const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
+    if (fine.nsub >= 128)
+        hipLaunchKernelGGL(k_restrict_residual<true>, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.T,
+                           fine.RHS, fine.RES, coarse.RHS, fine.stc, fine.children, fine.pitch, coarse.pitch, fine.N,
+                           log2i(fine.nsub), tl, rdt);
+    else
+        hipLaunchKernelGGL(k_restrict_residual<false>, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.T,
+                           fine.RHS, fine.RES, coarse.RHS, fine.stc, fine.children, fine.pitch, coarse.pitch, fine.N,
+                           log2i(fine.nsub), tl, rdt);
     return hipGetLastError();
 }
 
@@ -571,6 +678,15 @@ hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n)
     if (n2 == 0) return hipSuccess;
     const unsigned g = (unsigned)std::min<int64_t>((n2 + kBlock - 1) / kBlock, 8192);
     hipLaunchKernelGGL(k_copy, dim3(g), dim3(kBlock), 0, s, src, dst, n2);
+    return hipGetLastError();
+}
+
+hipError_t launch_told_halo(hipStream_t s, const Level &L, int U) {
+    const HaloPlan &P = L.halo;
+    if (P.n_told == 0 || U == 0) return hipSuccess;
+    const int m = 1 << L.isplit;
+    hipLaunchKernelGGL(k_told_halo, dim3(grid_for((int64_t)U * 3 * m)), dim3(kBlock), 0, s, L.TOLD, L.pitch,
+                       P.d_hface, P.d_surf, P.d_told_halo, U, m, log2i(L.nsub));
     return hipGetLastError();
 }
 

@@ -162,8 +162,9 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
     P.hface.assign((size_t)h->U * 3, make_int4(0, 0, 0, 0));
     P.bcv.clear();
     const int is = L.isplit, m = 1 << is, sl = h->slots;
-    std::vector<int> surf;
+    std::vector<int> &surf = P.surf;
     loc_surf_ele(is, surf);
+    P.n_told = 0;
     P.hsub.assign(L.nsub, make_int4(0, 0, 0, 0));
     for (int f = 1; f <= 3; ++f)
         for (int i = 1; i <= m; ++i) {
@@ -230,13 +231,17 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
                     if (kslot != i && kslot != m - i + 1) { h->err = "halo: slot map"; return PAMG_ERR_STATE; }
                     if (!dist || h->owner[ng] == h->rank) {
                         const int nl = dist ? g2l[ng] : ng;
-                        if (i == 1)
-                            P.hface[3 * (size_t)q + f - 1] = make_int4(1 | (rev_flag << 2), nl * sl * 3 + (nside - 1) * sl, 0, 0);
+                        if (i == 1) {
+                            P.hface[3 * (size_t)q + f - 1] =
+                                make_int4(1 | (rev_flag << 2), nl * sl * 3 + (nside - 1) * sl, 0, P.n_told);
+                            P.n_told += m;
+                        }
                         P.local.push_back(HaloCopy{src, nl * sl * 3 + off_in_elem});
                     } else {
                         if (i == 1) {
                             remote_block[3 * (size_t)q + f - 1] = std::make_pair(h->owner[ng], (int)by_peer[h->owner[ng]].size());
-                            P.hface[3 * (size_t)q + f - 1] = make_int4(2, 0, 0, 0);
+                            P.hface[3 * (size_t)q + f - 1] = make_int4(2, 0, 0, P.n_told);
+                            P.n_told += m;
                         }
                         by_peer[h->owner[ng]].push_back(HaloCopy{src, off_in_elem});
                     }
