@@ -211,7 +211,7 @@ int refresh_told_halo(pamg_handle *h, int l) {
 // restrictor(l) + get_residual(l) as one kernel (V-cycle driver)
 int restrict_residual(pamg_handle *h, int l) {
     Level &L = h->lv[l];
-    if (l >= h->p.multi_levels || L.nsub > 4096) {
+    if (l >= h->p.multi_levels || L.nsub > 1024) {
         CHK(restrict_(h, l));
         return residual(h, l);
     }

@@ -77,7 +77,8 @@ struct HaloArgs {
 // the iterate before the last sweep, which is what these threads hold in p[].
 // The halo metadata (face positions, face records, told) is fetched before the
 // sweeps so its latency hides under the arithmetic.
-__device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, int i, const double t[3]) {
+__device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, int i, const double t[3],
+                                          const double to[3]) {
     const int mode = rec.x & 3;
     if (mode == 0) {   // domain boundary: BC values into the own column (:1243-1252, :1287-1295, :1345-1353)
         const int a = (i - 1) * 3 + (f == 3 ? 1 : 0);
@@ -87,12 +88,7 @@ __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, in
         H.tov[rec.y + b] = v.y;
         H.tovo[rec.y + a] = v.x;
         H.tovo[rec.y + b] = v.y;
-        return;
-    }
-    // told is constant within a time step: its halo words come from a compact
-    // per-entry copy refreshed whenever told changes (k_told_halo)
-    const double *to = H.told + 3 * (int64_t)(rec.w + i - 1);
-    if (mode == 1) {   // neighbour on this rank: t_overlap(slot, Nside) of the neighbour
+    } else if (mode == 1) {   // neighbour on this rank: t_overlap(slot, Nside) of the neighbour
         const int k = (rec.x >> 2) ? (H.m - i + 1) : i;
         const int64_t d = rec.y + (int64_t)(k - 1) * 3;
 #pragma unroll
@@ -105,31 +101,46 @@ __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, in
 }
 
 struct HaloPre {
-    int4 hs0, hs1;        // face positions of the two sub-elements
-    int4 rec[3];          // face records of the un_ele
+    int4 hs0, hs1;              // face positions of the two sub-elements
+    int4 r1, r2, r3;            // face records (faces 1, 2, 3) of the un_ele
+    double a0, a1, a2, c0, c1, c2;   // told of the two sub-elements (compact told halo)
     bool any;
 };
+
+// entry of the compact told halo holding a boundary sub-element's told (-1: none)
+__device__ __forceinline__ int told_entry(const HaloPre &P, int4 hs) {
+    if (hs.x && (P.r1.x & 3)) return P.r1.w + hs.x - 1;
+    if (hs.y && (P.r2.x & 3)) return P.r2.w + hs.y - 1;
+    if (hs.z && (P.r3.x & 3)) return P.r3.w + hs.z - 1;
+    return -1;
+}
 
 __device__ __forceinline__ void halo_prefetch(const HaloArgs &H, int64_t s, int64_t u, int nsub_log2, HaloPre &P) {
     const int64_t sub = s & ((1ll << nsub_log2) - 1);
     P.hs0 = H.hsub[sub];
     P.hs1 = H.hsub[sub + 1];
     P.any = (P.hs0.x | P.hs0.y | P.hs0.z | P.hs1.x | P.hs1.y | P.hs1.z) != 0;
+    P.a0 = P.a1 = P.a2 = P.c0 = P.c1 = P.c2 = 0.0;
     if (P.any) {
-#pragma unroll
-        for (int f = 0; f < 3; ++f) P.rec[f] = H.hface[3 * u + f];
+        P.r1 = H.hface[3 * u];
+        P.r2 = H.hface[3 * u + 1];
+        P.r3 = H.hface[3 * u + 2];
+        const int e0 = told_entry(P, P.hs0), e1 = told_entry(P, P.hs1);
+        if (e0 >= 0) { P.a0 = H.told[3 * (int64_t)e0]; P.a1 = H.told[3 * (int64_t)e0 + 1]; P.a2 = H.told[3 * (int64_t)e0 + 2]; }
+        if (e1 >= 0) { P.c0 = H.told[3 * (int64_t)e1]; P.c1 = H.told[3 * (int64_t)e1 + 1]; P.c2 = H.told[3 * (int64_t)e1 + 2]; }
     }
 }
 
 __device__ __forceinline__ void halo_write(const HaloArgs &H, const HaloPre &P, const double p0[3],
                                            const double p1[3]) {
     if (!P.any) return;
-    if (P.hs0.x) halo_face(H, P.rec[0], 1, P.hs0.x, p0);
-    if (P.hs0.y) halo_face(H, P.rec[1], 2, P.hs0.y, p0);
-    if (P.hs0.z) halo_face(H, P.rec[2], 3, P.hs0.z, p0);
-    if (P.hs1.x) halo_face(H, P.rec[0], 1, P.hs1.x, p1);
-    if (P.hs1.y) halo_face(H, P.rec[1], 2, P.hs1.y, p1);
-    if (P.hs1.z) halo_face(H, P.rec[2], 3, P.hs1.z, p1);
+    const double t0[3] = {P.a0, P.a1, P.a2}, t1[3] = {P.c0, P.c1, P.c2};
+    if (P.hs0.x) halo_face(H, P.r1, 1, P.hs0.x, p0, t0);
+    if (P.hs0.y) halo_face(H, P.r2, 2, P.hs0.y, p0, t0);
+    if (P.hs0.z) halo_face(H, P.r3, 3, P.hs0.z, p0, t0);
+    if (P.hs1.x) halo_face(H, P.r1, 1, P.hs1.x, p1, t1);
+    if (P.hs1.y) halo_face(H, P.r2, 2, P.hs1.y, p1, t1);
+    if (P.hs1.z) halo_face(H, P.r3, 3, P.hs1.z, p1, t1);
 }
 
 // Gather of told at the halo's copied sub-elements (entry order (u, f, i)),
@@ -431,22 +442,40 @@ __global__ __launch_bounds__(kBlock) void k_restrict_tile(const double *__restri
 // restrictor(l) followed by get_residual(l) (:336, :338) in one pass over a
 // tile of whole un_eles: the previous cycle's residual is staged in LDS and
 // restricted into RHS_{l+1}; then the new residual A tnew - RHS overwrites it.
-template <bool UNIFORM>
+// ITER = tile / 512: every thread issues all its loads (old residual, tnew,
+// RHS) before the tile barrier, so the three streams are in flight together.
+template <bool UNIFORM, int ITER>
 __global__ __launch_bounds__(kBlock) void k_restrict_residual(const double *__restrict__ T,
                                                               const double *__restrict__ RHS, double *RES,
                                                               double *__restrict__ RHSc,
                                                               const double *__restrict__ stc,
                                                               const int4 *__restrict__ children, int64_t pitch_f,
-                                                              int64_t pitch_c, int64_t Nf, int nsubf_log2,
-                                                              int tile_log2, double rdt) {
+                                                              int64_t pitch_c, int64_t Nf, int nsubf_log2, double rdt) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int TF = 1 << tile_log2;
-    const int64_t f0 = (int64_t)blockIdx.x << tile_log2;
+    constexpr int TF = ITER * 2 * kBlock;
+    const int64_t f0 = (int64_t)blockIdx.x * TF;
     const int nf = (int)min((int64_t)TF, Nf - f0);
-    for (int j = 2 * threadIdx.x; j < nf; j += 2 * kBlock)
+    double2 r[ITER][3], x[ITER][3], b[ITER][3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-            *reinterpret_cast<double2 *>(&lds[c * TF + j]) = ld2(RES + c * pitch_f + f0 + j);
+    for (int it = 0; it < ITER; ++it) {
+        const int j = 2 * threadIdx.x + it * 2 * kBlock;
+        if (j < nf) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                r[it][c] = ld2(RES + c * pitch_f + f0 + j);
+                x[it][c] = ld2(T + c * pitch_f + f0 + j);
+                b[it][c] = ld2(RHS + c * pitch_f + f0 + j);
+            }
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const int j = 2 * threadIdx.x + it * 2 * kBlock;
+        if (j < nf) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) *reinterpret_cast<double2 *>(&lds[c * TF + j]) = r[it][c];
+        }
+    }
     __syncthreads();
     const int nsubc_log2 = nsubf_log2 - 2;
     const int64_t c0 = f0 >> 2;
@@ -459,25 +488,21 @@ __global__ __launch_bounds__(kBlock) void k_restrict_residual(const double *__re
         for (int i = 0; i < 3; ++i)
             RHSc[i * pitch_c + c0 + cc] = (lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]) / 3.;
     }
-    for (int j = 2 * threadIdx.x; j < nf; j += 2 * kBlock) {
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const int j = 2 * threadIdx.x + it * 2 * kBlock;
+        if (j >= nf) continue;
         const int64_t s = f0 + j;
         int64_t u = s >> nsubf_log2;
         if (UNIFORM) u = __builtin_amdgcn_readfirstlane((int)u);
-        double2 xv[3], bv[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            xv[c] = ld2(T + c * pitch_f + s);
-            bv[c] = ld2(RHS + c * pitch_f + s);
-        }
         Stc S;
         load_stc(stc + u * kStcStride, S);
-        const double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
+        const double x0[3] = {x[it][0].x, x[it][1].x, x[it][2].x}, x1[3] = {x[it][0].y, x[it][1].y, x[it][2].y};
         double A0[3], A1[3];
         apply_A(S, rdt, x0, A0);
         apply_A(S, rdt, x1, A1);
-        const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
 #pragma unroll
-        for (int c = 0; c < 3; ++c) st2(RES + c * pitch_f + s, make_double2(A0[c] - b0[c], A1[c] - b1[c]));
+        for (int c = 0; c < 3; ++c) st2(RES + c * pitch_f + s, make_double2(A0[c] - b[it][c].x, A1[c] - b[it][c].y));
     }
 }
 
@@ -630,16 +655,17 @@ hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse
 
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt) {
     if (fine.N == 0) return hipSuccess;
-    const int tl = tile_log2_for(fine.nsub);
+    // tiles of 1024 fine sub-elements = whole un_eles (nsub <= 1024; the caller splits larger ones)
+    const int tl = 10;
     const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
-    if (fine.nsub >= 128)
-        hipLaunchKernelGGL(k_restrict_residual<true>, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.T,
-                           fine.RHS, fine.RES, coarse.RHS, fine.stc, fine.children, fine.pitch, coarse.pitch, fine.N,
-                           log2i(fine.nsub), tl, rdt);
-    else
-        hipLaunchKernelGGL(k_restrict_residual<false>, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.T,
-                           fine.RHS, fine.RES, coarse.RHS, fine.stc, fine.children, fine.pitch, coarse.pitch, fine.N,
-                           log2i(fine.nsub), tl, rdt);
+    const size_t lds = (size_t)3 * 8 << tl;
+    const int lg = log2i(fine.nsub);
+#define PAMG_RR(U, IT)                                                                                          \
+    hipLaunchKernelGGL((k_restrict_residual<U, IT>), dim3(grid), dim3(kBlock), lds, s, fine.T, fine.RHS, fine.RES, \
+                       coarse.RHS, fine.stc, fine.children, fine.pitch, coarse.pitch, fine.N, lg, rdt)
+    if (fine.nsub >= 128) PAMG_RR(true, 2);
+    else PAMG_RR(false, 2);
+#undef PAMG_RR
     return hipGetLastError();
 }
 
