@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the n_split=3 and sweep-kernel side measurements")
     ap.add_argument("--halo-mode", type=int, default=0)
+    ap.add_argument("--fused", type=int, default=1, help="1: one fused kernel per V-cycle (default); 0: per-step kernels")
     return ap.parse_args()
 
 
@@ -80,17 +81,22 @@ def cpu_baseline():
                 nsplit3_vcycles_per_s=1.0 / t)
 
 
-def pmc_traffic(nsplit):
-    """HBM bytes per level-1 smoother launch from the committed rocprofv3 PMC
-    summary (profiles/pmc_smooth_l1.json), if one exists for this config."""
-    p = os.path.join(ROOT, "profiles", "pmc_smooth_l1.json")
+def pmc_traffic(kernel, nsplit, levels):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
+    PMC summary (profiles/pmc_<kernel>.json), if one exists for this config."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{kernel.lower()}.json")
     try:
         d = json.load(open(p))
-        if int(d.get("n_split", -1)) == nsplit:
+        if int(d.get("n_split", -1)) == nsplit and int(d.get("levels", levels)) == levels:
             return d.get("hbm_bytes_per_launch")
     except Exception:
         pass
     return None
+
+
+RK_DESC = {"vcycle": "k_vcycle (one launch per V-cycle: every level's smoother, restriction, residual "
+                     "and prolongation in LDS/registers)",
+           "smooth_L1": "k_smooth (level-1 smoother call, n_smooth sweeps fused)"}
 
 
 def main():
@@ -117,11 +123,11 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     device = local % ndev
     s = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
-                                   halo_mode=a.halo_mode, comm=comm)
+                                   halo_mode=a.halo_mode, comm=comm, fused=a.fused)
     s.begin_timestep()
     s.vcycle(a.warmup)
     s.synchronize()
-    s.timing_enable(0x7F)
+    s.timing_enable(0x17F)  # every class but sweep_bench
     s.timing_reset()
 
     def barrier():
@@ -146,11 +152,13 @@ def main():
     value = a.steps / elapsed
     # dominant kernel by total time inside the timed region
     dom = max((k for k in tm if tm[k]["launches"] > 0 and k != "sweep_bench"), key=lambda k: tm[k]["ms"])
-    kinfo = tm["smooth_L1"]
+    # roofline kernel: the fused V-cycle when it ran, else the level-1 smoother
+    rk = "vcycle" if tm["vcycle"]["launches"] else "smooth_L1"
+    kinfo = tm[rk]
     ms_per_launch = kinfo["ms"] / max(1, kinfo["launches"])
     bytes_per_launch = kinfo["bytes"] / max(1, kinfo["launches"])
     achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
-    traffic = pmc_traffic(a.nsplit) if world == 1 else None
+    traffic = pmc_traffic(rk, a.nsplit, a.levels) if world == 1 else None
     extra = {"kernels": {k: dict(ms_total=round(v["ms"], 4), launches=v["launches"],
                                  gbs=round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None)
                          for k, v in tm.items() if v["launches"]},
@@ -162,6 +170,18 @@ def main():
                 ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
                 frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
         s.close()
+        # the same workload through the per-step kernel sequence (bitwise-identical result)
+        su = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
+                                        fused=1 - a.fused)
+        su.begin_timestep()
+        su.vcycle(a.warmup)
+        su.synchronize()
+        t0 = time.perf_counter()
+        su.vcycle(a.steps)
+        su.synchronize()
+        extra["fused0_vcycles_per_s" if a.fused else "fused1_vcycles_per_s"] = round(
+            a.steps / (time.perf_counter() - t0), 2)
+        su.close()
         s3 = pamg.SemiImplicitIterative(mesh, 3, a.levels, n_smooth=a.nsmooth, solver=3, device=device)
         s3.begin_timestep()
         s3.vcycle(a.warmup)
@@ -194,7 +214,7 @@ def main():
                                    f"n_smooth={a.nsmooth} GS, 1 V-cycle per step",
                        "fine_sub_elements": mesh.U * 4 ** a.nsplit, "levels": a.levels,
                        "parallelism": f"dd{world}", "halo_mode": a.halo_mode},
-            "roofline": {"bound": "hbm", "kernel": "k_smooth (level-1 smoother call, n_smooth sweeps fused)",
+            "roofline": {"bound": "hbm", "kernel": RK_DESC[rk],
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "alg_bytes_per_launch": bytes_per_launch, "ms_per_launch": round(ms_per_launch, 4)},

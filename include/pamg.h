@@ -55,7 +55,8 @@ extern "C" {
 #define PAMG_K_RHS 5
 #define PAMG_K_HALO 6
 #define PAMG_K_SWEEP_BENCH 7
-#define PAMG_K_COUNT 8
+#define PAMG_K_VCYCLE 8
+#define PAMG_K_COUNT 9
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;
@@ -73,7 +74,9 @@ typedef struct {
     double theta;     /* time weighting, :117 (only 1.0 is accepted) */
     int halo_mode;    /* 0: halo written once per smoother call (state-identical),
                          1: one launch per sweep, halo at every sweep (reference timing) */
-    int reserved[7];
+    int fused;        /* 1: pamg_vcycle runs each V-cycle as one fused kernel when supported
+                         (solver 1/3, halo_mode 0, n_split <= 5); 0: one kernel per step */
+    int reserved[6];
 } pamg_params;
 
 /* mode-9 defaults of the reference (main.F90:46-47, transport_tri_semi.F90:117-140) */

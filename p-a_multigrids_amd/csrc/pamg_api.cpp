@@ -244,8 +244,31 @@ int prolong(pamg_handle *h, int l, bool fused_copy) {
     return PAMG_OK;
 }
 
+// algorithmic HBM bytes of one fused V-cycle (state traffic)
+double vcycle_bytes(pamg_handle *h) {
+    const int L = h->p.multi_levels;
+    double b = 0;
+    for (int l = 1; l <= L; ++l) {
+        const double N = (double)h->lv[l].N;
+        if (l == 1) b += (L > 1 ? 144.0 : 120.0) * N;
+        else b += (96.0 + (l < L ? 24.0 : 0.0)) * N;
+    }
+    return b + 168.0 * h->U * L;
+}
+
 int vcycle_once(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    if (h->p.fused && vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, ns)) {
+        {
+            Span sp(h, PAMG_K_VCYCLE, vcycle_bytes(h));
+            HIPCHK(h, launch_vcycle(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, 1 / h->p.dt,
+                                    h->tov, h->tovo));
+        }
+        h->tnn_level = 1;
+        // the remote halo words of every smoother call were packed in the kernel; the last
+        // (level-1) pack covers every slot the coarser levels wrote, so one exchange suffices
+        return halo(h, 1);
+    }
     for (int l = 1; l <= L; ++l) {           // :323-340
         CHK(smooth(h, l, true, ns));
         CHK(restrict_residual(h, l));
@@ -292,6 +315,7 @@ void pamg_default_params(pamg_params *p) {
     p->omega = 0.8;          // :140
     p->theta = 1.;           // :117
     p->halo_mode = 0;
+    p->fused = 1;
 }
 
 int pamg_create(const pamg_params *p, pamg_handle **out) {

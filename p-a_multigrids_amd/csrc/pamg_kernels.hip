@@ -19,129 +19,13 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "pamg_device.h"
 #include "pamg_internal.h"
 
 namespace pamg {
 namespace {
 
-constexpr int kBlock = 256;
-
-__device__ __forceinline__ double2 ld2(const double *p) { return *reinterpret_cast<const double2 *>(p); }
-__device__ __forceinline__ void st2(double *p, double2 v) { *reinterpret_cast<double2 *>(p) = v; }
-
-struct Stc {
-    double M[9], K[9], w[3];
-};
-
-__device__ __forceinline__ void load_stc(const double *__restrict__ rec, Stc &S) {
-#pragma unroll
-    for (int q = 0; q < 9; q += 1) S.M[q] = rec[kStcM + q];
-#pragma unroll
-    for (int q = 0; q < 9; q += 1) S.K[q] = rec[kStcK + q];
-#pragma unroll
-    for (int q = 0; q < 3; q += 1) S.w[q] = rec[kStcW + q];
-}
-
-// get_A_x (transport_tri_semi.F90:412-448) with theta = 1 and the zero
-// advection / flux / surface terms folded: A_i = rdt*(M x)_i + (Kd x)_i.
-__device__ __forceinline__ void apply_A(const Stc &S, double rdt, const double x[3], double A[3]) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        double mx = S.M[3 * i] * x[0] + S.M[3 * i + 1] * x[1] + S.M[3 * i + 2] * x[2];
-        double kx = S.K[3 * i] * x[0] + S.K[3 * i + 1] * x[1] + S.K[3 * i + 2] * x[2];
-        A[i] = rdt * mx + kx;
-    }
-}
-
-// One sweep of solve_Gauss_Seidel / solve_Jacobi (:491-507), which coincide
-// for the block-diagonal operator: x_i += (omega / D_i) * (b_i - A_i).
-__device__ __forceinline__ void sweep(const Stc &S, double rdt, const double b[3], double x[3]) {
-    double A[3];
-    apply_A(S, rdt, x, A);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) x[i] = x[i] + S.w[i] * (b[i] - A[i]);
-}
-
-// Halo words written by the smoother (update_overlaps, splitting.F90:1210-1397).
-struct HaloArgs {
-    const int4 *hsub;     // per sub-element: position along faces 1, 2, 3 (0 = none)
-    const int4 *hface;    // per (un_ele, face): {mode | rev << 2, dst base, aux, 0}
-    const double2 *bcv;   // boundary values sin(x + y) at the two face nodes
-    const double *told;   // told values of the copied sub-elements (3 per entry, hface.w = first entry)
-    double *tov, *tovo, *send;
-    int m;                // 2**i_split sub-elements per face
-};
-
-// The reference rewrites the halo at the start of every sweep from the then
-// current tnew (:550-556); the last write of a smoother call therefore carries
-// the iterate before the last sweep, which is what these threads hold in p[].
-// The halo metadata (face positions, face records, told) is fetched before the
-// sweeps so its latency hides under the arithmetic.
-__device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, int i, const double t[3],
-                                          const double to[3]) {
-    const int mode = rec.x & 3;
-    if (mode == 0) {   // domain boundary: BC values into the own column (:1243-1252, :1287-1295, :1345-1353)
-        const int a = (i - 1) * 3 + (f == 3 ? 1 : 0);
-        const int b = (i - 1) * 3 + (f == 2 ? 1 : 2);
-        const double2 v = H.bcv[rec.z + i - 1];
-        H.tov[rec.y + a] = v.x;
-        H.tov[rec.y + b] = v.y;
-        H.tovo[rec.y + a] = v.x;
-        H.tovo[rec.y + b] = v.y;
-    } else if (mode == 1) {   // neighbour on this rank: t_overlap(slot, Nside) of the neighbour
-        const int k = (rec.x >> 2) ? (H.m - i + 1) : i;
-        const int64_t d = rec.y + (int64_t)(k - 1) * 3;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) { H.tov[d + c] = t[c]; H.tovo[d + c] = to[c]; }
-    } else {                  // neighbour on another rank: packed send buffer (RCCL)
-        double *o = H.send + 6 * (int64_t)(rec.z + i - 1);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) { o[c] = t[c]; o[3 + c] = to[c]; }
-    }
-}
-
-struct HaloPre {
-    int4 hs0, hs1;              // face positions of the two sub-elements
-    int4 r1, r2, r3;            // face records (faces 1, 2, 3) of the un_ele
-    double a0, a1, a2, c0, c1, c2;   // told of the two sub-elements (compact told halo)
-    bool any;
-};
-
-// entry of the compact told halo holding a boundary sub-element's told (-1: none)
-__device__ __forceinline__ int told_entry(const HaloPre &P, int4 hs) {
-    if (hs.x && (P.r1.x & 3)) return P.r1.w + hs.x - 1;
-    if (hs.y && (P.r2.x & 3)) return P.r2.w + hs.y - 1;
-    if (hs.z && (P.r3.x & 3)) return P.r3.w + hs.z - 1;
-    return -1;
-}
-
-__device__ __forceinline__ void halo_prefetch(const HaloArgs &H, int64_t s, int64_t u, int nsub_log2, HaloPre &P) {
-    const int64_t sub = s & ((1ll << nsub_log2) - 1);
-    P.hs0 = H.hsub[sub];
-    P.hs1 = H.hsub[sub + 1];
-    P.any = (P.hs0.x | P.hs0.y | P.hs0.z | P.hs1.x | P.hs1.y | P.hs1.z) != 0;
-    P.a0 = P.a1 = P.a2 = P.c0 = P.c1 = P.c2 = 0.0;
-    if (P.any) {
-        P.r1 = H.hface[3 * u];
-        P.r2 = H.hface[3 * u + 1];
-        P.r3 = H.hface[3 * u + 2];
-        const int e0 = told_entry(P, P.hs0), e1 = told_entry(P, P.hs1);
-        if (e0 >= 0) { P.a0 = H.told[3 * (int64_t)e0]; P.a1 = H.told[3 * (int64_t)e0 + 1]; P.a2 = H.told[3 * (int64_t)e0 + 2]; }
-        if (e1 >= 0) { P.c0 = H.told[3 * (int64_t)e1]; P.c1 = H.told[3 * (int64_t)e1 + 1]; P.c2 = H.told[3 * (int64_t)e1 + 2]; }
-    }
-}
-
-__device__ __forceinline__ void halo_write(const HaloArgs &H, const HaloPre &P, const double p0[3],
-                                           const double p1[3]) {
-    if (!P.any) return;
-    const double t0[3] = {P.a0, P.a1, P.a2}, t1[3] = {P.c0, P.c1, P.c2};
-    if (P.hs0.x) halo_face(H, P.r1, 1, P.hs0.x, p0, t0);
-    if (P.hs0.y) halo_face(H, P.r2, 2, P.hs0.y, p0, t0);
-    if (P.hs0.z) halo_face(H, P.r3, 3, P.hs0.z, p0, t0);
-    if (P.hs1.x) halo_face(H, P.r1, 1, P.hs1.x, p1, t1);
-    if (P.hs1.y) halo_face(H, P.r2, 2, P.hs1.y, p1, t1);
-    if (P.hs1.z) halo_face(H, P.r3, 3, P.hs1.z, p1, t1);
-}
+using namespace detail;
 
 // Gather of told at the halo's copied sub-elements (entry order (u, f, i)),
 // run when told changes (time-step start, set_state), not per smoother call.

@@ -18,7 +18,8 @@ module pamg
     integer(c_int) :: n_split, multi_levels, n_smooth, n_coarse, solver, device
     real(c_double) :: dt, k, omega, theta
     integer(c_int) :: halo_mode
-    integer(c_int) :: reserved(7)
+    integer(c_int) :: fused
+    integer(c_int) :: reserved(6)
   end type pamg_params
 
   public :: pamg_default_params, pamg_msh_read, pamg_msh_size, pamg_msh_get, pamg_msh_free

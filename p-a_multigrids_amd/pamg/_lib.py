@@ -17,15 +17,15 @@ ERRORS = {-1: "PAMG_ERR_ARG", -2: "PAMG_ERR_HIP", -3: "PAMG_ERR_IO", -4: "PAMG_E
           -5: "PAMG_ERR_COMM", -6: "PAMG_ERR_NODEV"}
 
 TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN = 0, 1, 2, 3, 4
-K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH = range(8)
-K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench"]
+K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH, K_VCYCLE = range(9)
+K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle"]
 
 
 class PamgParams(C.Structure):
     _fields_ = [("n_split", C.c_int), ("multi_levels", C.c_int), ("n_smooth", C.c_int),
                 ("n_coarse", C.c_int), ("solver", C.c_int), ("device", C.c_int),
                 ("dt", C.c_double), ("k", C.c_double), ("omega", C.c_double), ("theta", C.c_double),
-                ("halo_mode", C.c_int), ("reserved", C.c_int * 7)]
+                ("halo_mode", C.c_int), ("fused", C.c_int), ("reserved", C.c_int * 6)]
 
 
 class PamgError(RuntimeError):

@@ -183,7 +183,7 @@ def test_state_errors_are_reported():
 
 def test_timing_counts_launches():
     meta, _ = goldens.load("u8_s3_l3_gs")
-    s = gpu_solver(meta)
+    s = gpu_solver(meta, fused=0)
     s.timing_enable(0xFF)
     s.timing_reset()
     s.run(1, 1)
@@ -192,3 +192,36 @@ def test_timing_counts_launches():
     # the driver fuses restrictor(l) with the following get_residual(l) (:336, :338)
     assert t["residual"]["launches"] == 3 and t["restrict"]["launches"] == 0
     assert t["prolong"]["launches"] == 2 and t["rhs"]["launches"] == 1
+
+
+def test_fused_vcycle_counts_one_launch_per_cycle():
+    meta, _ = goldens.load("u8_s3_l3_gs")
+    s = gpu_solver(meta)
+    s.timing_enable(0x1FF)
+    s.timing_reset()
+    s.run(2, 3)
+    t = s.timing()
+    assert t["vcycle"]["launches"] == 6
+    assert t["smooth_L1"]["launches"] == 0 and t["prolong"]["launches"] == 0
+    assert t["rhs"]["launches"] == 2
+
+
+@pytest.mark.parametrize("mesh,S,L,solver,ns", [
+    ("untitled8.msh", 1, 1, 3, 1), ("untitled8.msh", 2, 2, 3, 2), ("untitled8.msh", 3, 3, 1, 1),
+    ("irregular.msh", 3, 3, 3, 1), ("900_ele.msh", 2, 2, 3, 3), ("900_ele.msh", 4, 4, 1, 1),
+    ("untitled2048.msh", 5, 5, 3, 1), ("untitled8192.msh", 5, 3, 3, 4), ("test_sn2.msh", 4, 2, 3, 2)])
+def test_fused_vcycle_equals_kernel_sequence_bitwise(mesh, S, L, solver, ns):
+    """The one-launch V-cycle (pamg_vcycle.hip) computes the same operations in
+    the same order as the per-step kernels: every field of every level and the
+    halo arrays agree bit for bit, including partial tiles (U not a multiple of
+    the tile's element count) and meshes with boundary faces."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    a = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, fused=1)
+    b = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, fused=0)
+    a.run(2, 2)
+    b.run(2, 2)
+    sa, sb = a.state(), b.state()
+    for k in sb:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    for x, y in zip(a.overlap(), b.overlap()):
+        np.testing.assert_array_equal(x, y)
