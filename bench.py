@@ -94,8 +94,8 @@ def pmc_traffic(kernel, nsplit, levels):
     return None
 
 
-RK_DESC = {"vcycle": "k_vcycle (one launch per V-cycle: every level's smoother, restriction, residual "
-                     "and prolongation in LDS/registers)",
+RK_DESC = {"vcycle": "k_vc_fine (fused V-cycle, level-1 launch: both smoother calls, residual, prolongator; "
+                     "the coarse levels run in k_vc_coarse just before it)",
            "smooth_L1": "k_smooth (level-1 smoother call, n_smooth sweeps fused)"}
 
 
@@ -127,7 +127,7 @@ def main():
     s.begin_timestep()
     s.vcycle(a.warmup)
     s.synchronize()
-    s.timing_enable(0x17F)  # every class but sweep_bench
+    s.timing_enable(0x37F)  # every class but sweep_bench
     s.timing_reset()
 
     def barrier():
@@ -163,6 +163,10 @@ def main():
                                  gbs=round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None)
                          for k, v in tm.items() if v["launches"]},
              "dominant_kernel": dom, "fine_sub_elements_per_rank": s.U * 4 ** a.nsplit}
+    # whole-cycle algorithmic bytes over the whole-cycle time (all launches of the timed region)
+    tot_bytes = sum(v["bytes"] for v in tm.values())
+    extra["cycle_alg_bytes"] = tot_bytes / a.steps
+    extra["cycle_alg_gbs"] = round(tot_bytes / elapsed / 1e9, 1)
     if rank == 0 and world == 1 and not a.no_extra:
         for asm in (False, True):
             ms, by = s.sweep_bench(20, asm)

@@ -55,8 +55,9 @@ extern "C" {
 #define PAMG_K_RHS 5
 #define PAMG_K_HALO 6
 #define PAMG_K_SWEEP_BENCH 7
-#define PAMG_K_VCYCLE 8
-#define PAMG_K_COUNT 9
+#define PAMG_K_VCYCLE 8          /* fused V-cycle, level-1 launch */
+#define PAMG_K_VCYCLE_COARSE 9   /* fused V-cycle, levels 2..L launch */
+#define PAMG_K_COUNT 10
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;

@@ -244,25 +244,31 @@ int prolong(pamg_handle *h, int l, bool fused_copy) {
     return PAMG_OK;
 }
 
-// algorithmic HBM bytes of one fused V-cycle (state traffic)
-double vcycle_bytes(pamg_handle *h) {
+// algorithmic HBM bytes of the two fused V-cycle launches: state traffic
+// of every level plus one operator record per un_ele and level
+double vcycle_fine_bytes(pamg_handle *h) {
     const int L = h->p.multi_levels;
-    double b = 0;
-    for (int l = 1; l <= L; ++l) {
-        const double N = (double)h->lv[l].N;
-        if (l == 1) b += (L > 1 ? 144.0 : 120.0) * N;
-        else b += (96.0 + (l < L ? 24.0 : 0.0)) * N;
-    }
-    return b + 168.0 * h->U * L;
+    return 120.0 * h->lv[1].N + (L > 1 ? 24.0 * h->lv[2].N : 0.0) + 168.0 * h->U;
+}
+double vcycle_coarse_bytes(pamg_handle *h) {
+    const int L = h->p.multi_levels;
+    double b = 24.0 * h->lv[1].N;   // level-1 residual of the previous cycle (restrictor input)
+    for (int l = 2; l <= L; ++l) b += (96.0 + (l < L ? 24.0 : 0.0)) * h->lv[l].N;
+    return b + 168.0 * h->U * (L - 1);
 }
 
 int vcycle_once(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     if (h->p.fused && vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, ns)) {
+        if (L > 1) {   // levels 2..L first: level 1's halo words are the cycle's last
+            Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h));
+            HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse,
+                                           1 / h->p.dt, h->tov, h->tovo));
+        }
         {
-            Span sp(h, PAMG_K_VCYCLE, vcycle_bytes(h));
-            HIPCHK(h, launch_vcycle(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, 1 / h->p.dt,
-                                    h->tov, h->tovo));
+            Span sp(h, PAMG_K_VCYCLE, vcycle_fine_bytes(h));
+            HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, 1 / h->p.dt,
+                                         h->tov, h->tovo));
         }
         h->tnn_level = 1;
         // the remote halo words of every smoother call were packed in the kernel; the last

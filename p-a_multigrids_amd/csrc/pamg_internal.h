@@ -133,8 +133,10 @@ hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n)
 hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);
 // fused V-cycle (pamg_vcycle.hip); lv is the handle's 1-based level array
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth);
-hipError_t launch_vcycle(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
-                         double rdt, double *tov, double *tovo);
+hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                                int n_coarse, double rdt, double *tov, double *tovo);   // levels 2..L
+hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                              int n_coarse, double rdt, double *tov, double *tovo);     // level 1
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch);

@@ -1,30 +1,37 @@
-// Fused V-cycle for gfx950: one launch runs one pass of the n_multigrid loop
-// body of transport_tri_semi.F90:319-379 for every un_ele.
+// Fused V-cycle for gfx950: two launches run one pass of the n_multigrid
+// loop body of transport_tri_semi.F90:319-379 for every un_ele.
 //
 // Every operation of the V-cycle is local to one unstructured element (the
 // smoother, residual and RHS use the element's 3x3 operator; the children of a
 // coarse sub-element live in the same un_ele, splitting.F90:97-140), so a
-// workgroup can carry a tile of whole un_eles through the complete V-cycle
-// without exchanging data with other workgroups. A tile holds 1024 level-1
-// sub-elements (1024 / 4**(n_split-1) un_eles), 256 level-2 ones, 64 level-3
-// ones, ...; 512 threads own two level-1 sub-elements each and one sub-element
-// of every coarser level. The state between the steps lives in registers, the
-// inter-level transfers go through LDS. HBM is touched once per field and
-// level: tnew, RHS (level 1) and the previous residual are read, and tnew,
-// tnew_nonlin (level 1), the new residual and the restricted RHS are written.
-//
-// The computation is the reference's, step for step and in its operation
-// order (same device helpers as the per-step kernels; results are bitwise
-// equal to pamg_vcycle's multi-kernel form, tests/test_gpu_parity.py):
-//   restriction leg  l = 1..L : smoother (n sweeps, halo), restrictor of the
-//                               previous residual, new residual   (:323-340)
-//   coarsest level            : 15 smoother calls = 15 n sweeps   (:344-359)
-//   prolongation leg l = L-1..1: prolongator (computed on chip; the reference
-//                               overwrites its result with tnew_nonlin at the
-//                               first sweep, :550), smoother      (:363-378)
-// What is not written back is only what the reference overwrites before any
-// read: the intermediate tnew of each level and the prolonged tnew.
+// workgroup carries a tile of whole un_eles through its part of the cycle
+// without exchanging data with other workgroups. The computation is the
+// reference's, step for step and in its operation order (same device helpers
+// as the per-step kernels; results are bitwise equal to pamg_vcycle's
+// multi-kernel form, tests/test_gpu_parity.py). The schedule follows the data
+// dependences, which the block-diagonal operator leaves loose:
+//   * the restrictor (:336) reads the residual of the PREVIOUS cycle;
+//   * the prolongation-leg smoother of level l (:376) starts from
+//     tnew_nonlin = the restriction-leg tnew of level l (:367); the prolonged
+//     values are overwritten at its first sweep (:550);
+//   * so level 1 (the reference's finest level) depends on the coarser levels
+//     only through the prolongator's (dead) result and the halo words, whose
+//     final state is what level 1's last smoother call writes.
+// Launch 1, k_vc_coarse: levels 2..L of the cycle -- all restrictions (level
+//   1's from the old residual), both legs of every coarser level, the 15
+//   coarse smoother calls, the prolongator cascades among them. Small
+//   workgroups (256 level-2 sub-elements per tile): the 15 n_smooth dependent
+//   sweeps of the coarsest level are a latency chain, hidden by occupancy.
+// Launch 2, k_vc_fine: level 1 -- both smoother calls, get_residual, and the
+//   prolongator cascade from the final level-2 tnew; a streaming kernel
+//   (tnew, RHS in; residual, tnew, tnew_nonlin out) whose halo words are the
+//   cycle's last, as in the reference.
+// Levels are 0-based inside this file: level 0 = the reference's level 1.
 #include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "pamg_device.h"
 #include "pamg_internal.h"
@@ -34,90 +41,170 @@ namespace {
 
 using namespace detail;
 
-constexpr int kMT = 512;    // threads per workgroup
-constexpr int kT1 = 1024;   // level-1 sub-elements per tile
+constexpr int kMTf = 512;   // threads per workgroup, level-0 kernel (one adjacent pair each)
+constexpr int kMTc = 256;   // threads per workgroup, coarse-level kernel (one level-1 sub-element each)
 
 struct VLevel {
     double *T, *TNN, *RHS, *RES;
     const double *stc;
     const int4 *children;   // children (in-un_ele indices) of this level's sub-elements in the next finer level
     int64_t pitch;
-    int nsub_log2;
     HaloArgs H;
 };
 
 struct VArgs {
     VLevel lv[kMaxFusedLevels];
     int64_t U;
-    int G_log2;             // un_eles per tile = 1024 / nsub_1
     int n_smooth, n_coarse;
     double rdt;
+    long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
 };
 
-struct Sub {
-    double p[3], x[3], b[3];
-};
-
-__device__ __forceinline__ void load3(const double *f, int64_t pitch, int64_t s, double v[3]) {
-#pragma unroll
-    for (int c = 0; c < 3; ++c) v[c] = f[c * pitch + s];
+// phase stamps: 100 MHz wall clock per wave at the phase boundaries, plus the wave's HW_ID
+constexpr int kStampSlots = 10;
+template <int MT>
+__device__ __forceinline__ void stamp(const VArgs &A, int i) {
+    if (A.stamps && (threadIdx.x & 63) == 0)
+        A.stamps[((int64_t)blockIdx.x * (MT / 64) + (threadIdx.x >> 6)) * kStampSlots + i] = wall_clock64();
 }
-__device__ __forceinline__ void store3(double *f, int64_t pitch, int64_t s, const double v[3]) {
-#pragma unroll
-    for (int c = 0; c < 3; ++c) f[c * pitch + s] = v[c];
-}
-
-// one smoother call (or several) on one sub-element: x -> last iterate, p -> iterate before the last sweep
-__device__ __forceinline__ void smooth_sub(const VLevel &V, int64_t s, int sweeps, double rdt, Sub &q) {
-    Stc S;
-    load_stc(V.stc + (s >> V.nsub_log2) * kStcStride, S);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) q.p[c] = q.x[c];
-    for (int it = 0; it < sweeps; ++it) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) q.p[c] = q.x[c];
-        sweep(S, rdt, q.b, q.x);
+template <int MT>
+__device__ __forceinline__ void stamp_hwid(const VArgs &A) {
+    if (A.stamps && (threadIdx.x & 63) == 0) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        A.stamps[((int64_t)blockIdx.x * (MT / 64) + (threadIdx.x >> 6)) * kStampSlots + 9] = hw;
     }
 }
 
-// the halo words of one sub-element (update_overlaps at the start of the last sweep, :555)
-__device__ __forceinline__ void halo_sub(const VLevel &V, int64_t s, const double t[3]) {
-    const HaloArgs &H = V.H;
-    const int4 hs = H.hsub[s & ((1ll << V.nsub_log2) - 1)];
-    if ((hs.x | hs.y | hs.z) == 0) return;
-    const int64_t u = s >> V.nsub_log2;
+// tile geometry (0-based level l): 4**(S-l) sub-elements per un_ele; a tile holds
+// 1024 >> 2l sub-elements of level l (1024 / 4**S un_eles)
+template <int S, int L>
+struct Geo {
+    static constexpr int C = L - 1;                                // coarsest level
+    static constexpr int GL = 10 - 2 * S;                          // log2 un_eles per tile
+    static constexpr int lg(int l) { return 2 * (S - l); }
+    static constexpr int nt(int l) { return 1024 >> (2 * l); }
+    // each wave inside one un_ele (a wave spans 128 level-0 sub-elements, 64 of any other level)
+    static constexpr bool uni(int l) { return lg(l) >= (l == 0 ? 7 : 6); }
+    // coarse kernel LDS: old residual R_l and restriction-leg tnew F_l (1 <= l < C), final tnew Y_l (2 <= l <= C)
+    static constexpr int off(int l) {   // 3 * (nt(1) + ... + nt(l-1))
+        int o = 0;
+        for (int i = 1; i < l; ++i) o += 3 * nt(i);
+        return o;
+    }
+    static constexpr int nR = off(C);
+    static constexpr int R(int l) { return off(l); }
+    static constexpr int F(int l) { return nR + off(l); }
+    static constexpr int Y(int l) { return 2 * nR + off(l) - off(2); }
+    static constexpr int coarse_total = (C >= 2) ? 2 * nR + off(C + 1) - off(2) : 1;
+};
+
+// field access: wave-uniform plane base (SGPRs) + 32-bit sub-element index (one VGPR for all planes)
+__device__ __forceinline__ void load3(const double *f, int64_t pitch, uint32_t s, double v[3]) {
+    const uint32_t o = s << 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(f + c * pitch) + o);
+}
+__device__ __forceinline__ void store3(double *f, int64_t pitch, uint32_t s, const double v[3]) {
+    const uint32_t o = s << 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) *reinterpret_cast<double *>(reinterpret_cast<char *>(f + c * pitch) + o) = v[c];
+}
+// the adjacent pair s, s+1 (s even) with 16-byte accesses
+__device__ __forceinline__ void load3p(const double *f, int64_t pitch, uint32_t s, double a[3], double b[3]) {
+    const uint32_t o = s << 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double2 v = *reinterpret_cast<const double2 *>(reinterpret_cast<const char *>(f + c * pitch) + o);
+        a[c] = v.x;
+        b[c] = v.y;
+    }
+}
+__device__ __forceinline__ void store3p(double *f, int64_t pitch, uint32_t s, const double a[3], const double b[3]) {
+    const uint32_t o = s << 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        *reinterpret_cast<double2 *>(reinterpret_cast<char *>(f + c * pitch) + o) = make_double2(a[c], b[c]);
+}
+__device__ __forceinline__ void copy3(double d[3], const double s[3]) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = s[c];
+}
+
+// operator record of un_ele u; wave-uniform records come through the scalar cache
+// (uni is a compile-time constant at every call site once the level loops are unrolled)
+__device__ __forceinline__ void stencil(bool uni, const double *__restrict__ stc, uint32_t u, Stc &S) {
+    if (uni) u = __builtin_amdgcn_readfirstlane(u);
+    load_stc(stc + u * (uint32_t)kStcStride, S);
+}
+
+// n sweeps from x: x -> last iterate, p -> iterate before the last sweep (n >= 1)
+__device__ __forceinline__ void sweeps(const Stc &S, double rdt, int n, const double b[3], double x[3],
+                                       double p[3]) {
+    for (int it = 0; it < n; ++it) {
+        copy3(p, x);
+        sweep(S, rdt, b, x);
+    }
+}
+// two sub-elements of one un_ele, interleaved
+__device__ __forceinline__ void sweeps2(const Stc &S, double rdt, int n, const double b0[3], const double b1[3],
+                                        double x0[3], double x1[3], double p0[3], double p1[3]) {
+    for (int it = 0; it < n; ++it) {
+        copy3(p0, x0);
+        copy3(p1, x1);
+        sweep(S, rdt, b0, x0);
+        sweep(S, rdt, b1, x1);
+    }
+}
+
+__device__ __forceinline__ void residual(const Stc &S, double rdt, const double p[3], const double b[3],
+                                         double r[3]) {
+    double a[3];
+    apply_A(S, rdt, p, a);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) r[c] = a[c] - b[c];
+}
+
+// ---- halo words of one sub-element (update_overlaps, :555)
+// h: its positions along faces 1..3 packed 6 bits each (0: not on that face)
+__device__ __forceinline__ int hs_pack(int4 q) { return q.x | (q.y << 6) | (q.z << 12); }
+
+// told of a boundary sub-element (compact told halo entry of its first copied face), fetched
+// once in the prologue so that no halo write waits on a dependent load
+__device__ __forceinline__ void hs_told(bool uni, const HaloArgs &H, uint32_t u, int h, double to[3]) {
+    to[0] = to[1] = to[2] = 0.0;
+    if (h == 0) return;
+    if (uni) u = __builtin_amdgcn_readfirstlane(u);
     const int4 r1 = H.hface[3 * u], r2 = H.hface[3 * u + 1], r3 = H.hface[3 * u + 2];
+    const int a = h & 63, b = (h >> 6) & 63, c = h >> 12;
     int e = -1;
-    if (hs.x && (r1.x & 3)) e = r1.w + hs.x - 1;
-    else if (hs.y && (r2.x & 3)) e = r2.w + hs.y - 1;
-    else if (hs.z && (r3.x & 3)) e = r3.w + hs.z - 1;
-    double to[3] = {0.0, 0.0, 0.0};
+    if (a && (r1.x & 3)) e = r1.w + a - 1;
+    else if (b && (r2.x & 3)) e = r2.w + b - 1;
+    else if (c && (r3.x & 3)) e = r3.w + c - 1;
     if (e >= 0) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) to[c] = H.told[3 * (int64_t)e + c];
+        for (int k = 0; k < 3; ++k) to[k] = H.told[3 * (int64_t)e + k];
     }
-    if (hs.x) halo_face(H, r1, 1, hs.x, t, to);
-    if (hs.y) halo_face(H, r2, 2, hs.y, t, to);
-    if (hs.z) halo_face(H, r3, 3, hs.z, t, to);
 }
 
-__device__ __forceinline__ void residual_sub(const VLevel &V, int64_t s, double rdt, const Sub &q) {
-    Stc S;
-    load_stc(V.stc + (s >> V.nsub_log2) * kStcStride, S);
-    double A[3], r[3];
-    apply_A(S, rdt, q.p, A);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) r[c] = A[c] - q.b[c];
-    store3(V.RES, V.pitch, s, r);
+__device__ __forceinline__ void hs_write(bool uni, const HaloArgs &H, uint32_t u, int h, const double t[3],
+                                         const double to[3]) {
+    if (h == 0) return;
+    if (uni) u = __builtin_amdgcn_readfirstlane(u);
+    const int4 r1 = H.hface[3 * u], r2 = H.hface[3 * u + 1], r3 = H.hface[3 * u + 2];
+    const int a = h & 63, b = (h >> 6) & 63, c = h >> 12;
+    if (a) halo_face(H, r1, 1, a, t, to);
+    if (b) halo_face(H, r2, 2, b, t, to);
+    if (c) halo_face(H, r3, 3, c, t, to);
 }
 
-// prolongator cascade (splitting.F90:59-88) on the LDS image of the fine tile
-__device__ __forceinline__ void prolong_cascade(double *F, int nf, const int fi[4], const double y[3]) {
+// prolongator cascade (splitting.F90:59-88) on the LDS image of the fine tile (component stride n)
+__device__ __forceinline__ void prolong_cascade(double *F, int n, const int fi[4], const double y[3]) {
     double f[4][3];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int i = 0; i < 3; ++i) f[q][i] = F[i * nf + fi[q]];
+        for (int i = 0; i < 3; ++i) f[q][i] = F[i * n + fi[q]];
     f[0][0] = f[0][0] + 0.5 * y[2] + 0.5 * y[0];
     f[0][1] = f[0][1] + 0.5 * y[1] + 0.5 * y[2];
     f[0][2] = f[0][2] + y[2];
@@ -133,132 +220,318 @@ __device__ __forceinline__ void prolong_cascade(double *F, int nf, const int fi[
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int i = 0; i < 3; ++i) F[i * nf + fi[q]] = f[q][i];
+        for (int i = 0; i < 3; ++i) F[i * n + fi[q]] = f[q][i];
 }
 
-// Sub-element ownership inside a tile: level 1 -> tile-local t and t + 512,
-// level l >= 2 -> t (if t < n_l). Per-level register state st[l][k].
-template <int L>
-__global__ __launch_bounds__(kMT) void k_vcycle(VArgs A) {
-    __shared__ __attribute__((aligned(16))) double lds[3 * (kT1 + kT1 / 4)];
+// ===================================================================== coarse levels
+// Ownership: level l >= 1 -> sub-element t of the tile (if t < n_l).
+template <int S, int L>
+__global__ __launch_bounds__(kMTc) void k_vc_coarse(VArgs A, const double *__restrict__ sp1,
+                                                    const double *__restrict__ sp2, const double *__restrict__ sp3,
+                                                    const double *__restrict__ sp4) {
+    // operator records as restrict kernel arguments: never written here, so wave-uniform
+    // records are fetched with scalar loads
+    const double *__restrict__ SP[kMaxFusedLevels] = {nullptr, sp1, sp2, sp3, sp4};
+    using G = Geo<S, L>;
+    constexpr int C = G::C;
+    static_assert(C >= 1, "coarse kernel needs two levels");
+    __shared__ __attribute__((aligned(16))) double lds[G::coarse_total];
     const int t = threadIdx.x;
-    const int64_t u0 = (int64_t)blockIdx.x << A.G_log2;                  // first un_ele of the tile
-    const int64_t nue = min((int64_t)1 << A.G_log2, A.U - u0);          // un_eles in this tile
     const double rdt = A.rdt;
-    Sub st[L][2];
-    int nl[L];      // sub-elements of the tile on each level
-    int64_t s0[L];  // first global sub-element of the tile on each level
+    const int ns = A.n_smooth;
+    const int64_t u0 = (int64_t)blockIdx.x << G::GL;
+    const int nue = (int)min((int64_t)1 << G::GL, A.U - u0);
+    stamp<kMTc>(A, 0);
+    stamp_hwid<kMTc>(A);
+    bool vl[L];
+    uint32_t sl[L];
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-        nl[l] = (int)(nue << A.lv[l].nsub_log2);
-        s0[l] = u0 << A.lv[l].nsub_log2;
+    for (int l = 1; l < L; ++l) {
+        vl[l] = t < (nue << G::lg(l));
+        sl[l] = ((uint32_t)u0 << G::lg(l)) + (vl[l] ? t : 0);   // clamped: loads stay in bounds
     }
-    // ---- restriction leg (:323-340)
+    // ---- prologue
+    int hl[L];
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-        const VLevel &V = A.lv[l];
-        const int K = (l == 0) ? 2 : 1;
+    for (int l = 1; l < L; ++l) hl[l] = vl[l] ? hs_pack(A.lv[l].H.hsub[sl[l] & ((1 << G::lg(l)) - 1)]) : 0;
+    double rl[L][3], xl[L][3], bl[L][3], tl[L][3];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int j = t + k * kMT;
-            if (j >= nl[l]) continue;
-            const int64_t s = s0[l] + j;
-            load3(V.T, V.pitch, s, st[l][k].x);                 // tnew_nonlin := tnew (:327)
-            if (l == 0) load3(V.RHS, V.pitch, s, st[l][k].b);   // RHS_1 (get_RHS, constant in the step)
-            smooth_sub(V, s, A.n_smooth, rdt, st[l][k]);       // call smoother (:331)
-            halo_sub(V, s, st[l][k].p);
-        }
-        if (l + 1 < L) {                                        // call restrictor (:336)
-            const VLevel &C = A.lv[l + 1];
-            double *R = lds;
-            for (int j = t; j < nl[l]; j += kMT) {
-                double r[3];
-                load3(V.RES, V.pitch, s0[l] + j, r);           // previous cycle's residual
+    for (int l = 1; l < C; ++l) load3(A.lv[l].RES, A.lv[l].pitch, sl[l], rl[l]);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) R[c * nl[l] + j] = r[c];
-            }
-            __syncthreads();
-            if (t < nl[l + 1]) {
-                const int cin = t & ((1 << C.nsub_log2) - 1);
-                const int base = (t >> C.nsub_log2) << V.nsub_log2;
-                const int4 ch = C.children[cin];
-                const int pick[3] = {base + ch.z, base + ch.w, base + ch.x};
+    for (int l = 1; l < L; ++l) load3(A.lv[l].T, A.lv[l].pitch, sl[l], xl[l]);
 #pragma unroll
-                for (int i = 0; i < 3; ++i)
-                    st[l + 1][0].b[i] = (R[pick[i]] + R[nl[l] + pick[i]] + R[2 * nl[l] + pick[i]]) / 3.;
-                store3(C.RHS, C.pitch, s0[l + 1] + t, st[l + 1][0].b);
-            }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {                           // call get_residual (:338)
-            const int j = t + k * kMT;
-            if (j < nl[l]) residual_sub(V, s0[l] + j, rdt, st[l][k]);
-        }
-    }
-    // ---- coarsest level: 15 smoother calls from tnew_nonlin := tnew (:344-359)
+    for (int l = 1; l < L; ++l) hs_told(G::uni(l), A.lv[l].H, sl[l] >> G::lg(l), hl[l], tl[l]);
+    // restrictor of level 1 (:336) straight from the level-0 residual of the previous cycle
+    // (level 0 is rewritten only by the next launch)
     {
-        constexpr int l = L - 1;
+        const VLevel &V0 = A.lv[0];
+        const int4 c4 = A.lv[1].children[sl[1] & ((1 << G::lg(1)) - 1)];
+        const uint32_t base = (sl[1] >> G::lg(1)) << G::lg(0);
+        const uint32_t pick[3] = {base + c4.z, base + c4.w, base + c4.x};
+        double r[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) load3(V0.RES, V0.pitch, pick[i], r[i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) bl[1][i] = (r[i][0] + r[i][1] + r[i][2]) / 3.;
+        if (vl[1]) store3(A.lv[1].RHS, A.lv[1].pitch, sl[1], bl[1]);
+    }
+    if constexpr (C >= 2) {
+#pragma unroll
+        for (int l = 1; l < C; ++l)
+            if (vl[l])
+#pragma unroll
+                for (int c = 0; c < 3; ++c) lds[G::R(l) + c * G::nt(l) + t] = rl[l][c];
+        __syncthreads();
+#pragma unroll
+        for (int l = 1; l < C; ++l) {
+            if (!vl[l + 1]) continue;
+            const double *R = lds + G::R(l);
+            const int base = (t >> G::lg(l + 1)) << G::lg(l);
+            const int4 c4 = A.lv[l + 1].children[sl[l + 1] & ((1 << G::lg(l + 1)) - 1)];
+            const int pick[3] = {base + c4.z, base + c4.w, base + c4.x};
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                bl[l + 1][i] = (R[pick[i]] + R[G::nt(l) + pick[i]] + R[2 * G::nt(l) + pick[i]]) / 3.;
+            store3(A.lv[l + 1].RHS, A.lv[l + 1].pitch, sl[l + 1], bl[l + 1]);
+        }
+    }
+    stamp<kMTc>(A, 1);
+    // ---- levels 1..C-1, restriction leg: smoother (:331), get_residual (:338)
+#pragma unroll
+    for (int l = 1; l < C; ++l) {
+        if (!vl[l]) continue;
         const VLevel &V = A.lv[l];
-        const int K = (l == 0) ? 2 : 1;
+        const uint32_t u = sl[l] >> G::lg(l);
+        Stc St;
+        stencil(G::uni(l), SP[l], u, St);
+        double p[3];
+        sweeps(St, rdt, ns, bl[l], xl[l], p);
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int j = t + k * kMT;
-            if (j >= nl[l]) continue;
-            const int64_t s = s0[l] + j;
-            Sub q = st[l][k];
+        for (int c = 0; c < 3; ++c) lds[G::F(l) + c * G::nt(l) + t] = p[c];
+        hs_write(G::uni(l), V.H, u, hl[l], p, tl[l]);
+        double r[3];
+        residual(St, rdt, p, bl[l], r);
+        store3(V.RES, V.pitch, sl[l], r);
+    }
+    stamp<kMTc>(A, 2);
+    // ---- coarsest level: smoother + get_residual of the restriction leg, then the
+    //      15 smoother calls from tnew_nonlin := tnew (:344-359)
+    if (vl[C]) {
+        const VLevel &V = A.lv[C];
+        const uint32_t u = sl[C] >> G::lg(C);
+        Stc St;
+        stencil(G::uni(C), SP[C], u, St);
+        double p[3];
+        sweeps(St, rdt, ns, bl[C], xl[C], p);
+        hs_write(G::uni(C), V.H, u, hl[C], p, tl[C]);
+        double r[3];
+        residual(St, rdt, p, bl[C], r);
+        store3(V.RES, V.pitch, sl[C], r);
+        copy3(xl[C], p);
+        sweeps(St, rdt, ns * A.n_coarse, bl[C], xl[C], p);
+        hs_write(G::uni(C), V.H, u, hl[C], p, tl[C]);
+        store3(V.T, V.pitch, sl[C], p);
+        if constexpr (C >= 2)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) q.x[c] = q.p[c];
-            smooth_sub(V, s, A.n_smooth * A.n_coarse, rdt, q);
-            halo_sub(V, s, q.p);
-            store3(V.T, V.pitch, s, q.p);
-            if (l == 0) store3(V.TNN, V.pitch, s, q.x);
-            st[l][k].p[0] = q.p[0]; st[l][k].p[1] = q.p[1]; st[l][k].p[2] = q.p[2];   // final tnew of the level
+            for (int c = 0; c < 3; ++c) lds[G::Y(C) + c * G::nt(C) + t] = p[c];
+    }
+    stamp<kMTc>(A, 3);
+    // ---- prolongation leg, levels C-1..1: smoother from tnew_nonlin = restriction-leg tnew (:367, :376)
+#pragma unroll
+    for (int l = C - 1; l >= 1; --l) {
+        if (!vl[l]) continue;
+        const VLevel &V = A.lv[l];
+        const uint32_t u = sl[l] >> G::lg(l);
+        Stc St;
+        stencil(G::uni(l), SP[l], u, St);
+        double x[3], p[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c] = lds[G::F(l) + c * G::nt(l) + t];
+        sweeps(St, rdt, ns, bl[l], x, p);
+        hs_write(G::uni(l), V.H, u, hl[l], p, tl[l]);
+        store3(V.T, V.pitch, sl[l], p);
+        if (l >= 2)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) lds[G::Y(l) + c * G::nt(l) + t] = p[c];
+    }
+    stamp<kMTc>(A, 4);
+    // ---- prolongator (:370) among the coarse levels, on the LDS images (its result is dead)
+    if constexpr (C >= 2) {
+        __syncthreads();
+#pragma unroll
+        for (int l = 1; l < C; ++l) {
+            if (!vl[l + 1]) continue;
+            const double *Y = lds + G::Y(l + 1);
+            const int base = (t >> G::lg(l + 1)) << G::lg(l);
+            const int4 c4 = A.lv[l + 1].children[sl[l + 1] & ((1 << G::lg(l + 1)) - 1)];
+            const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+            const double y[3] = {Y[t], Y[G::nt(l + 1) + t], Y[2 * G::nt(l + 1) + t]};
+            prolong_cascade(lds + G::F(l), G::nt(l), fi, y);
         }
     }
-    // ---- prolongation leg (:363-378)
+    stamp<kMTc>(A, 7);
+}
+
+// ===================================================================== level 0
+// Ownership: the adjacent pair 2t, 2t+1 of the tile (16-byte accesses, one un_ele,
+// one operator record); for the prolongator, level-1 sub-element t.
+template <int S, int L>
+__global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0) {
+    using G = Geo<S, L>;
+    constexpr int C = G::C;
+    __shared__ __attribute__((aligned(16))) double F0[C > 0 ? 3 * 1024 : 1];   // restriction-leg tnew image
+    const int t = threadIdx.x;
+    const double rdt = A.rdt;
+    const int ns = A.n_smooth;
+    const int64_t u0 = (int64_t)blockIdx.x << G::GL;
+    const int nue = (int)min((int64_t)1 << G::GL, A.U - u0);
+    stamp<kMTf>(A, 0);
+    stamp_hwid<kMTf>(A);
+    const VLevel &V0 = A.lv[0];
+    const bool v0 = 2 * t < (nue << G::lg(0));
+    const uint32_t s0 = ((uint32_t)u0 << G::lg(0)) + (v0 ? 2 * t : 0);   // clamped: loads stay in bounds
+    const uint32_t w0 = s0 >> G::lg(0);                                  // un_ele of the pair
+    // ---- prologue
+    int h0[2];
 #pragma unroll
-    for (int l = L - 2; l >= 0; --l) {
-        const VLevel &V = A.lv[l], &C = A.lv[l + 1];
-        const int K = (l == 0) ? 2 : 1;
-        double *F = lds, *Y = lds + 3 * nl[l];
-        // prolongator (:370) on the LDS image of tnew (= tnew_nonlin, :367) with the final coarse tnew
+    for (int k = 0; k < 2; ++k) h0[k] = v0 ? hs_pack(V0.H.hsub[(s0 + k) & ((1 << G::lg(0)) - 1)]) : 0;
+    double x0[2][3], b0[2][3], p0[2][3], to0[2][3];
+    load3p(V0.T, V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
+    load3p(V0.RHS, V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
+    // final level-1 tnew (coarse launch) for the prolongator
+    bool v1 = false;
+    uint32_t s1 = 0;
+    double y1[3];
+    int4 c4 = make_int4(0, 0, 0, 0);
+    if constexpr (C > 0) {
+        v1 = t < (nue << G::lg(1));
+        s1 = ((uint32_t)u0 << G::lg(1)) + (v1 ? t : 0);
+        load3(A.lv[1].T, A.lv[1].pitch, s1, y1);
+        c4 = A.lv[1].children[s1 & ((1 << G::lg(1)) - 1)];
+    }
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int j = t + k * kMT;
-            if (j < nl[l])
+    for (int k = 0; k < 2; ++k) hs_told(G::uni(0), V0.H, w0, h0[k], to0[k]);
+    Stc St;
+    stencil(G::uni(0), sp0, w0, St);
+    // ---- restriction leg: smoother (:331), get_residual (:338)
+    sweeps2(St, rdt, ns, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
+    stamp<kMTf>(A, 1);
+    if (v0) {
+        if constexpr (C > 0)
 #pragma unroll
-                for (int c = 0; c < 3; ++c) F[c * nl[l] + j] = st[l][k].p[c];
-        }
-        if (t < nl[l + 1])
+            for (int c = 0; c < 3; ++c) st2(F0 + c * 1024 + 2 * t, make_double2(p0[0][c], p0[1][c]));
 #pragma unroll
-            for (int c = 0; c < 3; ++c) Y[c * nl[l + 1] + t] = st[l + 1][0].p[c];
+        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, h0[k], p0[k], to0[k]);
+        double r[2][3];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) residual(St, rdt, p0[k], b0[k], r[k]);
+        store3p(V0.RES, V0.pitch, s0, r[0], r[1]);
+    }
+    stamp<kMTf>(A, 2);
+    // ---- prolongation leg (:367-376) from the restriction-leg tnew; with one level,
+    //      the 15 coarse smoother calls (:344-359)
+    copy3(x0[0], p0[0]);
+    copy3(x0[1], p0[1]);
+    sweeps2(St, rdt, C > 0 ? ns : ns * A.n_coarse, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
+    stamp<kMTf>(A, 3);
+    if (v0) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, h0[k], p0[k], to0[k]);
+        store3p(V0.T, V0.pitch, s0, p0[0], p0[1]);
+        store3p(V0.TNN, V0.pitch, s0, x0[0], x0[1]);
+    }
+    stamp<kMTf>(A, 4);
+    // ---- prolongator (:370) on the LDS image (its result is dead, :550)
+    if constexpr (C > 0) {
         __syncthreads();
-        if (t < nl[l + 1]) {
-            const int cin = t & ((1 << C.nsub_log2) - 1);
-            const int base = (t >> C.nsub_log2) << V.nsub_log2;
-            const int4 ch = C.children[cin];
-            const int fi[4] = {base + ch.x, base + ch.y, base + ch.z, base + ch.w};
-            const double y[3] = {Y[t], Y[nl[l + 1] + t], Y[2 * nl[l + 1] + t]};
-            prolong_cascade(F, nl[l], fi, y);
-        }
-        __syncthreads();
-        // smoother from tnew_nonlin (:376): the prolonged tnew is overwritten at its first sweep (:550)
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int j = t + k * kMT;
-            if (j >= nl[l]) continue;
-            const int64_t s = s0[l] + j;
-            Sub q = st[l][k];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) q.x[c] = q.p[c];
-            smooth_sub(V, s, A.n_smooth, rdt, q);
-            halo_sub(V, s, q.p);
-            store3(V.T, V.pitch, s, q.p);
-            if (l == 0) store3(V.TNN, V.pitch, s, q.x);
-            st[l][k].p[0] = q.p[0]; st[l][k].p[1] = q.p[1]; st[l][k].p[2] = q.p[2];
+        if (v1) {
+            const int base = (t >> G::lg(1)) << G::lg(0);
+            const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+            prolong_cascade(F0, 1024, fi, y1);
         }
     }
+    stamp<kMTf>(A, 7);
+}
+
+template <int S, int L>
+hipError_t launch_sl(hipStream_t s, const VArgs &A, unsigned grid, bool coarse) {
+    if (coarse) {
+        if constexpr (L >= 2)
+            hipLaunchKernelGGL((k_vc_coarse<S, L>), dim3(grid), dim3(kMTc), 0, s, A, A.lv[1].stc, A.lv[2].stc,
+                               A.lv[3].stc, A.lv[4].stc);
+        else
+            return hipErrorInvalidValue;
+    } else {
+        hipLaunchKernelGGL((k_vc_fine<S, L>), dim3(grid), dim3(kMTf), 0, s, A, A.lv[0].stc);
+    }
+    return hipGetLastError();
+}
+
+template <int S>
+hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, bool coarse) {
+    switch (L) {
+        case 1: return launch_sl<S, 1>(s, A, grid, coarse);
+        case 2: if constexpr (S >= 2) return launch_sl<S, 2>(s, A, grid, coarse); break;
+        case 3: if constexpr (S >= 3) return launch_sl<S, 3>(s, A, grid, coarse); break;
+        case 4: if constexpr (S >= 4) return launch_sl<S, 4>(s, A, grid, coarse); break;
+        case 5: if constexpr (S >= 5) return launch_sl<S, 5>(s, A, grid, coarse); break;
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
+                       double rdt, double *tov, double *tovo, bool coarse) {
+    if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
+    VArgs A{};
+    for (int l = 0; l < L; ++l) {
+        const Level &V = lv[l + 1];
+        if (V.nsub != (1 << (2 * (n_split - l)))) return hipErrorInvalidValue;
+        if ((uint64_t)V.pitch * 3 >= (1ull << 29)) return hipErrorInvalidValue;   // 32-bit byte offsets
+        VLevel &o = A.lv[l];
+        o.T = V.T; o.TNN = V.TNN; o.RHS = V.RHS; o.RES = V.RES; o.stc = V.stc;
+        o.children = (l > 0) ? lv[l].children : nullptr;   // children of level l+1 in level l
+        o.pitch = V.pitch;
+        const HaloPlan &P = V.halo;
+        o.H = HaloArgs{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << V.isplit};
+    }
+    A.U = U;
+    A.n_smooth = n_smooth;
+    A.n_coarse = n_coarse;
+    A.rdt = rdt;
+    const int GL = 10 - 2 * n_split;   // 1024 / 4**n_split un_eles per tile
+    const unsigned grid = (unsigned)(((int64_t)U + (1 << GL) - 1) >> GL);
+    if (grid == 0) return hipSuccess;
+    // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
+    static const char *stamp_path = getenv("PAMG_VCYCLE_STAMPS");
+    const int waves = (coarse ? kMTc : kMTf) / 64;
+    const size_t nst = (size_t)grid * waves * kStampSlots;
+    if (stamp_path) {
+        hipError_t e = hipMalloc(&A.stamps, nst * sizeof(long long));
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(A.stamps, 0, nst * sizeof(long long), s);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipErrorInvalidValue;
+    switch (n_split) {
+        case 1: e = launch_s<1>(s, A, grid, L, coarse); break;
+        case 2: e = launch_s<2>(s, A, grid, L, coarse); break;
+        case 3: e = launch_s<3>(s, A, grid, L, coarse); break;
+        case 4: e = launch_s<4>(s, A, grid, L, coarse); break;
+        case 5: e = launch_s<5>(s, A, grid, L, coarse); break;
+    }
+    if (stamp_path) {
+        std::vector<long long> hst(nst);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpy(hst.data(), A.stamps, nst * sizeof(long long), hipMemcpyDeviceToHost);
+        (void)hipFree(A.stamps);
+        if (FILE *f = fopen(stamp_path, "ab")) {
+            const long long hdr[4] = {grid, waves, kStampSlots, L * (coarse ? -1 : 1)};
+            fwrite(hdr, sizeof hdr, 1, f);
+            fwrite(hst.data(), sizeof(long long), nst, f);
+            fclose(f);
+        }
+    }
+    return e;
 }
 
 }  // namespace
@@ -269,37 +542,15 @@ bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mo
            n_split >= L;
 }
 
-hipError_t launch_vcycle(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
-                         double rdt, double *tov, double *tovo) {
-    VArgs A{};
-    for (int l = 0; l < L; ++l) {
-        const Level &V = lv[l + 1];
-        VLevel &o = A.lv[l];
-        o.T = V.T; o.TNN = V.TNN; o.RHS = V.RHS; o.RES = V.RES; o.stc = V.stc;
-        o.children = (l > 0) ? lv[l].children : nullptr;   // children of level l+1 in level l
-        o.pitch = V.pitch;
-        int lg = 0;
-        while ((1 << lg) < V.nsub) ++lg;
-        o.nsub_log2 = lg;
-        const HaloPlan &P = V.halo;
-        o.H = HaloArgs{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << V.isplit};
-    }
-    A.U = U;
-    A.G_log2 = 10 - 2 * n_split;   // 1024 / 4**n_split un_eles per tile
-    A.n_smooth = n_smooth;
-    A.n_coarse = n_coarse;
-    A.rdt = rdt;
-    const unsigned grid = (unsigned)((U + (1 << A.G_log2) - 1) >> A.G_log2);
-    if (grid == 0) return hipSuccess;
-    switch (L) {
-        case 1: hipLaunchKernelGGL(k_vcycle<1>, dim3(grid), dim3(kMT), 0, s, A); break;
-        case 2: hipLaunchKernelGGL(k_vcycle<2>, dim3(grid), dim3(kMT), 0, s, A); break;
-        case 3: hipLaunchKernelGGL(k_vcycle<3>, dim3(grid), dim3(kMT), 0, s, A); break;
-        case 4: hipLaunchKernelGGL(k_vcycle<4>, dim3(grid), dim3(kMT), 0, s, A); break;
-        case 5: hipLaunchKernelGGL(k_vcycle<5>, dim3(grid), dim3(kMT), 0, s, A); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                                int n_coarse, double rdt, double *tov, double *tovo) {
+    if (L < 2) return hipSuccess;
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, true);
+}
+
+hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                              int n_coarse, double rdt, double *tov, double *tovo) {
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, false);
 }
 
 }  // namespace pamg

@@ -17,8 +17,10 @@ ERRORS = {-1: "PAMG_ERR_ARG", -2: "PAMG_ERR_HIP", -3: "PAMG_ERR_IO", -4: "PAMG_E
           -5: "PAMG_ERR_COMM", -6: "PAMG_ERR_NODEV"}
 
 TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN = 0, 1, 2, 3, 4
-K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH, K_VCYCLE = range(9)
-K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle"]
+(K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH, K_VCYCLE,
+ K_VCYCLE_COARSE) = range(10)
+K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle",
+           "vcycle_coarse"]
 
 
 class PamgParams(C.Structure):

@@ -197,11 +197,11 @@ def test_timing_counts_launches():
 def test_fused_vcycle_counts_one_launch_per_cycle():
     meta, _ = goldens.load("u8_s3_l3_gs")
     s = gpu_solver(meta)
-    s.timing_enable(0x1FF)
+    s.timing_enable(0x3FF)
     s.timing_reset()
     s.run(2, 3)
     t = s.timing()
-    assert t["vcycle"]["launches"] == 6
+    assert t["vcycle"]["launches"] == 6 and t["vcycle_coarse"]["launches"] == 6
     assert t["smooth_L1"]["launches"] == 0 and t["prolong"]["launches"] == 0
     assert t["rhs"]["launches"] == 2
 
