@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 TAG=${1:-run}
 echo "host: $(hostname) nproc=$(nproc)" > gpurun_out/env.txt
 timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
 timeout -k 10 400 python bench.py --steps 50 --warmup 5 > gpurun_out/bench_$TAG.log 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $R/gpurun_out/prof_$TAG.log 2>&1

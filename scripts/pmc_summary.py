@@ -4,7 +4,9 @@
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE (KiB) reports
 half the bytes of wide coalesced streaming reads -> x2; WRITE_SIZE (KiB) is exact
 for 16-B-per-lane streaming stores. Usage:
-  pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON N_SPLIT [alg_bytes_l1_smooth]"""
+  pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON N_SPLIT [alg_bytes_per_launch] [kernel_prefix]
+kernel_prefix selects the roofline kernel (default "k_vc_fine", the fused V-cycle's
+level-1 launch; "void k_smooth<false, true>" for the per-step level-1 smoother)."""
 import collections
 import csv
 import glob
@@ -25,7 +27,8 @@ def per_kernel(d, counter):
 
 def main():
     fdir, wdir, out, nsplit = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
-    alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    alg = float(sys.argv[5]) if len(sys.argv) > 5 and sys.argv[5] else None
+    prefix = sys.argv[6] if len(sys.argv) > 6 else "k_vc_fine"
     f = per_kernel(fdir, "FETCH_SIZE")
     w = per_kernel(wdir, "WRITE_SIZE")
     rows = []
@@ -34,13 +37,13 @@ def main():
         wk = sum(w.get(key, [0])) / max(1, len(w.get(key, [])))
         rows.append(dict(kernel=key[0], grid=key[1], fetch_bytes=2 * fk * 1024, write_bytes=wk * 1024,
                          hbm_bytes=2 * fk * 1024 + wk * 1024, n=len(f.get(key, []))))
-    smooth = [r for r in rows if r["kernel"].startswith("void k_smooth<false, true>")]
+    smooth = [r for r in rows if r["kernel"].replace("void ", "").startswith(prefix.replace("void ", ""))]
     smooth.sort(key=lambda r: -r["grid"])
     res = {"n_split": nsplit, "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1, KiB->B",
            "kernels": rows}
     if smooth:
         res["hbm_bytes_per_launch"] = smooth[0]["hbm_bytes"]
-        res["smooth_l1"] = smooth[0]
+        res["kernel"] = smooth[0]
         if alg:
             res["alg_bytes_per_launch"] = alg
             res["traffic_over_alg"] = smooth[0]["hbm_bytes"] / alg
@@ -48,7 +51,7 @@ def main():
     for r in rows[:12]:
         print(f"{r['kernel'][:36]:36s} {r['grid']:9d} fetch {r['fetch_bytes']/1e6:9.1f} MB  write {r['write_bytes']/1e6:9.1f} MB")
     if smooth:
-        print("l1 smooth hbm bytes/launch", smooth[0]["hbm_bytes"], res.get("traffic_over_alg"))
+        print(prefix, "hbm bytes/launch", smooth[0]["hbm_bytes"], res.get("traffic_over_alg"))
 
 
 if __name__ == "__main__":
