@@ -166,6 +166,7 @@ int halo(pamg_handle *h, int l) {
 int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
     Level &L = h->lv[l];
     h->tnn_level = l;
+    h->overlap_static_l1 = false;   // the per-step smoother writes every halo word of level l
     if (sweeps <= 0) {
         if (src_is_T) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
         return PAMG_OK;
@@ -204,6 +205,7 @@ int restrict_(pamg_handle *h, int l);
 
 // told changed on level l: refresh the compact told copy the halo reads
 int refresh_told_halo(pamg_handle *h, int l) {
+    h->overlap_static_l1 = false;
     HIPCHK(h, launch_told_halo(h->stream, h->lv[l], h->U));
     return PAMG_OK;
 }
@@ -260,6 +262,10 @@ double vcycle_coarse_bytes(pamg_handle *h) {
 int vcycle_once(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     if (h->p.fused && vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, ns)) {
+        if (!h->overlap_static_l1) {   // once per time step: the halo words the cycle's last smoother
+            HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo));   // leaves constant
+            h->overlap_static_l1 = true;
+        }
         if (L > 1) {   // levels 2..L first: level 1's halo words are the cycle's last
             Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h));
             HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse,
@@ -429,9 +435,14 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         L.T = base; L.TNN = base + 3 * L.pitch; L.RHS = base + 6 * L.pitch; L.RES = base + 9 * L.pitch;
         L.TOLD = base + 12 * L.pitch;
         std::vector<double> stc((size_t)std::max(Ul, 1) * kStcStride, 0.0);
-        for (int q = 0; q < Ul; ++q)
+        for (int q = 0; q < Ul; ++q) {
             level_stencil(X + 6 * (size_t)h->owned[q], L.isplit, h->p.k, h->p.dt, h->p.omega,
                           &stc[(size_t)q * kStcStride]);
+            if (!mass_is_p1_midpoint(&stc[(size_t)q * kStcStride])) {
+                h->err = "mass matrix of un_ele " + std::to_string(h->owned[q] + 1) + " is not c*[[2,1,1],[1,2,1],[1,1,2]]";
+                return PAMG_ERR_STATE;
+            }
+        }
         CHK(dev_upload(h, &L.stc, stc));
         std::vector<int2> sub(L.nsub);
         for (int e = 1; e <= L.nsub; ++e) {

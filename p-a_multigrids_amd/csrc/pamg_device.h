@@ -15,13 +15,16 @@ constexpr int kBlock = 256;
 __device__ __forceinline__ double2 ld2(const double *p) { return *reinterpret_cast<const double2 *>(p); }
 __device__ __forceinline__ void st2(double *p, double2 v) { *reinterpret_cast<double2 *>(p) = v; }
 
+// The P1 mass matrix of the reference's 3-point edge-midpoint rule is exactly
+// M = c [[2,1,1],[1,2,1],[1,1,2]] with c = detwei / 4 (every product N_gi w_g N_gj is
+// 0 or 0.25 detwei, detwei equal at the three points of an affine element); the host
+// checks this bit for bit (level_stencil). The kernels therefore keep c, not M.
 struct Stc {
-    double M[9], K[9], w[3];
+    double c, K[9], w[3];
 };
 
 __device__ __forceinline__ void load_stc(const double *__restrict__ rec, Stc &S) {
-#pragma unroll
-    for (int q = 0; q < 9; q += 1) S.M[q] = rec[kStcM + q];
+    S.c = rec[kStcC];
 #pragma unroll
     for (int q = 0; q < 9; q += 1) S.K[q] = rec[kStcK + q];
 #pragma unroll
@@ -30,12 +33,18 @@ __device__ __forceinline__ void load_stc(const double *__restrict__ rec, Stc &S)
 
 // get_A_x (transport_tri_semi.F90:412-448) with theta = 1 and the zero
 // advection / flux / surface terms folded: A_i = rdt*(M x)_i + (Kd x)_i.
+// (M x)_i is the reference's (M_i1 x_1 + M_i2 x_2) + M_i3 x_3 to the last bit: with
+// y_j = c x_j the diagonal product M_ii x_i = (2c) x_i is exactly 2 y_i, so
+// M_i1 x_1 + M_i2 x_2 is one fma(2, y_i, y_j) (a single rounding of an exact sum, as
+// the reference's add) -- 9 operations instead of 15.
 __device__ __forceinline__ void apply_A(const Stc &S, double rdt, const double x[3], double A[3]) {
+    const double y0 = S.c * x[0], y1 = S.c * x[1], y2 = S.c * x[2];
+    const double mx[3] = {__builtin_fma(2.0, y0, y1) + y2, __builtin_fma(2.0, y1, y0) + y2,
+                          __builtin_fma(2.0, y2, y0 + y1)};
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        double mx = S.M[3 * i] * x[0] + S.M[3 * i + 1] * x[1] + S.M[3 * i + 2] * x[2];
         double kx = S.K[3 * i] * x[0] + S.K[3 * i + 1] * x[1] + S.K[3 * i + 2] * x[2];
-        A[i] = rdt * mx + kx;
+        A[i] = rdt * mx[i] + kx;
     }
 }
 
@@ -63,10 +72,17 @@ struct HaloArgs {
 // the iterate before the last sweep, which is what these threads hold in p[].
 // The halo metadata (face positions, face records, told) is fetched before the
 // sweeps so its latency hides under the arithmetic.
+// TNEW / STATIC select the words written: TNEW the tnew copies (t_overlap of a
+// neighbour on this rank, the tnew half of a send entry); STATIC the words that do
+// not change within a time step (t_overlap_old from told, the boundary values of
+// both arrays, the told half of a send entry). The per-step kernels write both;
+// the fused V-cycle writes TNEW only and leaves STATIC to k_overlap_static.
+template <bool TNEW = true, bool STATIC = true>
 __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, int i, const double t[3],
                                           const double to[3]) {
     const int mode = rec.x & 3;
     if (mode == 0) {   // domain boundary: BC values into the own column (:1243-1252, :1287-1295, :1345-1353)
+        if (!STATIC) return;
         const int a = (i - 1) * 3 + (f == 3 ? 1 : 0);
         const int b = (i - 1) * 3 + (f == 2 ? 1 : 2);
         const double2 v = H.bcv[rec.z + i - 1];
@@ -78,11 +94,17 @@ __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, in
         const int k = (rec.x >> 2) ? (H.m - i + 1) : i;
         const int64_t d = rec.y + (int64_t)(k - 1) * 3;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) { H.tov[d + c] = t[c]; H.tovo[d + c] = to[c]; }
+        for (int c = 0; c < 3; ++c) {
+            if (TNEW) H.tov[d + c] = t[c];
+            if (STATIC) H.tovo[d + c] = to[c];
+        }
     } else {                  // neighbour on another rank: packed send buffer (RCCL)
         double *o = H.send + 6 * (int64_t)(rec.z + i - 1);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) { o[c] = t[c]; o[3 + c] = to[c]; }
+        for (int c = 0; c < 3; ++c) {
+            if (TNEW) o[c] = t[c];
+            if (STATIC) o[3 + c] = to[c];
+        }
     }
 }
 

@@ -15,10 +15,11 @@ constexpr int kMaxLevels = 12;
 constexpr int kMaxFusedLevels = 5;
 
 // Per (un_ele, level) operator record, fp64, 32 doubles = 256 B (two 128-B lines):
-// M (3x3 row-major) | Kd (3x3 row-major) | w = omega / D (3) | pad.
+// M (3x3 row-major) | Kd (3x3 row-major) | w = omega / D (3) | c = M_12 | pad.
 // M and Kd are get_un_ele_mass_stiff_diffvol (ShapFun_unstruc.F90:304-335) reduced as
-// transport_tri_semi.F90:592-607; D is get_diagonal (:481-486).
-constexpr int kStcM = 0, kStcK = 9, kStcW = 18, kStcStride = 32;
+// transport_tri_semi.F90:592-607; D is get_diagonal (:481-486); M = c [[2,1,1],[1,2,1],[1,1,2]]
+// exactly (checked in level_stencil), which the smoother kernels use (pamg_device.h apply_A).
+constexpr int kStcM = 0, kStcK = 9, kStcW = 18, kStcC = 21, kStcStride = 32;
 
 // Level-1 geometry record per un_ele (get_splitting, Msh2Tri.F90:69-107):
 // x3, y3, v1x, v1y, v2x, v2y (v = edge / 2**i_split), pad to 8 doubles.
@@ -100,6 +101,10 @@ struct pamg_handle {
     double *tov = nullptr, *tovo = nullptr; // (slots, 3, U) t_overlap / t_overlap_old
     int slots = 0;
     int tnn_level = 1;
+    // t_overlap_old and the boundary words hold what level 1's smoother writes in this
+    // time step (the fused V-cycle then writes only the tnew words); cleared by every
+    // operation that writes or changes them otherwise
+    bool overlap_static_l1 = false;
     bool mesh_ready = false;
     std::string err;
     pamg::Timing timing;
@@ -117,6 +122,8 @@ void element_conversion(int fin[4], int coarse_ele, int i_split);
 void loc_surf_ele(int n, std::vector<int> &surf);
 void get_splitting(const double *un_x, int n_split, int str_ele, double str_x[3][2]);
 void level_stencil(const double *X, int i_split, double k, double dt, double omega, double *rec);
+// M == c [[2,1,1],[1,2,1],[1,1,2]] bit for bit (the form the smoother kernels evaluate)
+bool mass_is_p1_midpoint(const double *rec);
 int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const int *fneig, const int *dir);
 }  // namespace pamg
 
@@ -131,6 +138,7 @@ hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double 
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
 hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
 hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);
+hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo);
 // fused V-cycle (pamg_vcycle.hip); lv is the handle's 1-based level array
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth);
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,

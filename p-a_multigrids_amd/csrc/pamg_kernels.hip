@@ -45,6 +45,36 @@ __global__ __launch_bounds__(kBlock) void k_told_halo(const double *__restrict__
     for (int c = 0; c < 3; ++c) o[c] = TOLD[c * pitch + s];
 }
 
+// The halo words that are constant within a time step (t_overlap_old from told, the
+// boundary values sin(x + y) of both arrays, the told half of the send entries), as
+// the level's smoother writes them (update_overlaps, splitting.F90:1210-1397); one
+// thread per (un_ele, face, position), the order of k_told_halo. The fused V-cycle
+// writes only the tnew words; this kernel runs before its first launch in a time step.
+__global__ __launch_bounds__(kBlock) void k_overlap_static(HaloArgs H, const int *__restrict__ surf, int U) {
+    const int m = H.m;
+    const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= (int64_t)U * 3 * m) return;
+    const int i = (int)(idx % m) + 1;
+    const int f = (int)((idx / m) % 3) + 1;
+    const int64_t q = idx / (3 * m);
+    const int4 rec = H.hface[3 * q + f - 1];
+    double to[3] = {0.0, 0.0, 0.0};
+    if (rec.x & 3) {
+        // the sub-element's told sits in the compact told halo at its first copied face
+        const int sub = surf[(i - 1) + (f - 1) * m] - 1;
+        const int4 hs = H.hsub[sub];
+        const int4 r[3] = {H.hface[3 * q], H.hface[3 * q + 1], H.hface[3 * q + 2]};
+        const int pos[3] = {hs.x, hs.y, hs.z};
+        int e = -1;
+        for (int g = 0; g < 3 && e < 0; ++g)
+            if (pos[g] && (r[g].x & 3)) e = r[g].w + pos[g] - 1;
+        if (e >= 0)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) to[c] = H.told[3 * (int64_t)e + c];
+    }
+    halo_face<false, true>(H, rec, f, i, to, to);
+}
+
 // Fused smoother call(s): `sweeps` consecutive sweeps kept in registers.
 // Reference semantics (:548-550): each sweep starts with tnew := tnew_nonlin,
 // so after the call tnew holds the iterate before the last sweep and
@@ -597,6 +627,15 @@ hipError_t launch_told_halo(hipStream_t s, const Level &L, int U) {
     const int m = 1 << L.isplit;
     hipLaunchKernelGGL(k_told_halo, dim3(grid_for((int64_t)U * 3 * m)), dim3(kBlock), 0, s, L.TOLD, L.pitch,
                        P.d_hface, P.d_surf, P.d_told_halo, U, m, log2i(L.nsub));
+    return hipGetLastError();
+}
+
+hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo) {
+    const HaloPlan &P = L.halo;
+    if (U == 0 || P.d_hface == nullptr) return hipSuccess;
+    const int m = 1 << L.isplit;
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, m};
+    hipLaunchKernelGGL(k_overlap_static, dim3(grid_for((int64_t)U * 3 * m)), dim3(kBlock), 0, s, H, P.d_surf, U);
     return hipGetLastError();
 }
 

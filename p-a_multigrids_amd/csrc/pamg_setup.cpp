@@ -146,6 +146,15 @@ void level_stencil(const double *X, int i_split, double k, double dt, double ome
         double D = rdt * ml[i] + Kd[i][i] + 0.0;
         rec[kStcW + i] = omega / D;
     }
+    rec[kStcC] = M[0][1];
+}
+
+bool mass_is_p1_midpoint(const double *rec) {
+    const double c = rec[kStcC];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            if (rec[kStcM + 3 * i + j] != (i == j ? 2.0 * c : c)) return false;
+    return true;
 }
 
 // Halo plan of update_overlaps (splitting.F90:1210-1397) for level l:

@@ -31,6 +31,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "pamg_device.h"
@@ -42,7 +43,7 @@ namespace {
 using namespace detail;
 
 constexpr int kMTf = 512;   // threads per workgroup, level-0 kernel (one adjacent pair each)
-constexpr int kMTc = 256;   // threads per workgroup, coarse-level kernel (one level-1 sub-element each)
+constexpr int kMTc = 64;    // threads per workgroup, coarse-level kernel (one wave per tile)
 
 struct VLevel {
     double *T, *TNN, *RHS, *RES;
@@ -57,6 +58,7 @@ struct VArgs {
     int64_t U;
     int n_smooth, n_coarse;
     double rdt;
+    int cascade;            // 0: skip the (dead) prolongator cascades (PAMG_DIAG_NOCASCADE diagnostics)
     long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
 };
 
@@ -86,17 +88,6 @@ struct Geo {
     static constexpr int nt(int l) { return 1024 >> (2 * l); }
     // each wave inside one un_ele (a wave spans 128 level-0 sub-elements, 64 of any other level)
     static constexpr bool uni(int l) { return lg(l) >= (l == 0 ? 7 : 6); }
-    // coarse kernel LDS: old residual R_l and restriction-leg tnew F_l (1 <= l < C), final tnew Y_l (2 <= l <= C)
-    static constexpr int off(int l) {   // 3 * (nt(1) + ... + nt(l-1))
-        int o = 0;
-        for (int i = 1; i < l; ++i) o += 3 * nt(i);
-        return o;
-    }
-    static constexpr int nR = off(C);
-    static constexpr int R(int l) { return off(l); }
-    static constexpr int F(int l) { return nR + off(l); }
-    static constexpr int Y(int l) { return 2 * nR + off(l) - off(2); }
-    static constexpr int coarse_total = (C >= 2) ? 2 * nR + off(C + 1) - off(2) : 1;
 };
 
 // field access: wave-uniform plane base (SGPRs) + 32-bit sub-element index (one VGPR for all planes)
@@ -131,6 +122,14 @@ __device__ __forceinline__ void copy3(double d[3], const double s[3]) {
     for (int c = 0; c < 3; ++c) d[c] = s[c];
 }
 
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
 // operator record of un_ele u; wave-uniform records come through the scalar cache
 // (uni is a compile-time constant at every call site once the level loops are unrolled)
 __device__ __forceinline__ void stencil(bool uni, const double *__restrict__ stc, uint32_t u, Stc &S) {
@@ -157,6 +156,18 @@ __device__ __forceinline__ void sweeps2(const Stc &S, double rdt, int n, const d
     }
 }
 
+// N sub-elements of one un_ele, interleaved
+template <int N>
+__device__ __forceinline__ void sweepsN(const Stc &S, double rdt, int n, const double b[N][3], double x[N][3],
+                                        double p[N][3]) {
+    for (int it = 0; it < n; ++it) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) copy3(p[q], x[q]);
+#pragma unroll
+        for (int q = 0; q < N; ++q) sweep(S, rdt, b[q], x[q]);
+    }
+}
+
 __device__ __forceinline__ void residual(const Stc &S, double rdt, const double p[3], const double b[3],
                                          double r[3]) {
     double a[3];
@@ -169,33 +180,16 @@ __device__ __forceinline__ void residual(const Stc &S, double rdt, const double 
 // h: its positions along faces 1..3 packed 6 bits each (0: not on that face)
 __device__ __forceinline__ int hs_pack(int4 q) { return q.x | (q.y << 6) | (q.z << 12); }
 
-// told of a boundary sub-element (compact told halo entry of its first copied face), fetched
-// once in the prologue so that no halo write waits on a dependent load
-__device__ __forceinline__ void hs_told(bool uni, const HaloArgs &H, uint32_t u, int h, double to[3]) {
-    to[0] = to[1] = to[2] = 0.0;
+// tnew words of the halo (update_overlaps); t_overlap_old and the boundary values are
+// constant within a time step and are written by k_overlap_static (pamg_kernels.hip)
+__device__ __forceinline__ void hs_write(bool uni, const HaloArgs &H, uint32_t u, int h, const double t[3]) {
     if (h == 0) return;
     if (uni) u = __builtin_amdgcn_readfirstlane(u);
     const int4 r1 = H.hface[3 * u], r2 = H.hface[3 * u + 1], r3 = H.hface[3 * u + 2];
     const int a = h & 63, b = (h >> 6) & 63, c = h >> 12;
-    int e = -1;
-    if (a && (r1.x & 3)) e = r1.w + a - 1;
-    else if (b && (r2.x & 3)) e = r2.w + b - 1;
-    else if (c && (r3.x & 3)) e = r3.w + c - 1;
-    if (e >= 0) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) to[k] = H.told[3 * (int64_t)e + k];
-    }
-}
-
-__device__ __forceinline__ void hs_write(bool uni, const HaloArgs &H, uint32_t u, int h, const double t[3],
-                                         const double to[3]) {
-    if (h == 0) return;
-    if (uni) u = __builtin_amdgcn_readfirstlane(u);
-    const int4 r1 = H.hface[3 * u], r2 = H.hface[3 * u + 1], r3 = H.hface[3 * u + 2];
-    const int a = h & 63, b = (h >> 6) & 63, c = h >> 12;
-    if (a) halo_face(H, r1, 1, a, t, to);
-    if (b) halo_face(H, r2, 2, b, t, to);
-    if (c) halo_face(H, r3, 3, c, t, to);
+    if (a) halo_face<true, false>(H, r1, 1, a, t, t);
+    if (b) halo_face<true, false>(H, r2, 2, b, t, t);
+    if (c) halo_face<true, false>(H, r3, 3, c, t, t);
 }
 
 // prolongator cascade (splitting.F90:59-88) on the LDS image of the fine tile (component stride n)
@@ -224,7 +218,46 @@ __device__ __forceinline__ void prolong_cascade(double *F, int n, const int fi[4
 }
 
 // ===================================================================== coarse levels
-// Ownership: level l >= 1 -> sub-element t of the tile (if t < n_l).
+// One wave per tile. Level l >= 1 of a tile has nt(l) sub-elements; lane t owns the
+// sub-elements t + 64 k, k < K(l) = max(1, nt(l) / 64), that are < nt(l): four of
+// level 1, one of level 2, one on the first nt(l) lanes below. The coarsest level's
+// 1 + n_coarse smoother calls are a chain of dependent sweeps, issue-bound on the
+// wave that runs it; with one wave per tile no wave waits on it, and the many tiles
+// resident per CU overlap their memory phases with the chains of the others.
+// LDS per level l: B_l = RHS (3 x nt(l)), W_l = tnew: the restriction-leg iterate
+// (l < C) or, on the coarsest level, its tnew, and Y_l (2 <= l < C) the final tnew of
+// a middle level (input of the prolongator cascade into level l - 1).
+template <int S, int L>
+struct CGeo {
+    using G = Geo<S, L>;
+    static constexpr int C = G::C;
+    static constexpr int K(int l) { return G::nt(l) >= 64 ? G::nt(l) / 64 : 1; }
+    // every lane of a chunk inside one un_ele (operator records through the scalar cache)
+    static constexpr bool uni(int l) { return (G::nt(l) < 64 ? G::nt(l) : 64) <= (1 << G::lg(l)); }
+    // every chunk of the level inside one un_ele: the chunks are smoothed together (ILP)
+    static constexpr bool one(int l) { return G::nt(l) <= (1 << G::lg(l)); }
+    static constexpr int sz(int l) { return 3 * G::nt(l); }
+    static constexpr int B(int l) {
+        int o = 0;
+        for (int i = 1; i < l; ++i) o += 2 * sz(i);
+        return o;
+    }
+    static constexpr int W(int l) { return B(l) + sz(l); }
+    static constexpr int Y(int l) {   // 2 <= l < C
+        int o = B(C + 1);
+        for (int i = 2; i < l; ++i) o += sz(i);
+        return o;
+    }
+    static constexpr int dump = Y(C);            // 3 slots per lane for the stores of idle lanes
+    static constexpr int total = dump + 3 * 64;
+    // restrictor chunks: (level l + 1, chunk k) for l = 0..C-1
+    static constexpr int nrc() {
+        int n = 0;
+        for (int l = 1; l <= C; ++l) n += K(l);
+        return n;
+    }
+};
+
 template <int S, int L>
 __global__ __launch_bounds__(kMTc) void k_vc_coarse(VArgs A, const double *__restrict__ sp1,
                                                     const double *__restrict__ sp2, const double *__restrict__ sp3,
@@ -233,9 +266,10 @@ __global__ __launch_bounds__(kMTc) void k_vc_coarse(VArgs A, const double *__res
     // records are fetched with scalar loads
     const double *__restrict__ SP[kMaxFusedLevels] = {nullptr, sp1, sp2, sp3, sp4};
     using G = Geo<S, L>;
+    using Q = CGeo<S, L>;
     constexpr int C = G::C;
     static_assert(C >= 1, "coarse kernel needs two levels");
-    __shared__ __attribute__((aligned(16))) double lds[G::coarse_total];
+    __shared__ __attribute__((aligned(16))) double lds[Q::total];
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
@@ -243,130 +277,180 @@ __global__ __launch_bounds__(kMTc) void k_vc_coarse(VArgs A, const double *__res
     const int nue = (int)min((int64_t)1 << G::GL, A.U - u0);
     stamp<kMTc>(A, 0);
     stamp_hwid<kMTc>(A);
-    bool vl[L];
-    uint32_t sl[L];
+    // chunk k of level l: tile index t + 64 k, valid if inside the tile's un_eles; idle
+    // lanes load index 0 (in bounds) and store to the dump slots (no branches, so the
+    // loads of a phase are all in flight together)
+    auto ok = [&](int l, int k) -> bool { return t + 64 * k < G::nt(l) && t + 64 * k < (nue << G::lg(l)); };
+    auto gix = [&](int l, int k) -> uint32_t {
+        return ((uint32_t)u0 << G::lg(l)) + (uint32_t)(ok(l, k) ? t + 64 * k : 0);
+    };
+    auto lix = [&](int base, int l, int k, int c) -> int {   // LDS slot of component c
+        return ok(l, k) ? base + c * G::nt(l) + t + 64 * k : Q::dump + 3 * t + c;
+    };
+    // ---- prologue, batch 1: tnew of every level (tnew_nonlin := tnew, :327 / :348), halo
+    //      positions, children of the restrictor chunks
+    int hl[L][4];
+    double xi[L][4][3];
+    int4 ch[L][4];
 #pragma unroll
-    for (int l = 1; l < L; ++l) {
-        vl[l] = t < (nue << G::lg(l));
-        sl[l] = ((uint32_t)u0 << G::lg(l)) + (vl[l] ? t : 0);   // clamped: loads stay in bounds
-    }
-    // ---- prologue
-    int hl[L];
+    for (int l = 1; l < L; ++l)
 #pragma unroll
-    for (int l = 1; l < L; ++l) hl[l] = vl[l] ? hs_pack(A.lv[l].H.hsub[sl[l] & ((1 << G::lg(l)) - 1)]) : 0;
-    double rl[L][3], xl[L][3], bl[L][3], tl[L][3];
-#pragma unroll
-    for (int l = 1; l < C; ++l) load3(A.lv[l].RES, A.lv[l].pitch, sl[l], rl[l]);
-#pragma unroll
-    for (int l = 1; l < L; ++l) load3(A.lv[l].T, A.lv[l].pitch, sl[l], xl[l]);
-#pragma unroll
-    for (int l = 1; l < L; ++l) hs_told(G::uni(l), A.lv[l].H, sl[l] >> G::lg(l), hl[l], tl[l]);
-    // restrictor of level 1 (:336) straight from the level-0 residual of the previous cycle
-    // (level 0 is rewritten only by the next launch)
-    {
-        const VLevel &V0 = A.lv[0];
-        const int4 c4 = A.lv[1].children[sl[1] & ((1 << G::lg(1)) - 1)];
-        const uint32_t base = (sl[1] >> G::lg(1)) << G::lg(0);
-        const uint32_t pick[3] = {base + c4.z, base + c4.w, base + c4.x};
-        double r[3][3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) load3(V0.RES, V0.pitch, pick[i], r[i]);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) bl[1][i] = (r[i][0] + r[i][1] + r[i][2]) / 3.;
-        if (vl[1]) store3(A.lv[1].RHS, A.lv[1].pitch, sl[1], bl[1]);
-    }
-    if constexpr (C >= 2) {
-#pragma unroll
-        for (int l = 1; l < C; ++l)
-            if (vl[l])
-#pragma unroll
-                for (int c = 0; c < 3; ++c) lds[G::R(l) + c * G::nt(l) + t] = rl[l][c];
-        __syncthreads();
-#pragma unroll
-        for (int l = 1; l < C; ++l) {
-            if (!vl[l + 1]) continue;
-            const double *R = lds + G::R(l);
-            const int base = (t >> G::lg(l + 1)) << G::lg(l);
-            const int4 c4 = A.lv[l + 1].children[sl[l + 1] & ((1 << G::lg(l + 1)) - 1)];
-            const int pick[3] = {base + c4.z, base + c4.w, base + c4.x};
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-                bl[l + 1][i] = (R[pick[i]] + R[G::nt(l) + pick[i]] + R[2 * G::nt(l) + pick[i]]) / 3.;
-            store3(A.lv[l + 1].RHS, A.lv[l + 1].pitch, sl[l + 1], bl[l + 1]);
+        for (int k = 0; k < Q::K(l); ++k) {
+            const uint32_t g = gix(l, k);
+            load3(A.lv[l].T, A.lv[l].pitch, g, xi[l][k]);
+            const int4 hs = A.lv[l].H.hsub[g & ((1 << G::lg(l)) - 1)];
+            hl[l][k] = ok(l, k) ? hs_pack(hs) : 0;
+            ch[l][k] = A.lv[l].children[g & ((1 << G::lg(l)) - 1)];
         }
-    }
+#pragma unroll
+    for (int l = 1; l < L; ++l)
+#pragma unroll
+        for (int k = 0; k < Q::K(l); ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) lds[lix(Q::W(l), l, k, c)] = xi[l][k][c];
+    // ---- batch 2: restrictor (:336) of every level from the residual of the PREVIOUS cycle,
+    //      RHS_{l+1}(1, c) = mean(res_l(:, f3)), (2, c) = mean(res_l(:, f4)), (3, c) = mean(res_l(:, f1))
+    //      (splitting.F90:10-32, 146-151); all read before any residual is rewritten
+    double rr[L][4][3][3];
+#pragma unroll
+    for (int l = 0; l < C; ++l)
+#pragma unroll
+        for (int k = 0; k < Q::K(l + 1); ++k) {
+            const uint32_t g = gix(l + 1, k);
+            const int4 c4 = ch[l + 1][k];
+            const uint32_t base = (g >> G::lg(l + 1)) << G::lg(l);
+            const uint32_t pick[3] = {base + c4.z, base + c4.w, base + c4.x};
+#pragma unroll
+            for (int q = 0; q < 3; ++q) load3(A.lv[l].RES, A.lv[l].pitch, pick[q], rr[l + 1][k][q]);
+        }
+#pragma unroll
+    for (int l = 1; l <= C; ++l)
+#pragma unroll
+        for (int k = 0; k < Q::K(l); ++k) {
+            double b[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) b[q] = (rr[l][k][q][0] + rr[l][k][q][1] + rr[l][k][q][2]) / 3.;
+            if (ok(l, k)) store3(A.lv[l].RHS, A.lv[l].pitch, gix(l, k), b);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) lds[lix(Q::B(l), l, k, c)] = b[c];
+        }
     stamp<kMTc>(A, 1);
-    // ---- levels 1..C-1, restriction leg: smoother (:331), get_residual (:338)
+    // smoother calls on the chunks of level l (x from W, b from B); the chunks of one un_ele
+    // are interleaved (ILP), otherwise each reads its own operator record
+    auto smooth_chunks = [&](auto LC, int nsw, double (&x)[4][3], const double (&b)[4][3], double (&p)[4][3]) {
+        constexpr int l = decltype(LC)::value;
+        constexpr int K = Q::K(l);
+        if constexpr (Q::one(l)) {
+            Stc St;
+            stencil(Q::uni(l), SP[l], gix(l, 0) >> G::lg(l), St);
+            sweepsN<K>(St, rdt, nsw, reinterpret_cast<const double(&)[K][3]>(b),
+                       reinterpret_cast<double(&)[K][3]>(x), reinterpret_cast<double(&)[K][3]>(p));
+        } else {
 #pragma unroll
-    for (int l = 1; l < C; ++l) {
-        if (!vl[l]) continue;
+            for (int k = 0; k < K; ++k) {
+                Stc St;
+                stencil(Q::uni(l), SP[l], gix(l, k) >> G::lg(l), St);
+                sweeps(St, rdt, nsw, b[k], x[k], p[k]);
+            }
+        }
+    };
+    auto residual_chunks = [&](auto LC, const double (&b)[4][3], const double (&p)[4][3]) {
+        constexpr int l = decltype(LC)::value;
         const VLevel &V = A.lv[l];
-        const uint32_t u = sl[l] >> G::lg(l);
-        Stc St;
-        stencil(G::uni(l), SP[l], u, St);
-        double p[3];
-        sweeps(St, rdt, ns, bl[l], xl[l], p);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) lds[G::F(l) + c * G::nt(l) + t] = p[c];
-        hs_write(G::uni(l), V.H, u, hl[l], p, tl[l]);
-        double r[3];
-        residual(St, rdt, p, bl[l], r);
-        store3(V.RES, V.pitch, sl[l], r);
-    }
+        for (int k = 0; k < Q::K(l); ++k) {
+            Stc St;
+            stencil(Q::uni(l), SP[l], gix(l, k) >> G::lg(l), St);
+            double r[3];
+            residual(St, rdt, p[k], b[k], r);
+            if (ok(l, k)) store3(V.RES, V.pitch, gix(l, k), r);
+        }
+    };
+    auto load_wb = [&](auto LC, double (&x)[4][3], double (&b)[4][3]) {
+        constexpr int l = decltype(LC)::value;
+#pragma unroll
+        for (int k = 0; k < Q::K(l); ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                x[k][c] = lds[lix(Q::W(l), l, k, c)];
+                b[k][c] = lds[lix(Q::B(l), l, k, c)];
+            }
+    };
+    auto halo_chunks = [&](auto LC, const double (&p)[4][3]) {
+        constexpr int l = decltype(LC)::value;
+#pragma unroll
+        for (int k = 0; k < Q::K(l); ++k) hs_write(Q::uni(l), A.lv[l].H, gix(l, k) >> G::lg(l), hl[l][k], p[k]);
+    };
+    // ---- levels 1..C-1, restriction leg: smoother (:331), get_residual (:338)
+    static_for<1, C>([&](auto LC) {
+        constexpr int l = decltype(LC)::value;
+        double x[4][3], b[4][3], p[4][3];
+        load_wb(LC, x, b);
+        smooth_chunks(LC, ns, x, b, p);
+#pragma unroll
+        for (int k = 0; k < Q::K(l); ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) lds[lix(Q::W(l), l, k, c)] = p[k][c];
+        halo_chunks(LC, p);
+        residual_chunks(LC, b, p);
+    });
     stamp<kMTc>(A, 2);
     // ---- coarsest level: smoother + get_residual of the restriction leg, then the
-    //      15 smoother calls from tnew_nonlin := tnew (:344-359)
-    if (vl[C]) {
-        const VLevel &V = A.lv[C];
-        const uint32_t u = sl[C] >> G::lg(C);
-        Stc St;
-        stencil(G::uni(C), SP[C], u, St);
-        double p[3];
-        sweeps(St, rdt, ns, bl[C], xl[C], p);
-        hs_write(G::uni(C), V.H, u, hl[C], p, tl[C]);
-        double r[3];
-        residual(St, rdt, p, bl[C], r);
-        store3(V.RES, V.pitch, sl[C], r);
-        copy3(xl[C], p);
-        sweeps(St, rdt, ns * A.n_coarse, bl[C], xl[C], p);
-        hs_write(G::uni(C), V.H, u, hl[C], p, tl[C]);
-        store3(V.T, V.pitch, sl[C], p);
-        if constexpr (C >= 2)
+    //      n_coarse smoother calls from tnew_nonlin := tnew (:344-359)
+    {
+        using LC = std::integral_constant<int, C>;
+        double x[4][3], b[4][3], p[4][3];
+        load_wb(LC{}, x, b);
+        smooth_chunks(LC{}, ns, x, b, p);
+        halo_chunks(LC{}, p);
+        residual_chunks(LC{}, b, p);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) lds[G::Y(C) + c * G::nt(C) + t] = p[c];
+        for (int k = 0; k < Q::K(C); ++k) copy3(x[k], p[k]);
+        smooth_chunks(LC{}, ns * A.n_coarse, x, b, p);
+        halo_chunks(LC{}, p);
+#pragma unroll
+        for (int k = 0; k < Q::K(C); ++k) {
+            if (ok(C, k)) store3(A.lv[C].T, A.lv[C].pitch, gix(C, k), p[k]);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) lds[lix(Q::W(C), C, k, c)] = p[k][c];
+        }
     }
     stamp<kMTc>(A, 3);
     // ---- prolongation leg, levels C-1..1: smoother from tnew_nonlin = restriction-leg tnew (:367, :376)
+    static_for<1, C>([&](auto LR) {
+        constexpr int l = C - decltype(LR)::value;
+        using LC = std::integral_constant<int, l>;
+        double x[4][3], b[4][3], p[4][3];
+        load_wb(LC{}, x, b);
+        smooth_chunks(LC{}, ns, x, b, p);
+        halo_chunks(LC{}, p);
 #pragma unroll
-    for (int l = C - 1; l >= 1; --l) {
-        if (!vl[l]) continue;
-        const VLevel &V = A.lv[l];
-        const uint32_t u = sl[l] >> G::lg(l);
-        Stc St;
-        stencil(G::uni(l), SP[l], u, St);
-        double x[3], p[3];
+        for (int k = 0; k < Q::K(l); ++k) {
+            if (ok(l, k)) store3(A.lv[l].T, A.lv[l].pitch, gix(l, k), p[k]);
+            if constexpr (l >= 2)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) x[c] = lds[G::F(l) + c * G::nt(l) + t];
-        sweeps(St, rdt, ns, bl[l], x, p);
-        hs_write(G::uni(l), V.H, u, hl[l], p, tl[l]);
-        store3(V.T, V.pitch, sl[l], p);
-        if (l >= 2)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) lds[G::Y(l) + c * G::nt(l) + t] = p[c];
-    }
+                for (int c = 0; c < 3; ++c) lds[lix(Q::Y(l), l, k, c)] = p[k][c];
+        }
+    });
     stamp<kMTc>(A, 4);
-    // ---- prolongator (:370) among the coarse levels, on the LDS images (its result is dead)
+    // ---- prolongator (:370) among the coarse levels, on the LDS images of the
+    //      restriction-leg tnew (its result is dead, :550)
     if constexpr (C >= 2) {
         __syncthreads();
 #pragma unroll
         for (int l = 1; l < C; ++l) {
-            if (!vl[l + 1]) continue;
-            const double *Y = lds + G::Y(l + 1);
-            const int base = (t >> G::lg(l + 1)) << G::lg(l);
-            const int4 c4 = A.lv[l + 1].children[sl[l + 1] & ((1 << G::lg(l + 1)) - 1)];
-            const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
-            const double y[3] = {Y[t], Y[G::nt(l + 1) + t], Y[2 * G::nt(l + 1) + t]};
-            prolong_cascade(lds + G::F(l), G::nt(l), fi, y);
+            const int ysrc = (l + 1 == C) ? Q::W(C) : Q::Y(l + 1);
+#pragma unroll
+            for (int k = 0; k < Q::K(l + 1); ++k) {
+                if (!ok(l + 1, k)) continue;
+                const int j = t + 64 * k;
+                const int4 c4 = ch[l + 1][k];
+                const int base = (j >> G::lg(l + 1)) << G::lg(l);
+                const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+                const double y[3] = {lds[ysrc + j], lds[ysrc + G::nt(l + 1) + j], lds[ysrc + 2 * G::nt(l + 1) + j]};
+                prolong_cascade(lds + Q::W(l), G::nt(l), fi, y);
+            }
+            __syncthreads();
         }
     }
     stamp<kMTc>(A, 7);
@@ -395,7 +479,7 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     int h0[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) h0[k] = v0 ? hs_pack(V0.H.hsub[(s0 + k) & ((1 << G::lg(0)) - 1)]) : 0;
-    double x0[2][3], b0[2][3], p0[2][3], to0[2][3];
+    double x0[2][3], b0[2][3], p0[2][3];
     load3p(V0.T, V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
     load3p(V0.RHS, V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
     // final level-1 tnew (coarse launch) for the prolongator
@@ -409,8 +493,6 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
         load3(A.lv[1].T, A.lv[1].pitch, s1, y1);
         c4 = A.lv[1].children[s1 & ((1 << G::lg(1)) - 1)];
     }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) hs_told(G::uni(0), V0.H, w0, h0[k], to0[k]);
     Stc St;
     stencil(G::uni(0), sp0, w0, St);
     // ---- restriction leg: smoother (:331), get_residual (:338)
@@ -421,7 +503,7 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
 #pragma unroll
             for (int c = 0; c < 3; ++c) st2(F0 + c * 1024 + 2 * t, make_double2(p0[0][c], p0[1][c]));
 #pragma unroll
-        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, h0[k], p0[k], to0[k]);
+        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, h0[k], p0[k]);
         double r[2][3];
 #pragma unroll
         for (int k = 0; k < 2; ++k) residual(St, rdt, p0[k], b0[k], r[k]);
@@ -436,13 +518,14 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     stamp<kMTf>(A, 3);
     if (v0) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, h0[k], p0[k], to0[k]);
+        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, h0[k], p0[k]);
         store3p(V0.T, V0.pitch, s0, p0[0], p0[1]);
         store3p(V0.TNN, V0.pitch, s0, x0[0], x0[1]);
     }
     stamp<kMTf>(A, 4);
     // ---- prolongator (:370) on the LDS image (its result is dead, :550)
     if constexpr (C > 0) {
+        if (!A.cascade) return;
         __syncthreads();
         if (v1) {
             const int base = (t >> G::lg(1)) << G::lg(0);
@@ -498,6 +581,8 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.n_smooth = n_smooth;
     A.n_coarse = n_coarse;
     A.rdt = rdt;
+    static const bool diag_nocascade = getenv("PAMG_DIAG_NOCASCADE") != nullptr;
+    A.cascade = diag_nocascade ? 0 : 1;
     const int GL = 10 - 2 * n_split;   // 1024 / 4**n_split un_eles per tile
     const unsigned grid = (unsigned)(((int64_t)U + (1 << GL) - 1) >> GL);
     if (grid == 0) return hipSuccess;
