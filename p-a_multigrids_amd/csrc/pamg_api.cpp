@@ -213,6 +213,7 @@ int refresh_told_halo(pamg_handle *h, int l) {
 // restrictor(l) + get_residual(l) as one kernel (V-cycle driver)
 int restrict_residual(pamg_handle *h, int l) {
     Level &L = h->lv[l];
+    h->rhsn_valid = false;
     if (l >= h->p.multi_levels || L.nsub > 1024) {
         CHK(restrict_(h, l));
         return residual(h, l);
@@ -225,6 +226,7 @@ int restrict_residual(pamg_handle *h, int l) {
 
 int residual(pamg_handle *h, int l) {
     Level &L = h->lv[l];
+    h->rhsn_valid = false;
     if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, false));   // get_RHS inside get_residual (:865-867)
     Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)L.N + 168.0 * h->U);
     HIPCHK(h, launch_residual(h->stream, L, 1 / h->p.dt));
@@ -262,6 +264,11 @@ double vcycle_coarse_bytes(pamg_handle *h) {
 int vcycle_once(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     if (h->p.fused && vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, ns)) {
+        if (!h->rhsn_valid) {   // residuals changed outside the fused cycle: restrict them afresh
+            for (int l = 1; l < L; ++l)
+                HIPCHK(h, launch_restrict(h->stream, h->lv[l], h->lv[l + 1], h->U, h->lv[l + 1].RHSN));
+            h->rhsn_valid = true;
+        }
         if (!h->overlap_static_l1) {   // once per time step: the halo words the cycle's last smoother
             HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo));   // leaves constant
             h->overlap_static_l1 = true;
@@ -430,10 +437,11 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         L.N = (int64_t)L.nsub * Ul;
         L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64);
         double *base = nullptr;
-        CHK(dev_alloc(h, &base, 15 * (size_t)L.pitch));
-        HIPCHK(h, hipMemsetAsync(base, 0, 15 * (size_t)L.pitch * sizeof(double), h->stream));
+        CHK(dev_alloc(h, &base, 18 * (size_t)L.pitch));
+        HIPCHK(h, hipMemsetAsync(base, 0, 18 * (size_t)L.pitch * sizeof(double), h->stream));
         L.T = base; L.TNN = base + 3 * L.pitch; L.RHS = base + 6 * L.pitch; L.RES = base + 9 * L.pitch;
         L.TOLD = base + 12 * L.pitch;
+        L.RHSN = base + 15 * L.pitch;   // restriction of the zero residual: valid
         std::vector<double> stc((size_t)std::max(Ul, 1) * kStcStride, 0.0);
         for (int q = 0; q < Ul; ++q) {
             level_stencil(X + 6 * (size_t)h->owned[q], L.isplit, h->p.k, h->p.dt, h->p.omega,
@@ -519,6 +527,7 @@ int pamg_set_state(pamg_handle *h, int level, int what, const double *host) {
     HIPCHK(h, hipMemcpyAsync(h->scratch, host, 3 * (size_t)L.N * sizeof(double), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, launch_to_soa(h->stream, h->scratch, dst, L.N, L.pitch));
     if (what == PAMG_TOLD) CHK(refresh_told_halo(h, level));
+    if (what == PAMG_RESIDUAL) h->rhsn_valid = false;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return PAMG_OK;
 }

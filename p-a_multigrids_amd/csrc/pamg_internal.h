@@ -68,6 +68,9 @@ struct Level {
     int64_t pitch = 0;    // plane stride (>= N, multiple of 64)
     // SoA planes [3][pitch]
     double *T = nullptr, *TNN = nullptr, *RHS = nullptr, *RES = nullptr, *TOLD = nullptr;
+    // restrictor(l - 1) of the finer level's current residual, computed where that residual
+    // is produced (fused V-cycle) and consumed as RHS by the next cycle (l >= 2)
+    double *RHSN = nullptr;
     double *stc = nullptr;            // U_local * kStcStride
     int2 *subinfo = nullptr;          // nsub: (irow, ipos) of get_str_info
     int4 *children = nullptr;         // nsub/4 (children of the next coarser level's sub-elements)
@@ -105,6 +108,8 @@ struct pamg_handle {
     // time step (the fused V-cycle then writes only the tnew words); cleared by every
     // operation that writes or changes them otherwise
     bool overlap_static_l1 = false;
+    // RHSN of every level holds the restriction of the finer level's current residual
+    bool rhsn_valid = true;
     bool mesh_ready = false;
     std::string err;
     pamg::Timing timing;
@@ -132,7 +137,7 @@ namespace pamg {
 hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int sweeps, int solver,
                          double rdt, double omega, double *tov, double *tovo);
 hipError_t launch_residual(hipStream_t s, const Level &L, double rdt);
-hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U);
+hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U, double *out = nullptr);
 hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn);
 hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, bool start_of_step);
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);

@@ -552,16 +552,17 @@ hipError_t launch_residual(hipStream_t s, const Level &L, double rdt) {
 // tile of whole un_eles with at least 1024 fine sub-elements; LDS = 3 * TF * 8 B (<= 96 KiB)
 inline int tile_log2_for(int nsub_f) { const int lg = log2i(nsub_f); return lg > 10 ? lg : 10; }
 
-hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U) {
+hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U, double *out) {
+    double *dst = out ? out : coarse.RHS;
     (void)U;
     if (coarse.N == 0) return hipSuccess;
     if (fine.nsub <= 4096) {
         const int tl = tile_log2_for(fine.nsub);
         const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
-        hipLaunchKernelGGL(k_restrict_tile, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.RES, coarse.RHS,
+        hipLaunchKernelGGL(k_restrict_tile, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.RES, dst,
                            fine.children, fine.pitch, coarse.pitch, fine.N, log2i(fine.nsub), tl);
     } else {
-        hipLaunchKernelGGL(k_restrict, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.RES, coarse.RHS,
+        hipLaunchKernelGGL(k_restrict, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.RES, dst,
                            fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub));
     }
     return hipGetLastError();

@@ -45,8 +45,15 @@ using namespace detail;
 constexpr int kMTf = 512;   // threads per workgroup, level-0 kernel (one adjacent pair each)
 constexpr int kMTc = 64;    // threads per workgroup, coarse-level kernel (one wave per tile)
 
+// the planes of a level are one allocation (pamg_api.cpp): tnew, tnew_nonlin, RHS,
+// residual, told, RHSN at plane offsets 0, 3, 6, 9, 12, 15 (one base pointer in SGPRs)
 struct VLevel {
-    double *T, *TNN, *RHS, *RES;
+    double *base;
+    __device__ __forceinline__ double *T() const { return base; }
+    __device__ __forceinline__ double *TNN() const { return base + 3 * pitch; }
+    __device__ __forceinline__ double *RHS() const { return base + 6 * pitch; }
+    __device__ __forceinline__ double *RES() const { return base + 9 * pitch; }
+    __device__ __forceinline__ double *RHSN() const { return base + 15 * pitch; }
     const double *stc;
     const int4 *children;   // children (in-un_ele indices) of this level's sub-elements in the next finer level
     int64_t pitch;
@@ -58,20 +65,23 @@ struct VArgs {
     int64_t U;
     int n_smooth, n_coarse;
     double rdt;
-    int cascade;            // 0: skip the (dead) prolongator cascades (PAMG_DIAG_NOCASCADE diagnostics)
     long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
 };
 
 // phase stamps: 100 MHz wall clock per wave at the phase boundaries, plus the wave's HW_ID
+// (diagnostics build only: make PAMG_STAMPS=1; the pointer costs SGPRs the kernels need)
+#ifndef PAMG_STAMPS
+#define PAMG_STAMPS 0
+#endif
 constexpr int kStampSlots = 10;
 template <int MT>
 __device__ __forceinline__ void stamp(const VArgs &A, int i) {
-    if (A.stamps && (threadIdx.x & 63) == 0)
+    if (PAMG_STAMPS && A.stamps && (threadIdx.x & 63) == 0)
         A.stamps[((int64_t)blockIdx.x * (MT / 64) + (threadIdx.x >> 6)) * kStampSlots + i] = wall_clock64();
 }
 template <int MT>
 __device__ __forceinline__ void stamp_hwid(const VArgs &A) {
-    if (A.stamps && (threadIdx.x & 63) == 0) {
+    if (PAMG_STAMPS && A.stamps && (threadIdx.x & 63) == 0) {
         unsigned hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         A.stamps[((int64_t)blockIdx.x * (MT / 64) + (threadIdx.x >> 6)) * kStampSlots + 9] = hw;
@@ -137,14 +147,6 @@ __device__ __forceinline__ void stencil(bool uni, const double *__restrict__ stc
     load_stc(stc + u * (uint32_t)kStcStride, S);
 }
 
-// n sweeps from x: x -> last iterate, p -> iterate before the last sweep (n >= 1)
-__device__ __forceinline__ void sweeps(const Stc &S, double rdt, int n, const double b[3], double x[3],
-                                       double p[3]) {
-    for (int it = 0; it < n; ++it) {
-        copy3(p, x);
-        sweep(S, rdt, b, x);
-    }
-}
 // two sub-elements of one un_ele, interleaved
 __device__ __forceinline__ void sweeps2(const Stc &S, double rdt, int n, const double b0[3], const double b1[3],
                                         double x0[3], double x1[3], double p0[3], double p1[3]) {
@@ -220,237 +222,197 @@ __device__ __forceinline__ void prolong_cascade(double *F, int n, const int fi[4
 // ===================================================================== coarse levels
 // One wave per tile. Level l >= 1 of a tile has nt(l) sub-elements; lane t owns the
 // sub-elements t + 64 k, k < K(l) = max(1, nt(l) / 64), that are < nt(l): four of
-// level 1, one of level 2, one on the first nt(l) lanes below. The coarsest level's
-// 1 + n_coarse smoother calls are a chain of dependent sweeps, issue-bound on the
-// wave that runs it; with one wave per tile no wave waits on it, and the many tiles
-// resident per CU overlap their memory phases with the chains of the others.
-// LDS per level l: B_l = RHS (3 x nt(l)), W_l = tnew: the restriction-leg iterate
-// (l < C) or, on the coarsest level, its tnew, and Y_l (2 <= l < C) the final tnew of
-// a middle level (input of the prolongator cascade into level l - 1).
+// level 1, one of level 2, one on the first nt(l) lanes below. The lane's share of
+// every coarse level -- a "chunk" per (level, k) -- lives in registers for the whole
+// cycle, and the levels are smoothed in lockstep: the data dependences of the cycle
+//  tie a level's smoother calls to its own earlier ones and to the
+// prologue only (the restrictor reads the PREVIOUS cycle's residual), so
+//   phase A: the restriction-leg smoother call of every level, interleaved, then
+//            get_residual of every level;
+//   phase B: the 1 + n_coarse smoother calls of the coarsest level, with the
+//            prolongation-leg call of every other level interleaved into its first
+//            n_smooth sweeps.
+// A sweep is a chain of 8 dependent fp64 operations; interleaving the chunks keeps
+// the wave issuing instead of waiting on that latency.
 template <int S, int L>
 struct CGeo {
     using G = Geo<S, L>;
     static constexpr int C = G::C;
     static constexpr int K(int l) { return G::nt(l) >= 64 ? G::nt(l) / 64 : 1; }
-    // every lane of a chunk inside one un_ele (operator records through the scalar cache)
+    // the lanes of a chunk inside one un_ele (operator record through the scalar cache)
     static constexpr bool uni(int l) { return (G::nt(l) < 64 ? G::nt(l) : 64) <= (1 << G::lg(l)); }
-    // every chunk of the level inside one un_ele: the chunks are smoothed together (ILP)
+    // the whole level of the tile inside one un_ele: one operator record for all its chunks
     static constexpr bool one(int l) { return G::nt(l) <= (1 << G::lg(l)); }
-    static constexpr int sz(int l) { return 3 * G::nt(l); }
-    static constexpr int B(int l) {
-        int o = 0;
-        for (int i = 1; i < l; ++i) o += 2 * sz(i);
-        return o;
-    }
-    static constexpr int W(int l) { return B(l) + sz(l); }
-    static constexpr int Y(int l) {   // 2 <= l < C
-        int o = B(C + 1);
-        for (int i = 2; i < l; ++i) o += sz(i);
-        return o;
-    }
-    static constexpr int dump = Y(C);            // 3 slots per lane for the stores of idle lanes
-    static constexpr int total = dump + 3 * 64;
-    // restrictor chunks: (level l + 1, chunk k) for l = 0..C-1
-    static constexpr int nrc() {
-        int n = 0;
-        for (int l = 1; l <= C; ++l) n += K(l);
-        return n;
-    }
+    static constexpr int NCH = [] { int n = 0; for (int l = 1; l <= C; ++l) n += K(l); return n; }();
+    static constexpr int lev(int j) { int l = 1; while (j >= K(l)) { j -= K(l); ++l; } return l; }
+    static constexpr int kk(int j) { int l = 1; while (j >= K(l)) { j -= K(l); ++l; } return j; }
+    // LDS images for the (dead) prolongator cascades: F_l (restriction-leg tnew, 1 <= l < C)
+    // and Y_l (final tnew, 2 <= l <= C)
+    static constexpr int F(int l) { int o = 0; for (int i = 1; i < l; ++i) o += 3 * G::nt(i); return o; }
+    static constexpr int Y(int l) { int o = F(C); for (int i = 2; i < l; ++i) o += 3 * G::nt(i); return o; }
+    // M_l (1 <= l < C): mean of the three new residual components of each sub-element,
+    // the restrictor's input (splitting.F90:146-151)
+    static constexpr int M(int l) { int o = Y(C + 1); for (int i = 1; i < l; ++i) o += G::nt(i); return o; }
+    static constexpr int total = M(C) > 0 ? M(C) : 1;
 };
 
 template <int S, int L>
-__global__ __launch_bounds__(kMTc) void k_vc_coarse(VArgs A, const double *__restrict__ sp1,
-                                                    const double *__restrict__ sp2, const double *__restrict__ sp3,
-                                                    const double *__restrict__ sp4) {
+__global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__restrict__ sp1,
+                                                       const double *__restrict__ sp2, const double *__restrict__ sp3,
+                                                       const double *__restrict__ sp4) {
     // operator records as restrict kernel arguments: never written here, so wave-uniform
     // records are fetched with scalar loads
     const double *__restrict__ SP[kMaxFusedLevels] = {nullptr, sp1, sp2, sp3, sp4};
     using G = Geo<S, L>;
     using Q = CGeo<S, L>;
     constexpr int C = G::C;
+    constexpr int N = Q::NCH;
     static_assert(C >= 1, "coarse kernel needs two levels");
     __shared__ __attribute__((aligned(16))) double lds[Q::total];
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
     const int64_t u0 = (int64_t)blockIdx.x << G::GL;
-    const int nue = (int)min((int64_t)1 << G::GL, A.U - u0);
+    const int nue = G::GL == 0 ? 1 : (int)min((int64_t)1 << G::GL, A.U - u0);   // un_eles in this tile
     stamp<kMTc>(A, 0);
     stamp_hwid<kMTc>(A);
-    // chunk k of level l: tile index t + 64 k, valid if inside the tile's un_eles; idle
-    // lanes load index 0 (in bounds) and store to the dump slots (no branches, so the
-    // loads of a phase are all in flight together)
-    auto ok = [&](int l, int k) -> bool { return t + 64 * k < G::nt(l) && t + 64 * k < (nue << G::lg(l)); };
-    auto gix = [&](int l, int k) -> uint32_t {
-        return ((uint32_t)u0 << G::lg(l)) + (uint32_t)(ok(l, k) ? t + 64 * k : 0);
-    };
-    auto lix = [&](int base, int l, int k, int c) -> int {   // LDS slot of component c
-        return ok(l, k) ? base + c * G::nt(l) + t + 64 * k : Q::dump + 3 * t + c;
-    };
-    // ---- prologue, batch 1: tnew of every level (tnew_nonlin := tnew, :327 / :348), halo
-    //      positions, children of the restrictor chunks
-    int hl[L][4];
-    double xi[L][4][3];
-    int4 ch[L][4];
+    // chunk j = (level l, k): tile index t + 64 k; idle lanes (beyond the level or the
+    // tile's un_eles) compute on index 0 and store nothing
+    bool ok[N];
+    uint32_t gx[N];
 #pragma unroll
-    for (int l = 1; l < L; ++l)
-#pragma unroll
-        for (int k = 0; k < Q::K(l); ++k) {
-            const uint32_t g = gix(l, k);
-            load3(A.lv[l].T, A.lv[l].pitch, g, xi[l][k]);
-            const int4 hs = A.lv[l].H.hsub[g & ((1 << G::lg(l)) - 1)];
-            hl[l][k] = ok(l, k) ? hs_pack(hs) : 0;
-            ch[l][k] = A.lv[l].children[g & ((1 << G::lg(l)) - 1)];
-        }
-#pragma unroll
-    for (int l = 1; l < L; ++l)
-#pragma unroll
-        for (int k = 0; k < Q::K(l); ++k)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) lds[lix(Q::W(l), l, k, c)] = xi[l][k][c];
-    // ---- batch 2: restrictor (:336) of every level from the residual of the PREVIOUS cycle,
-    //      RHS_{l+1}(1, c) = mean(res_l(:, f3)), (2, c) = mean(res_l(:, f4)), (3, c) = mean(res_l(:, f1))
-    //      (splitting.F90:10-32, 146-151); all read before any residual is rewritten
-    double rr[L][4][3][3];
-#pragma unroll
-    for (int l = 0; l < C; ++l)
-#pragma unroll
-        for (int k = 0; k < Q::K(l + 1); ++k) {
-            const uint32_t g = gix(l + 1, k);
-            const int4 c4 = ch[l + 1][k];
-            const uint32_t base = (g >> G::lg(l + 1)) << G::lg(l);
-            const uint32_t pick[3] = {base + c4.z, base + c4.w, base + c4.x};
-#pragma unroll
-            for (int q = 0; q < 3; ++q) load3(A.lv[l].RES, A.lv[l].pitch, pick[q], rr[l + 1][k][q]);
-        }
+    for (int j = 0; j < N; ++j) {
+        const int l = Q::lev(j), i = t + 64 * Q::kk(j);
+        ok[j] = i < G::nt(l) && i < (nue << G::lg(l));
+        gx[j] = ((uint32_t)u0 << G::lg(l)) + (uint32_t)(ok[j] ? i : 0);
+    }
+    // operator records: one per level when the tile's level lies in one un_ele (n_split = 5),
+    // else one per chunk, fetched where used
+    Stc SL[C + 1];
 #pragma unroll
     for (int l = 1; l <= C; ++l)
+        if (Q::one(l)) stencil(Q::uni(l), SP[l], ((uint32_t)u0 << G::lg(l)) >> G::lg(l), SL[l]);
+    auto stc_of = [&](int j, Stc &St) {
+        const int l = Q::lev(j);
+        if (Q::one(l)) St = SL[l];
+        else stencil(Q::uni(l), SP[l], gx[j] >> G::lg(l), St);
+    };
+    // ---- prologue: tnew of every level (tnew_nonlin := tnew, :327 / :348), halo positions,
+    //      and the restrictor (:336) of every level: RHS_l := RHSN_l, the restriction of the
+    //      PREVIOUS cycle's residual, computed when that residual was (below, and in the
+    //      level-1 launch for level 1)
+    double x[N][3], b[N][3], p[N][3];
+    int hl[N];
 #pragma unroll
-        for (int k = 0; k < Q::K(l); ++k) {
-            double b[3];
+    for (int j = 0; j < N; ++j) {
+        const int l = Q::lev(j);
+        load3(A.lv[l].T(), A.lv[l].pitch, gx[j], x[j]);
+        const int4 hs = A.lv[l].H.hsub[gx[j] & ((1 << G::lg(l)) - 1)];
+        hl[j] = ok[j] ? hs_pack(hs) : 0;
+    }
 #pragma unroll
-            for (int q = 0; q < 3; ++q) b[q] = (rr[l][k][q][0] + rr[l][k][q][1] + rr[l][k][q][2]) / 3.;
-            if (ok(l, k)) store3(A.lv[l].RHS, A.lv[l].pitch, gix(l, k), b);
+    for (int j = 0; j < N; ++j) load3(A.lv[Q::lev(j)].RHSN(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) lds[lix(Q::B(l), l, k, c)] = b[c];
-        }
+    for (int j = 0; j < N; ++j)
+        if (ok[j]) store3(A.lv[Q::lev(j)].RHS(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
     stamp<kMTc>(A, 1);
-    // smoother calls on the chunks of level l (x from W, b from B); the chunks of one un_ele
-    // are interleaved (ILP), otherwise each reads its own operator record
-    auto smooth_chunks = [&](auto LC, int nsw, double (&x)[4][3], const double (&b)[4][3], double (&p)[4][3]) {
-        constexpr int l = decltype(LC)::value;
-        constexpr int K = Q::K(l);
-        if constexpr (Q::one(l)) {
+    // ---- phase A: restriction-leg smoother call of every level (:331), then get_residual (:338)
+    for (int it = 0; it < ns; ++it) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
             Stc St;
-            stencil(Q::uni(l), SP[l], gix(l, 0) >> G::lg(l), St);
-            sweepsN<K>(St, rdt, nsw, reinterpret_cast<const double(&)[K][3]>(b),
-                       reinterpret_cast<double(&)[K][3]>(x), reinterpret_cast<double(&)[K][3]>(p));
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                Stc St;
-                stencil(Q::uni(l), SP[l], gix(l, k) >> G::lg(l), St);
-                sweeps(St, rdt, nsw, b[k], x[k], p[k]);
-            }
+            stc_of(j, St);
+            copy3(p[j], x[j]);
+            sweep(St, rdt, b[j], x[j]);
         }
-    };
-    auto residual_chunks = [&](auto LC, const double (&b)[4][3], const double (&p)[4][3]) {
-        constexpr int l = decltype(LC)::value;
-        const VLevel &V = A.lv[l];
-#pragma unroll
-        for (int k = 0; k < Q::K(l); ++k) {
-            Stc St;
-            stencil(Q::uni(l), SP[l], gix(l, k) >> G::lg(l), St);
-            double r[3];
-            residual(St, rdt, p[k], b[k], r);
-            if (ok(l, k)) store3(V.RES, V.pitch, gix(l, k), r);
-        }
-    };
-    auto load_wb = [&](auto LC, double (&x)[4][3], double (&b)[4][3]) {
-        constexpr int l = decltype(LC)::value;
-#pragma unroll
-        for (int k = 0; k < Q::K(l); ++k)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                x[k][c] = lds[lix(Q::W(l), l, k, c)];
-                b[k][c] = lds[lix(Q::B(l), l, k, c)];
-            }
-    };
-    auto halo_chunks = [&](auto LC, const double (&p)[4][3]) {
-        constexpr int l = decltype(LC)::value;
-#pragma unroll
-        for (int k = 0; k < Q::K(l); ++k) hs_write(Q::uni(l), A.lv[l].H, gix(l, k) >> G::lg(l), hl[l][k], p[k]);
-    };
-    // ---- levels 1..C-1, restriction leg: smoother (:331), get_residual (:338)
-    static_for<1, C>([&](auto LC) {
-        constexpr int l = decltype(LC)::value;
-        double x[4][3], b[4][3], p[4][3];
-        load_wb(LC, x, b);
-        smooth_chunks(LC, ns, x, b, p);
-#pragma unroll
-        for (int k = 0; k < Q::K(l); ++k)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) lds[lix(Q::W(l), l, k, c)] = p[k][c];
-        halo_chunks(LC, p);
-        residual_chunks(LC, b, p);
-    });
+    }
     stamp<kMTc>(A, 2);
-    // ---- coarsest level: smoother + get_residual of the restriction leg, then the
-    //      n_coarse smoother calls from tnew_nonlin := tnew (:344-359)
-    {
-        using LC = std::integral_constant<int, C>;
-        double x[4][3], b[4][3], p[4][3];
-        load_wb(LC{}, x, b);
-        smooth_chunks(LC{}, ns, x, b, p);
-        halo_chunks(LC{}, p);
-        residual_chunks(LC{}, b, p);
 #pragma unroll
-        for (int k = 0; k < Q::K(C); ++k) copy3(x[k], p[k]);
-        smooth_chunks(LC{}, ns * A.n_coarse, x, b, p);
-        halo_chunks(LC{}, p);
+    for (int j = 0; j < N; ++j) {
+        const int l = Q::lev(j);
+        const VLevel &V = A.lv[l];
+        Stc St;
+        stc_of(j, St);
+        hs_write(Q::uni(l), V.H, gx[j] >> G::lg(l), hl[j], p[j]);
+        double r[3];
+        residual(St, rdt, p[j], b[j], r);
+        if (ok[j]) store3(V.RES(), V.pitch, gx[j], r);
+        if (l < C) {   // restriction-leg tnew: start of the prolongation leg and cascade target
+            if (ok[j]) {
+                const int i = t + 64 * Q::kk(j);
 #pragma unroll
-        for (int k = 0; k < Q::K(C); ++k) {
-            if (ok(C, k)) store3(A.lv[C].T, A.lv[C].pitch, gix(C, k), p[k]);
+                for (int c = 0; c < 3; ++c) lds[Q::F(l) + c * G::nt(l) + i] = p[j][c];
+                lds[Q::M(l) + i] = (r[0] + r[1] + r[2]) / 3.;
+            }
+        }
+        copy3(x[j], p[j]);   // tnew_nonlin := tnew (:348 coarsest, :367 the others)
+    }
+    // restrictor of the next cycle (:336): RHSN_l(1, c) = mean(res(:, f3)),
+    // (2, c) = mean(res(:, f4)), (3, c) = mean(res(:, f1)) (splitting.F90:10-32, 146-151)
+    if constexpr (C >= 2) {
+        __syncthreads();
 #pragma unroll
-            for (int c = 0; c < 3; ++c) lds[lix(Q::W(C), C, k, c)] = p[k][c];
+        for (int j = 0; j < N; ++j) {
+            const int l = Q::lev(j);
+            if (l < 2 || !ok[j]) continue;
+            const int i = t + 64 * Q::kk(j);
+            const int4 c4 = A.lv[l].children[gx[j] & ((1 << G::lg(l)) - 1)];
+            const int base = (i >> G::lg(l)) << G::lg(l - 1);
+            const double rn[3] = {lds[Q::M(l - 1) + base + c4.z], lds[Q::M(l - 1) + base + c4.w],
+                                  lds[Q::M(l - 1) + base + c4.x]};
+            store3(A.lv[l].RHSN(), A.lv[l].pitch, gx[j], rn);
         }
     }
     stamp<kMTc>(A, 3);
-    // ---- prolongation leg, levels C-1..1: smoother from tnew_nonlin = restriction-leg tnew (:367, :376)
-    static_for<1, C>([&](auto LR) {
-        constexpr int l = C - decltype(LR)::value;
-        using LC = std::integral_constant<int, l>;
-        double x[4][3], b[4][3], p[4][3];
-        load_wb(LC{}, x, b);
-        smooth_chunks(LC{}, ns, x, b, p);
-        halo_chunks(LC{}, p);
+    // ---- phase B: the n_coarse smoother calls of the coarsest level (:351-353) with the
+    //      prolongation-leg call (:376) of every other level in its first n_smooth sweeps
+    const int nB = ns * A.n_coarse;
+    for (int it = 0; it < min(ns, nB); ++it) {
 #pragma unroll
-        for (int k = 0; k < Q::K(l); ++k) {
-            if (ok(l, k)) store3(A.lv[l].T, A.lv[l].pitch, gix(l, k), p[k]);
-            if constexpr (l >= 2)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) lds[lix(Q::Y(l), l, k, c)] = p[k][c];
+        for (int j = 0; j < N; ++j) {
+            Stc St;
+            stc_of(j, St);
+            copy3(p[j], x[j]);
+            sweep(St, rdt, b[j], x[j]);
         }
-    });
+    }
+    for (int it = ns; it < nB; ++it) {   // the coarsest level alone
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            if (Q::lev(j) < C) continue;
+            Stc St;
+            stc_of(j, St);
+            copy3(p[j], x[j]);
+            sweep(St, rdt, b[j], x[j]);
+        }
+    }
     stamp<kMTc>(A, 4);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const int l = Q::lev(j);
+        const VLevel &V = A.lv[l];
+        hs_write(Q::uni(l), V.H, gx[j] >> G::lg(l), hl[j], p[j]);
+        if (ok[j]) {
+            store3(V.T(), V.pitch, gx[j], p[j]);
+            if (l >= 2)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) lds[Q::Y(l) + c * G::nt(l) + t + 64 * Q::kk(j)] = p[j][c];
+        }
+    }
     // ---- prolongator (:370) among the coarse levels, on the LDS images of the
     //      restriction-leg tnew (its result is dead, :550)
     if constexpr (C >= 2) {
         __syncthreads();
 #pragma unroll
-        for (int l = 1; l < C; ++l) {
-            const int ysrc = (l + 1 == C) ? Q::W(C) : Q::Y(l + 1);
-#pragma unroll
-            for (int k = 0; k < Q::K(l + 1); ++k) {
-                if (!ok(l + 1, k)) continue;
-                const int j = t + 64 * k;
-                const int4 c4 = ch[l + 1][k];
-                const int base = (j >> G::lg(l + 1)) << G::lg(l);
-                const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
-                const double y[3] = {lds[ysrc + j], lds[ysrc + G::nt(l + 1) + j], lds[ysrc + 2 * G::nt(l + 1) + j]};
-                prolong_cascade(lds + Q::W(l), G::nt(l), fi, y);
-            }
-            __syncthreads();
+        for (int j = 0; j < N; ++j) {
+            const int l = Q::lev(j);   // coarse side l, fine side l - 1 >= 1
+            if (l < 2 || !ok[j]) continue;
+            const int i = t + 64 * Q::kk(j);
+            const int4 c4 = A.lv[l].children[gx[j] & ((1 << G::lg(l)) - 1)];
+            const int base = (i >> G::lg(l)) << G::lg(l - 1);
+            const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+            const double y[3] = {lds[Q::Y(l) + i], lds[Q::Y(l) + G::nt(l) + i], lds[Q::Y(l) + 2 * G::nt(l) + i]};
+            prolong_cascade(lds + Q::F(l - 1), G::nt(l - 1), fi, y);
         }
     }
     stamp<kMTc>(A, 7);
@@ -464,11 +426,12 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     using G = Geo<S, L>;
     constexpr int C = G::C;
     __shared__ __attribute__((aligned(16))) double F0[C > 0 ? 3 * 1024 : 1];   // restriction-leg tnew image
+    __shared__ __attribute__((aligned(16))) double M0[C > 0 ? 1024 : 1];       // residual means (restrictor input)
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
     const int64_t u0 = (int64_t)blockIdx.x << G::GL;
-    const int nue = (int)min((int64_t)1 << G::GL, A.U - u0);
+    const int nue = G::GL == 0 ? 1 : (int)min((int64_t)1 << G::GL, A.U - u0);   // un_eles in this tile
     stamp<kMTf>(A, 0);
     stamp_hwid<kMTf>(A);
     const VLevel &V0 = A.lv[0];
@@ -480,19 +443,8 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
 #pragma unroll
     for (int k = 0; k < 2; ++k) h0[k] = v0 ? hs_pack(V0.H.hsub[(s0 + k) & ((1 << G::lg(0)) - 1)]) : 0;
     double x0[2][3], b0[2][3], p0[2][3];
-    load3p(V0.T, V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
-    load3p(V0.RHS, V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
-    // final level-1 tnew (coarse launch) for the prolongator
-    bool v1 = false;
-    uint32_t s1 = 0;
-    double y1[3];
-    int4 c4 = make_int4(0, 0, 0, 0);
-    if constexpr (C > 0) {
-        v1 = t < (nue << G::lg(1));
-        s1 = ((uint32_t)u0 << G::lg(1)) + (v1 ? t : 0);
-        load3(A.lv[1].T, A.lv[1].pitch, s1, y1);
-        c4 = A.lv[1].children[s1 & ((1 << G::lg(1)) - 1)];
-    }
+    load3p(V0.T(), V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
+    load3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
     Stc St;
     stencil(G::uni(0), sp0, w0, St);
     // ---- restriction leg: smoother (:331), get_residual (:338)
@@ -502,14 +454,33 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
         if constexpr (C > 0)
 #pragma unroll
             for (int c = 0; c < 3; ++c) st2(F0 + c * 1024 + 2 * t, make_double2(p0[0][c], p0[1][c]));
+        // halo records by vector loads: the boundary lanes are few, and scalar copies of the
+        // records would push the kernel past 80 SGPRs (7 instead of 8 waves per SIMD)
 #pragma unroll
-        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, h0[k], p0[k]);
+        for (int k = 0; k < 2; ++k) hs_write(false, V0.H, w0, h0[k], p0[k]);
         double r[2][3];
 #pragma unroll
         for (int k = 0; k < 2; ++k) residual(St, rdt, p0[k], b0[k], r[k]);
-        store3p(V0.RES, V0.pitch, s0, r[0], r[1]);
+        store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
+        if constexpr (C > 0)   // restrictor input: mean of the residual components (splitting.F90:146-151)
+            st2(M0 + 2 * t, make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.));
     }
     stamp<kMTf>(A, 2);
+    // level-1 sub-element t: its final tnew (coarse launch) for the prolongator, its children
+    // for the prolongator and the restrictor, fetched behind the prolongation-leg sweeps
+    // (threads 0..255: prolongator of sub-element t; threads 256..511: restrictor of t - 256)
+    const int j1 = t & (G::nt(1) - 1);
+    const bool casc = t < G::nt(1);
+    bool v1 = false;
+    uint32_t s1 = 0;
+    double y1[3] = {0.0, 0.0, 0.0};
+    int4 c4 = make_int4(0, 0, 0, 0);
+    if constexpr (C > 0) {
+        v1 = j1 < (nue << G::lg(1));
+        s1 = ((uint32_t)u0 << G::lg(1)) + (v1 ? j1 : 0);
+        if (casc) load3(A.lv[1].T(), A.lv[1].pitch, s1, y1);
+        c4 = A.lv[1].children[s1 & ((1 << G::lg(1)) - 1)];
+    }
     // ---- prolongation leg (:367-376) from the restriction-leg tnew; with one level,
     //      the 15 coarse smoother calls (:344-359)
     copy3(x0[0], p0[0]);
@@ -518,19 +489,24 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     stamp<kMTf>(A, 3);
     if (v0) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, h0[k], p0[k]);
-        store3p(V0.T, V0.pitch, s0, p0[0], p0[1]);
-        store3p(V0.TNN, V0.pitch, s0, x0[0], x0[1]);
+        for (int k = 0; k < 2; ++k) hs_write(false, V0.H, w0, h0[k], p0[k]);
+        store3p(V0.T(), V0.pitch, s0, p0[0], p0[1]);
+        store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
     }
     stamp<kMTf>(A, 4);
-    // ---- prolongator (:370) on the LDS image (its result is dead, :550)
+    // ---- prolongator (:370) on the LDS image (its result is dead, :550), and the restrictor
+    //      of the next cycle (:336) from this cycle's residual (splitting.F90:10-32)
     if constexpr (C > 0) {
-        if (!A.cascade) return;
         __syncthreads();
         if (v1) {
-            const int base = (t >> G::lg(1)) << G::lg(0);
-            const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
-            prolong_cascade(F0, 1024, fi, y1);
+            const int base = (j1 >> G::lg(1)) << G::lg(0);
+            if (casc) {
+                const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+                prolong_cascade(F0, 1024, fi, y1);
+            } else {
+                const double rn[3] = {M0[base + c4.z], M0[base + c4.w], M0[base + c4.x]};
+                store3(A.lv[1].RHSN(), A.lv[1].pitch, s1, rn);
+            }
         }
     }
     stamp<kMTf>(A, 7);
@@ -571,7 +547,10 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
         if (V.nsub != (1 << (2 * (n_split - l)))) return hipErrorInvalidValue;
         if ((uint64_t)V.pitch * 3 >= (1ull << 29)) return hipErrorInvalidValue;   // 32-bit byte offsets
         VLevel &o = A.lv[l];
-        o.T = V.T; o.TNN = V.TNN; o.RHS = V.RHS; o.RES = V.RES; o.stc = V.stc;
+        if (V.TNN != V.T + 3 * V.pitch || V.RHS != V.T + 6 * V.pitch || V.RES != V.T + 9 * V.pitch ||
+            V.RHSN != V.T + 15 * V.pitch)
+            return hipErrorInvalidValue;
+        o.base = V.T; o.stc = V.stc;
         o.children = (l > 0) ? lv[l].children : nullptr;   // children of level l+1 in level l
         o.pitch = V.pitch;
         const HaloPlan &P = V.halo;
@@ -581,13 +560,11 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.n_smooth = n_smooth;
     A.n_coarse = n_coarse;
     A.rdt = rdt;
-    static const bool diag_nocascade = getenv("PAMG_DIAG_NOCASCADE") != nullptr;
-    A.cascade = diag_nocascade ? 0 : 1;
     const int GL = 10 - 2 * n_split;   // 1024 / 4**n_split un_eles per tile
     const unsigned grid = (unsigned)(((int64_t)U + (1 << GL) - 1) >> GL);
     if (grid == 0) return hipSuccess;
     // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
-    static const char *stamp_path = getenv("PAMG_VCYCLE_STAMPS");
+    static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_VCYCLE_STAMPS") : nullptr;
     const int waves = (coarse ? kMTc : kMTf) / 64;
     const size_t nst = (size_t)grid * waves * kStampSlots;
     if (stamp_path) {

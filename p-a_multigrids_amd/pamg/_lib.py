@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libpamg.so")
+# PAMG_LIB: an alternative in-tree build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("PAMG_LIB") or os.path.join(PKG_DIR, "libpamg.so")
 
 PAMG_OK = 0
 ERRORS = {-1: "PAMG_ERR_ARG", -2: "PAMG_ERR_HIP", -3: "PAMG_ERR_IO", -4: "PAMG_ERR_STATE",
