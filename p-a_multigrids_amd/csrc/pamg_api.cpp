@@ -248,17 +248,22 @@ int prolong(pamg_handle *h, int l, bool fused_copy) {
     return PAMG_OK;
 }
 
-// algorithmic HBM bytes of the two fused V-cycle launches: state traffic
-// of every level plus one operator record per un_ele and level
+// algorithmic HBM bytes of the two fused V-cycle launches: the state each
+// launch must read and write once, plus the operator words it reads (c, Kd, omega/D: 104 B
+// per un_ele and level)
+//   level-1 launch: level 1 reads tnew, RHS and writes residual, tnew, tnew_nonlin (120 B);
+//                   level 2 reads the final tnew (prolongator) and writes RHSN (48 B)
+//   coarse launch:  level l >= 2 reads tnew, RHSN and writes RHS, residual, tnew (120 B);
+//                   RHSN of the levels l >= 3 is written here too (24 B)
 double vcycle_fine_bytes(pamg_handle *h) {
     const int L = h->p.multi_levels;
-    return 120.0 * h->lv[1].N + (L > 1 ? 24.0 * h->lv[2].N : 0.0) + 168.0 * h->U;
+    return 120.0 * h->lv[1].N + (L > 1 ? 48.0 * h->lv[2].N : 0.0) + 104.0 * h->U;
 }
 double vcycle_coarse_bytes(pamg_handle *h) {
     const int L = h->p.multi_levels;
-    double b = 24.0 * h->lv[1].N;   // level-1 residual of the previous cycle (restrictor input)
-    for (int l = 2; l <= L; ++l) b += (96.0 + (l < L ? 24.0 : 0.0)) * h->lv[l].N;
-    return b + 168.0 * h->U * (L - 1);
+    double b = 0.0;
+    for (int l = 2; l <= L; ++l) b += (120.0 + (l >= 3 ? 24.0 : 0.0)) * h->lv[l].N;
+    return b + 104.0 * h->U * (L - 1);
 }
 
 int vcycle_once(pamg_handle *h) {

@@ -7,25 +7,29 @@
 // workgroup carries a tile of whole un_eles through its part of the cycle
 // without exchanging data with other workgroups. The computation is the
 // reference's, step for step and in its operation order (same device helpers
-// as the per-step kernels; results are bitwise equal to pamg_vcycle's
-// multi-kernel form, tests/test_gpu_parity.py). The schedule follows the data
-// dependences, which the block-diagonal operator leaves loose:
-//   * the restrictor (:336) reads the residual of the PREVIOUS cycle;
+// as the per-step kernels; the state after every cycle is bitwise equal to
+// pamg_vcycle's multi-kernel form, tests/test_gpu_parity.py). The schedule
+// follows the data dependences, which the block-diagonal operator leaves loose:
+//   * the restrictor (:336) reads the residual of the PREVIOUS cycle, so it is
+//     evaluated where that residual is produced and kept as RHSN (the next
+//     cycle's RHS) -- no launch re-reads a residual;
 //   * the prolongation-leg smoother of level l (:376) starts from
 //     tnew_nonlin = the restriction-leg tnew of level l (:367); the prolonged
-//     values are overwritten at its first sweep (:550);
-//   * so level 1 (the reference's finest level) depends on the coarser levels
-//     only through the prolongator's (dead) result and the halo words, whose
-//     final state is what level 1's last smoother call writes.
-// Launch 1, k_vc_coarse: levels 2..L of the cycle -- all restrictions (level
-//   1's from the old residual), both legs of every coarser level, the 15
-//   coarse smoother calls, the prolongator cascades among them. Small
-//   workgroups (256 level-2 sub-elements per tile): the 15 n_smooth dependent
-//   sweeps of the coarsest level are a latency chain, hidden by occupancy.
-// Launch 2, k_vc_fine: level 1 -- both smoother calls, get_residual, and the
-//   prolongator cascade from the final level-2 tnew; a streaming kernel
-//   (tnew, RHS in; residual, tnew, tnew_nonlin out) whose halo words are the
-//   cycle's last, as in the reference.
+//     values are overwritten at its first sweep (:550), so every level's two
+//     smoother calls depend on its own state only;
+//   * the halo words (update_overlaps, :555) have no reader in the cycle; the
+//     last writer of every word is level 1's prolongation-leg smoother call
+//     (the coarser levels write subsets of its slots), so the cycle writes each
+//     word once, with that value (t_overlap_old and the boundary words, which
+//     do not change within a time step: k_overlap_static, once per step).
+// Launch 1, k_vc_coarse: levels 2..L -- one wave per tile, the lane's share of
+//   every level in registers, the levels smoothed in lockstep (the coarsest
+//   level's 1 + 15 smoother calls are a chain of dependent sweeps; the other
+//   levels' calls are interleaved into it), the prolongator cascades among them.
+// Launch 2, k_vc_fine: level 1 -- both smoother calls, get_residual, the
+//   restrictor of its residual into level 2's RHSN, and the prolongator cascade
+//   from the final level-2 tnew; a streaming kernel (tnew, RHS in; residual,
+//   tnew, tnew_nonlin out).
 // Levels are 0-based inside this file: level 0 = the reference's level 1.
 #include <hip/hip_runtime.h>
 
@@ -302,13 +306,10 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     //      PREVIOUS cycle's residual, computed when that residual was (below, and in the
     //      level-1 launch for level 1)
     double x[N][3], b[N][3], p[N][3];
-    int hl[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         const int l = Q::lev(j);
         load3(A.lv[l].T(), A.lv[l].pitch, gx[j], x[j]);
-        const int4 hs = A.lv[l].H.hsub[gx[j] & ((1 << G::lg(l)) - 1)];
-        hl[j] = ok[j] ? hs_pack(hs) : 0;
     }
 #pragma unroll
     for (int j = 0; j < N; ++j) load3(A.lv[Q::lev(j)].RHSN(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
@@ -333,7 +334,6 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
         const VLevel &V = A.lv[l];
         Stc St;
         stc_of(j, St);
-        hs_write(Q::uni(l), V.H, gx[j] >> G::lg(l), hl[j], p[j]);
         double r[3];
         residual(St, rdt, p[j], b[j], r);
         if (ok[j]) store3(V.RES(), V.pitch, gx[j], r);
@@ -391,7 +391,6 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     for (int j = 0; j < N; ++j) {
         const int l = Q::lev(j);
         const VLevel &V = A.lv[l];
-        hs_write(Q::uni(l), V.H, gx[j] >> G::lg(l), hl[j], p[j]);
         if (ok[j]) {
             store3(V.T(), V.pitch, gx[j], p[j]);
             if (l >= 2)
@@ -454,10 +453,6 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
         if constexpr (C > 0)
 #pragma unroll
             for (int c = 0; c < 3; ++c) st2(F0 + c * 1024 + 2 * t, make_double2(p0[0][c], p0[1][c]));
-        // halo records by vector loads: the boundary lanes are few, and scalar copies of the
-        // records would push the kernel past 80 SGPRs (7 instead of 8 waves per SIMD)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) hs_write(false, V0.H, w0, h0[k], p0[k]);
         double r[2][3];
 #pragma unroll
         for (int k = 0; k < 2; ++k) residual(St, rdt, p0[k], b0[k], r[k]);
@@ -488,6 +483,9 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     sweeps2(St, rdt, C > 0 ? ns : ns * A.n_coarse, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
     stamp<kMTf>(A, 3);
     if (v0) {
+        // the cycle's halo words (update_overlaps, :555), all written here (see the header);
+        // halo records by vector loads: the boundary lanes are few, and scalar copies of the
+        // records would push the kernel past 80 SGPRs (7 instead of 8 waves per SIMD)
 #pragma unroll
         for (int k = 0; k < 2; ++k) hs_write(false, V0.H, w0, h0[k], p0[k]);
         store3p(V0.T(), V0.pitch, s0, p0[0], p0[1]);
