@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include <vector>
@@ -242,21 +243,27 @@ template <int S, int L>
 struct CGeo {
     using G = Geo<S, L>;
     static constexpr int C = G::C;
-    static constexpr int K(int l) { return G::nt(l) >= 64 ? G::nt(l) / 64 : 1; }
+    // tile: 2**TL level-1 sub-elements (the reference's finest level) = 2**GL un_eles; one
+    // un_ele at n_split = 5, at least 256 level-1 sub-elements below (enough waves for the
+    // small meshes, whose un_eles then share a wave)
+    static constexpr int TL = 2 * S > 8 ? 2 * S : 8;
+    static constexpr int GL = TL - 2 * S;
+    static constexpr int nt(int l) { return (1 << TL) >> (2 * l); }
+    static constexpr int K(int l) { return nt(l) >= 64 ? nt(l) / 64 : 1; }
     // the lanes of a chunk inside one un_ele (operator record through the scalar cache)
-    static constexpr bool uni(int l) { return (G::nt(l) < 64 ? G::nt(l) : 64) <= (1 << G::lg(l)); }
+    static constexpr bool uni(int l) { return (nt(l) < 64 ? nt(l) : 64) <= (1 << G::lg(l)); }
     // the whole level of the tile inside one un_ele: one operator record for all its chunks
-    static constexpr bool one(int l) { return G::nt(l) <= (1 << G::lg(l)); }
+    static constexpr bool one(int l) { return nt(l) <= (1 << G::lg(l)); }
     static constexpr int NCH = [] { int n = 0; for (int l = 1; l <= C; ++l) n += K(l); return n; }();
     static constexpr int lev(int j) { int l = 1; while (j >= K(l)) { j -= K(l); ++l; } return l; }
     static constexpr int kk(int j) { int l = 1; while (j >= K(l)) { j -= K(l); ++l; } return j; }
     // LDS images for the (dead) prolongator cascades: F_l (restriction-leg tnew, 1 <= l < C)
     // and Y_l (final tnew, 2 <= l <= C)
-    static constexpr int F(int l) { int o = 0; for (int i = 1; i < l; ++i) o += 3 * G::nt(i); return o; }
-    static constexpr int Y(int l) { int o = F(C); for (int i = 2; i < l; ++i) o += 3 * G::nt(i); return o; }
+    static constexpr int F(int l) { int o = 0; for (int i = 1; i < l; ++i) o += 3 * nt(i); return o; }
+    static constexpr int Y(int l) { int o = F(C); for (int i = 2; i < l; ++i) o += 3 * nt(i); return o; }
     // M_l (1 <= l < C): mean of the three new residual components of each sub-element,
     // the restrictor's input (splitting.F90:146-151)
-    static constexpr int M(int l) { int o = Y(C + 1); for (int i = 1; i < l; ++i) o += G::nt(i); return o; }
+    static constexpr int M(int l) { int o = Y(C + 1); for (int i = 1; i < l; ++i) o += nt(i); return o; }
     static constexpr int total = M(C) > 0 ? M(C) : 1;
 };
 
@@ -276,8 +283,8 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
-    const int64_t u0 = (int64_t)blockIdx.x << G::GL;
-    const int nue = G::GL == 0 ? 1 : (int)min((int64_t)1 << G::GL, A.U - u0);   // un_eles in this tile
+    const int64_t u0 = (int64_t)blockIdx.x << Q::GL;
+    const int nue = Q::GL == 0 ? 1 : (int)min((int64_t)1 << Q::GL, A.U - u0);   // un_eles in this tile
     stamp<kMTc>(A, 0);
     stamp_hwid<kMTc>(A);
     // chunk j = (level l, k): tile index t + 64 k; idle lanes (beyond the level or the
@@ -287,20 +294,19 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         const int l = Q::lev(j), i = t + 64 * Q::kk(j);
-        ok[j] = i < G::nt(l) && i < (nue << G::lg(l));
+        ok[j] = i < Q::nt(l) && i < (nue << G::lg(l));
         gx[j] = ((uint32_t)u0 << G::lg(l)) + (uint32_t)(ok[j] ? i : 0);
     }
-    // operator records: one per level when the tile's level lies in one un_ele (n_split = 5),
-    // else one per chunk, fetched where used
-    Stc SL[C + 1];
+    // operator records, fetched once: one per level when the tile's level lies in one un_ele
+    // (scalar registers), else one per chunk (vector registers when the chunk spans un_eles)
+    Stc SL[C + 1], SC[N];
 #pragma unroll
     for (int l = 1; l <= C; ++l)
         if (Q::one(l)) stencil(Q::uni(l), SP[l], ((uint32_t)u0 << G::lg(l)) >> G::lg(l), SL[l]);
-    auto stc_of = [&](int j, Stc &St) {
-        const int l = Q::lev(j);
-        if (Q::one(l)) St = SL[l];
-        else stencil(Q::uni(l), SP[l], gx[j] >> G::lg(l), St);
-    };
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+        if (!Q::one(Q::lev(j))) stencil(Q::uni(Q::lev(j)), SP[Q::lev(j)], gx[j] >> G::lg(Q::lev(j)), SC[j]);
+    auto stc_of = [&](int j, Stc &St) { St = Q::one(Q::lev(j)) ? SL[Q::lev(j)] : SC[j]; };
     // ---- prologue: tnew of every level (tnew_nonlin := tnew, :327 / :348), halo positions,
     //      and the restrictor (:336) of every level: RHS_l := RHSN_l, the restriction of the
     //      PREVIOUS cycle's residual, computed when that residual was (below, and in the
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
             if (ok[j]) {
                 const int i = t + 64 * Q::kk(j);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) lds[Q::F(l) + c * G::nt(l) + i] = p[j][c];
+                for (int c = 0; c < 3; ++c) lds[Q::F(l) + c * Q::nt(l) + i] = p[j][c];
                 lds[Q::M(l) + i] = (r[0] + r[1] + r[2]) / 3.;
             }
         }
@@ -395,7 +401,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
             store3(V.T(), V.pitch, gx[j], p[j]);
             if (l >= 2)
 #pragma unroll
-                for (int c = 0; c < 3; ++c) lds[Q::Y(l) + c * G::nt(l) + t + 64 * Q::kk(j)] = p[j][c];
+                for (int c = 0; c < 3; ++c) lds[Q::Y(l) + c * Q::nt(l) + t + 64 * Q::kk(j)] = p[j][c];
         }
     }
     // ---- prolongator (:370) among the coarse levels, on the LDS images of the
@@ -410,8 +416,8 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
             const int4 c4 = A.lv[l].children[gx[j] & ((1 << G::lg(l)) - 1)];
             const int base = (i >> G::lg(l)) << G::lg(l - 1);
             const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
-            const double y[3] = {lds[Q::Y(l) + i], lds[Q::Y(l) + G::nt(l) + i], lds[Q::Y(l) + 2 * G::nt(l) + i]};
-            prolong_cascade(lds + Q::F(l - 1), G::nt(l - 1), fi, y);
+            const double y[3] = {lds[Q::Y(l) + i], lds[Q::Y(l) + Q::nt(l) + i], lds[Q::Y(l) + 2 * Q::nt(l) + i]};
+            prolong_cascade(lds + Q::F(l - 1), Q::nt(l - 1), fi, y);
         }
     }
     stamp<kMTc>(A, 7);
@@ -558,7 +564,8 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.n_smooth = n_smooth;
     A.n_coarse = n_coarse;
     A.rdt = rdt;
-    const int GL = 10 - 2 * n_split;   // 1024 / 4**n_split un_eles per tile
+    // tile: 1024 level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
+    const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : 10 - 2 * n_split;
     const unsigned grid = (unsigned)(((int64_t)U + (1 << GL) - 1) >> GL);
     if (grid == 0) return hipSuccess;
     // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
