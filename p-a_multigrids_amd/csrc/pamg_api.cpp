@@ -83,14 +83,15 @@ hipEvent_t take_event(pamg_handle *h) {
 }
 
 struct Span {
-    pamg_handle *h; int kid; double bytes; hipEvent_t a = nullptr;
-    Span(pamg_handle *h_, int kid_, double bytes_) : h(h_), kid(kid_), bytes(bytes_) {
-        if (h->timing.mask & (1u << kid)) { a = take_event(h); (void)hipEventRecord(a, h->stream); }
+    pamg_handle *h; int kid; double bytes; hipStream_t s; hipEvent_t a = nullptr;
+    Span(pamg_handle *h_, int kid_, double bytes_, hipStream_t s_ = nullptr)
+        : h(h_), kid(kid_), bytes(bytes_), s(s_ ? s_ : h_->stream) {
+        if (h->timing.mask & (1u << kid)) { a = take_event(h); (void)hipEventRecord(a, s); }
     }
     ~Span() {
         if (!a) return;
         hipEvent_t b = take_event(h);
-        (void)hipEventRecord(b, h->stream);
+        (void)hipEventRecord(b, s);
         h->timing.pending.push_back(Timing::Rec{kid, a, b, bytes});
     }
 };
@@ -140,24 +141,55 @@ double *field_ptr(pamg_handle *h, int l, int what) {
 // The halo words of a smoother call are written by the smoother kernel itself
 // (local neighbours and boundary values into t_overlap, remote neighbours into
 // the packed send buffer); what remains here is the exchange with other ranks.
-int halo(pamg_handle *h, int l) {
+int exchange(pamg_handle *h, int l, int buf, hipStream_t st) {
     Level &L = h->lv[l];
     const HaloPlan &P = L.halo;
-    if (h->comm && !P.peers.empty()) {
-        Span sp(h, PAMG_K_HALO, 2.0 * 48.0 * (double)(P.remote.size() + P.recv_dst.size()));
-        NCCLCHK(h, ncclGroupStart());
-        for (size_t q = 0; q < P.peers.size(); ++q) {
-            const int peer = P.peers[q];
-            const size_t ns = (size_t)(P.send_peer_off[q + 1] - P.send_peer_off[q]);
-            const size_t nr = (size_t)(P.recv_peer_off[q + 1] - P.recv_peer_off[q]);
-            if (ns) NCCLCHK(h, ncclSend(P.d_send + 6 * (size_t)P.send_peer_off[q], 6 * ns, ncclDouble, peer,
-                                        h->comm->nccl, h->stream));
-            if (nr) NCCLCHK(h, ncclRecv(P.d_recv + 6 * (size_t)P.recv_peer_off[q], 6 * nr, ncclDouble, peer,
-                                        h->comm->nccl, h->stream));
-        }
-        NCCLCHK(h, ncclGroupEnd());
-        HIPCHK(h, launch_halo_unpack(h->stream, L, h->tov, h->tovo));
+    const double *send = P.send_buf(buf);
+    Span sp(h, PAMG_K_HALO, 2.0 * 48.0 * (double)(P.remote.size() + P.recv_dst.size()), st);
+    NCCLCHK(h, ncclGroupStart());
+    for (size_t q = 0; q < P.peers.size(); ++q) {
+        const int peer = P.peers[q];
+        const size_t ns = (size_t)(P.send_peer_off[q + 1] - P.send_peer_off[q]);
+        const size_t nr = (size_t)(P.recv_peer_off[q + 1] - P.recv_peer_off[q]);
+        if (ns) NCCLCHK(h, ncclSend(send + 6 * (size_t)P.send_peer_off[q], 6 * ns, ncclDouble, peer, h->comm->nccl, st));
+        if (nr) NCCLCHK(h, ncclRecv(P.d_recv + 6 * (size_t)P.recv_peer_off[q], 6 * nr, ncclDouble, peer,
+                                    h->comm->nccl, st));
     }
+    NCCLCHK(h, ncclGroupEnd());
+    HIPCHK(h, launch_halo_unpack(st, L, h->tov, h->tovo));
+    return PAMG_OK;
+}
+
+int halo(pamg_handle *h, int l) {
+    const HaloPlan &P = h->lv[l].halo;
+    if (h->comm && !P.peers.empty()) {
+        h->lv[l].halo.send_cur = 0;   // the per-step kernels pack into the first buffer
+        return exchange(h, l, 0, h->stream);
+    }
+    return PAMG_OK;
+}
+
+// fused V-cycle: the exchange of level 1's words packed into `buf` runs on stream_comm,
+// overlapped with the next cycle (nothing in a cycle reads t_overlap)
+int halo_async(pamg_handle *h, int buf) {
+    HaloPlan &P = h->lv[1].halo;
+    P.send_cur = buf;
+    if (!h->comm || P.peers.empty()) return PAMG_OK;
+    HIPCHK(h, hipEventRecord(h->ev_packed, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->stream_comm, h->ev_packed, 0));
+    CHK(exchange(h, 1, buf, h->stream_comm));
+    HIPCHK(h, hipEventRecord(h->ev_sent[buf], h->stream_comm));
+    h->sent_pending[buf] = true;
+    return PAMG_OK;
+}
+
+// `stream` continues after every exchange in flight
+int join_comm(pamg_handle *h) {
+    for (int b = 0; b < 2; ++b)
+        if (h->sent_pending[b]) {
+            HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[b], 0));
+            h->sent_pending[b] = false;
+        }
     return PAMG_OK;
 }
 
@@ -266,33 +298,9 @@ double vcycle_coarse_bytes(pamg_handle *h) {
     return b + 104.0 * h->U * (L - 1);
 }
 
-int vcycle_once(pamg_handle *h) {
+// one V-cycle as the per-step kernel sequence of transport_tri_semi.F90:319-379
+int vcycle_steps(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
-    if (h->p.fused && vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, ns)) {
-        if (!h->rhsn_valid) {   // residuals changed outside the fused cycle: restrict them afresh
-            for (int l = 1; l < L; ++l)
-                HIPCHK(h, launch_restrict(h->stream, h->lv[l], h->lv[l + 1], h->U, h->lv[l + 1].RHSN));
-            h->rhsn_valid = true;
-        }
-        if (!h->overlap_static_l1) {   // once per time step: the halo words the cycle's last smoother
-            HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo));   // leaves constant
-            h->overlap_static_l1 = true;
-        }
-        if (L > 1) {   // levels 2..L first: level 1's halo words are the cycle's last
-            Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h));
-            HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse,
-                                           1 / h->p.dt, h->tov, h->tovo));
-        }
-        {
-            Span sp(h, PAMG_K_VCYCLE, vcycle_fine_bytes(h));
-            HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, 1 / h->p.dt,
-                                         h->tov, h->tovo));
-        }
-        h->tnn_level = 1;
-        // the remote halo words of every smoother call were packed in the kernel; the last
-        // (level-1) pack covers every slot the coarser levels wrote, so one exchange suffices
-        return halo(h, 1);
-    }
     for (int l = 1; l <= L; ++l) {           // :323-340
         CHK(smooth(h, l, true, ns));
         CHK(restrict_residual(h, l));
@@ -305,12 +313,53 @@ int vcycle_once(pamg_handle *h) {
     return PAMG_OK;
 }
 
+// n V-cycles as two fused launches each (pamg_vcycle.hip)
+int vcycle_fused(pamg_handle *h, int n) {
+    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    const double rdt = 1 / h->p.dt;
+    HaloPlan &P1 = h->lv[1].halo;
+    const bool two = P1.d_send_b != nullptr;   // remote peers: pack into alternate buffers
+    if (!h->rhsn_valid) {   // residuals changed outside the fused cycle: restrict them afresh
+        for (int l = 1; l < L; ++l)
+            HIPCHK(h, launch_restrict(h->stream, h->lv[l], h->lv[l + 1], h->U, h->lv[l + 1].RHSN));
+        h->rhsn_valid = true;
+    }
+    if (!h->overlap_static_l1) {   // once per time step: the halo words the cycle's last smoother
+        CHK(join_comm(h));         // leaves constant (into both send buffers)
+        HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo));
+        if (two) HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, P1.d_send_b));
+        h->overlap_static_l1 = true;
+    }
+    for (int c = 0; c < n; ++c) {
+        const int buf = two ? 1 - P1.send_cur : 0;
+        if (h->sent_pending[buf]) {   // the exchange that read this buffer two cycles ago
+            HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[buf], 0));
+            h->sent_pending[buf] = false;
+        }
+        if (L > 1) {   // levels 2..L first: the prolongator of level 1 reads their final tnew
+            Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h));
+            HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
+                                           h->tovo));
+        }
+        {
+            Span sp(h, PAMG_K_VCYCLE, vcycle_fine_bytes(h));
+            HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
+                                         h->tovo, P1.send_buf(buf)));
+        }
+        h->tnn_level = 1;
+        // every halo word of the cycle was written by the level-1 launch (its remote ones
+        // packed into `buf`): one exchange per cycle, in flight during the next one
+        CHK(halo_async(h, buf));
+    }
+    return join_comm(h);
+}
+
 void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
         Level &L = h->lv[l];
         dev_free(L.T); dev_free(L.stc); dev_free(L.subinfo); dev_free(L.children); dev_free(L.blocks);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
-        dev_free(L.halo.d_send); dev_free(L.halo.d_recv);
+        dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
         dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
         dev_free(L.halo.d_surf); dev_free(L.halo.d_told_halo);
         L = Level();
@@ -356,7 +405,11 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
     h->p = *p;
     h->device = p->device;
     if (hipSetDevice(h->device) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->stream_comm, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_sent[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_sent[1], hipEventDisableTiming) != hipSuccess) {
         delete h;
         return PAMG_ERR_HIP;
     }
@@ -488,6 +541,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         CHK(dev_alloc(h, &P.d_told_halo, 3 * (size_t)P.n_told));
         CHK(refresh_told_halo(h, l));
         CHK(dev_alloc(h, &P.d_send, 6 * P.remote.size()));
+        if (l == 1 && !P.remote.empty()) CHK(dev_alloc(h, &P.d_send_b, 6 * P.remote.size()));
         CHK(dev_alloc(h, &P.d_recv, 6 * P.recv_dst.size()));
     }
     // initial condition (:237-252): tnew = 0, region 4 => 1 on level 1
@@ -624,7 +678,10 @@ int pamg_prolongator(pamg_handle *h, int level) {
 int pamg_vcycle(pamg_handle *h, int n) {
     if (!h || n < 0) return PAMG_ERR_ARG;
     CHK(check_level(h, 1));
-    for (int c = 0; c < n; ++c) CHK(vcycle_once(h));
+    const int L = h->p.multi_levels;
+    if (h->p.fused && vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth))
+        return vcycle_fused(h, n);
+    for (int c = 0; c < n; ++c) CHK(vcycle_steps(h));
     return PAMG_OK;
 }
 
@@ -713,6 +770,10 @@ int pamg_destroy(pamg_handle *h) {
         if (h->comm->nccl) ncclCommDestroy(h->comm->nccl);
         delete h->comm;
     }
+    (void)hipStreamSynchronize(h->stream_comm);
+    for (hipEvent_t e : {h->ev_packed, h->ev_sent[0], h->ev_sent[1]})
+        if (e) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(h->stream_comm);
     (void)hipStreamDestroy(h->stream);
     delete h;
     return PAMG_OK;

@@ -59,6 +59,11 @@ struct HaloPlan {
     HaloBC *d_bc = nullptr;
     int *d_recv_dst = nullptr;
     double *d_send = nullptr, *d_recv = nullptr;   // 6 doubles per entry (tnew 3, told 3)
+    // second send buffer: the fused V-cycle packs cycle k+1 while cycle k's exchange is in
+    // flight; send_cur = the buffer holding the last packed words
+    double *d_send_b = nullptr;
+    int send_cur = 0;
+    double *send_buf(int i) const { return i ? d_send_b : d_send; }
 };
 
 struct Level {
@@ -108,6 +113,11 @@ struct pamg_handle {
     // time step (the fused V-cycle then writes only the tnew words); cleared by every
     // operation that writes or changes them otherwise
     bool overlap_static_l1 = false;
+    // the fused V-cycle's halo exchange (RCCL) runs on stream_comm, overlapped with the next
+    // cycle; joined back into `stream` before pamg_vcycle returns
+    hipStream_t stream_comm = nullptr;
+    hipEvent_t ev_packed = nullptr, ev_sent[2] = {nullptr, nullptr};
+    bool sent_pending[2] = {false, false};
     // RHSN of every level holds the restriction of the finer level's current residual
     bool rhsn_valid = true;
     bool mesh_ready = false;
@@ -143,13 +153,15 @@ hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double 
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
 hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
 hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);
-hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo);
+hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo,
+                                 double *send = nullptr);
 // fused V-cycle (pamg_vcycle.hip); lv is the handle's 1-based level array
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth);
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                 int n_coarse, double rdt, double *tov, double *tovo);   // levels 2..L
+// level 1; its remote halo words packed into send1 (one of level 1's two send buffers)
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                              int n_coarse, double rdt, double *tov, double *tovo);     // level 1
+                              int n_coarse, double rdt, double *tov, double *tovo, double *send1);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch);

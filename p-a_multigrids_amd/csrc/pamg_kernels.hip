@@ -631,11 +631,11 @@ hipError_t launch_told_halo(hipStream_t s, const Level &L, int U) {
     return hipGetLastError();
 }
 
-hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo) {
+hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo, double *send) {
     const HaloPlan &P = L.halo;
     if (U == 0 || P.d_hface == nullptr) return hipSuccess;
     const int m = 1 << L.isplit;
-    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, m};
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, send ? send : P.d_send, m};
     hipLaunchKernelGGL(k_overlap_static, dim3(grid_for((int64_t)U * 3 * m)), dim3(kBlock), 0, s, H, P.d_surf, U);
     return hipGetLastError();
 }

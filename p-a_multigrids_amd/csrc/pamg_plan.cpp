@@ -102,7 +102,7 @@ int pamg_halo_loopback(pamg_handle *const *hs, int n, int level) {
             const size_t ns = qa < 0 ? 0 : (size_t)(Pa.send_peer_off[qa + 1] - Pa.send_peer_off[qa]);
             if (nr != ns) { hb->err = "loopback: send/recv counts differ"; return PAMG_ERR_STATE; }
             if (nr == 0) continue;
-            if (hipMemcpy(Pb.d_recv + 6 * (size_t)Pb.recv_peer_off[qb], Pa.d_send + 6 * (size_t)Pa.send_peer_off[qa],
+            if (hipMemcpy(Pb.d_recv + 6 * (size_t)Pb.recv_peer_off[qb], Pa.send_buf(Pa.send_cur) + 6 * (size_t)Pa.send_peer_off[qa],
                           6 * nr * sizeof(double), hipMemcpyDeviceToDevice) != hipSuccess)
                 return PAMG_ERR_HIP;
         }

@@ -543,7 +543,7 @@ hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, bool co
 }
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
-                       double rdt, double *tov, double *tovo, bool coarse) {
+                       double rdt, double *tov, double *tovo, double *send1, bool coarse) {
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
     VArgs A{};
     for (int l = 0; l < L; ++l) {
@@ -558,7 +558,8 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
         o.children = (l > 0) ? lv[l].children : nullptr;   // children of level l+1 in level l
         o.pitch = V.pitch;
         const HaloPlan &P = V.halo;
-        o.H = HaloArgs{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << V.isplit};
+        o.H = HaloArgs{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, (l == 0 && send1) ? send1 : P.d_send,
+                       1 << V.isplit};
     }
     A.U = U;
     A.n_smooth = n_smooth;
@@ -612,12 +613,12 @@ bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mo
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                 int n_coarse, double rdt, double *tov, double *tovo) {
     if (L < 2) return hipSuccess;
-    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, true);
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, nullptr, true);
 }
 
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                              int n_coarse, double rdt, double *tov, double *tovo) {
-    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, false);
+                              int n_coarse, double rdt, double *tov, double *tovo, double *send1) {
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, false);
 }
 
 }  // namespace pamg

@@ -1,0 +1,38 @@
+"""Per-rank cycle time of the x-strip partition of untitled8192 at N = 1, 2, 4, 8 ranks,
+simulated on one GPU (rank 0's partition, detached: no RCCL), to size the strong-scaling
+overheads (GPU box only)."""
+import os
+import sys
+import time
+
+import torch  # noqa: F401
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "p-a_multigrids_amd"))
+import pamg  # noqa: E402
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+mesh = pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "untitled8192.msh"))
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+base = None
+for n in (1, 2, 4, 8):
+    comm = None if n == 1 else (n, 0, None, mesh.x_strip_owner(n))
+    s = pamg.SemiImplicitIterative(mesh, S, 3, n_smooth=4, solver=3, comm=comm)
+    s.begin_timestep()
+    s.vcycle(5)
+    s.synchronize()
+    res = []
+    for timed in (0, 1):
+        s.timing_enable(0x37F if timed else 0)
+        s.timing_reset()
+        k = 50
+        t0 = time.perf_counter()
+        s.vcycle(k)
+        s.synchronize()
+        dt = (time.perf_counter() - t0) / k * 1e3
+        tm = s.timing()
+        res.append((dt, {kk: round(v["ms"] / k, 4) for kk, v in tm.items() if v["launches"]}))
+    if base is None:
+        base = res[0][0]
+    print(f"N={n}: {res[0][0]:.4f} ms/cycle (ideal {base / n:.4f}, eff {base / n / res[0][0]:.2f}); "
+          f"timed {res[1][0]:.4f} {res[1][1]}", flush=True)
+    s.close()
