@@ -75,9 +75,14 @@ typedef struct {
     double theta;     /* time weighting, :117 (only 1.0 is accepted) */
     int halo_mode;    /* 0: halo written once per smoother call (state-identical),
                          1: one launch per sweep, halo at every sweep (reference timing) */
-    int fused;        /* 1: pamg_vcycle runs each V-cycle as one fused kernel when supported
-                         (solver 1/3, halo_mode 0, n_split <= 5); 0: one kernel per step */
-    int reserved[6];
+    int fused;        /* 1: pamg_vcycle runs each V-cycle as two fused launches when supported
+                         (solver 1/3, halo_mode 0, n_split <= 5, coarse_solver 0); 0: one kernel
+                         per step */
+    int coarse_solver; /* 0: the reference's n_coarse smoother calls on the coarsest level (:351-353);
+                          1: its exact local solve instead, tnew = tnew_nonlin = A_e^-1 RHS with
+                          A_e = (1/dt) M + Kd inverted by FINDInv (matrix_inversion.F90:50-148) --
+                          the direct path of SURVEY.md 8(f), not the reference's mode 9 */
+    int reserved[5];
 } pamg_params;
 
 /* mode-9 defaults of the reference (main.F90:46-47, transport_tri_semi.F90:117-140) */
@@ -140,6 +145,17 @@ int pamg_timing_read(pamg_handle *h, int kid, double *ms_total, long *launches, 
  * (assembled=0: per-un_ele stencils; assembled=1: per-sub-element 3x3 blocks,
  * block-CSR with one block per block-row, the matrices.F90 format) */
 int pamg_sweep_bench(pamg_handle *h, int sweeps, int assembled, double *ms_avg, double *bytes_per_launch);
+
+/* ---- local block solve: replaces FINDInv (matrix_inversion.F90:50-148 = matrices.F90:1618-1716) ----
+ * nb n x n matrices, column-major (n, n, nb) host arrays as the reference's
+ * `matrix(n,n)`; inverted on the handle's device by the reference's Gauss-Jordan
+ * (no pivoting, its zero-pivot row repair and give-up rule), bitwise equal to
+ * it. errorflag[q] = 0, or -1 for a matrix the routine calls non-invertible
+ * (inverse 0). n <= 8 (element blocks; the reference's dense global inverse of
+ * modes 4/8 is out of scope). */
+int pamg_block_inverse(pamg_handle *h, int n, long nb, const double *A, double *inv, int *errorflag);
+/* tnew = tnew_nonlin = A_e^-1 RHS on `level` (the coarse_solver = 1 step, callable per level) */
+int pamg_direct_solve(pamg_handle *h, int level);
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---- */
 int pamg_comm_unique_id(char out[128]);

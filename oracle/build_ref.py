@@ -32,7 +32,10 @@ Patches (each is an exact, asserted string replacement):
 
 Usage: python oracle/build_ref.py [--ref /root/reference] [--out oracle/_ref]
 Produces pamg_ref_fp64 (-fdefault-real-8 -fdefault-double-8: the parity
-target) and pamg_ref_fp32 (default real, as shipped).
+target), pamg_ref_fp32 (default real, as shipped) and
+findinv_ref_fp64 (the reference's FINDInv, matrix_inversion.F90, unmodified,
+behind oracle/ref_hooks/findinv_driver.F90: golden vectors of the local
+block inverse, tests/make_golden_findinv.py).
 """
 import argparse
 import os
@@ -194,6 +197,34 @@ def build(ref, out, fp64, verbose=False):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def build_findinv(ref, out, verbose=False):
+    """The reference's FINDInv (matrix_inversion.F90:50-148, unmodified, fp64 default real)
+    behind oracle/ref_hooks/findinv_driver.F90 -> oracle/_ref/findinv_ref_fp64."""
+    flags = ["-O2", "-fdefault-real-8", "-fdefault-double-8"]
+    tmp = tempfile.mkdtemp(prefix="pamg_findinv_")
+    try:
+        shutil.copy(os.path.join(ref, "matrix_inversion.F90"), tmp)
+        shutil.copy(os.path.join(HERE, "ref_hooks", "findinv_driver.F90"), tmp)
+        for s in ("matrix_inversion", "findinv_driver"):
+            r = subprocess.run([FLANG, "-c"] + flags + [s + ".F90", "-o", s + ".o"], cwd=tmp,
+                               capture_output=True, text=True)
+            if r.returncode != 0:
+                sys.stderr.write(r.stdout + r.stderr)
+                raise SystemExit(f"flang failed on {s}.F90")
+        os.makedirs(out, exist_ok=True)
+        exe = os.path.join(os.path.abspath(out), "findinv_ref_fp64")
+        r = subprocess.run([FLANG] + flags + ["matrix_inversion.o", "findinv_driver.o", "-o", exe], cwd=tmp,
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise SystemExit("flang link failed (findinv)")
+        if verbose:
+            print("built", exe)
+        return exe
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -206,6 +237,7 @@ def main():
         if a.only and a.only != ("fp64" if fp64 else "fp32"):
             continue
         build(a.ref, a.out, fp64, verbose=True)
+    build_findinv(a.ref, a.out, verbose=True)
 
 
 if __name__ == "__main__":

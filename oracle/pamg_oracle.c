@@ -39,6 +39,7 @@
 typedef struct {
     int n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid;
     double dt, k, omega, theta;
+    int coarse_solver;   /* 0: the reference (:351-353); 1: exact local solve (the build's direct path) */
 } orc_cfg;
 
 typedef struct {
@@ -541,6 +542,88 @@ static void prolongator(orc_state *s, int l) {
         }
 }
 
+/* matrix_inversion.F90:50-148 FINDInv: Gauss-Jordan on the augmented matrix
+ * [A | I], no pivoting; a zero pivot is repaired by adding the first lower row
+ * with a nonzero entry in that column (:75-86) -- but the search gives up at the
+ * first zero entry (:87-92); matrices are column-major (n, n). Returns the
+ * errorflag (0 / -1; inverse = 0 on -1). */
+int orc_findinv(int n, const double *A, double *inv) {
+    double aug[16][32];
+    if (n < 1 || n > 16) return -2;
+#define AG(i, j) aug[(i) - 1][(j) - 1]
+    for (int i = 1; i <= n; ++i)
+        for (int j = 1; j <= 2 * n; ++j) {
+            if (j <= n) AG(i, j) = A[(i - 1) + (size_t)(j - 1) * n];
+            else if (i + n == j) AG(i, j) = 1;
+            else AG(i, j) = 0;
+        }
+    for (int k = 1; k <= n - 1; ++k) {
+        if (AG(k, k) == 0) {
+            int flag = 0;
+            for (int i = k + 1; i <= n; ++i) {
+                if (AG(i, k) != 0) {
+                    for (int j = 1; j <= 2 * n; ++j) AG(k, j) = AG(k, j) + AG(i, j);
+                    flag = 1;
+                    break;
+                }
+                if (!flag) {
+                    for (int q = 0; q < n * n; ++q) inv[q] = 0;
+                    return -1;
+                }
+            }
+        }
+        for (int j = k + 1; j <= n; ++j) {
+            double m = AG(j, k) / AG(k, k);
+            for (int i = k; i <= 2 * n; ++i) AG(j, i) = AG(j, i) - m * AG(k, i);
+        }
+    }
+    for (int i = 1; i <= n; ++i)
+        if (AG(i, i) == 0) {
+            for (int q = 0; q < n * n; ++q) inv[q] = 0;
+            return -1;
+        }
+    for (int i = 1; i <= n; ++i) {
+        double m = AG(i, i);
+        for (int j = i; j <= 2 * n; ++j) AG(i, j) = AG(i, j) / m;
+    }
+    for (int k = n - 1; k >= 1; --k)
+        for (int i = 1; i <= k; ++i) {
+            double m = AG(i, k + 1);
+            for (int j = k; j <= 2 * n; ++j) AG(i, j) = AG(i, j) - AG(k + 1, j) * m;
+        }
+    for (int i = 1; i <= n; ++i)
+        for (int j = 1; j <= n; ++j) inv[(i - 1) + (size_t)(j - 1) * n] = AG(i, j + n);
+#undef AG
+    return 0;
+}
+
+/* THE BUILD'S DIRECT PATH (coarse_solver = 1; not in the reference's mode 9):
+ * tnew = tnew_nonlin = A_e^-1 RHS per sub-element, A_e = (1/dt) M + Kd the smoother's
+ * operator (get_A_x :412-448 assembled, theta = 1, u = 0) inverted by FINDInv. */
+static void direct_solve(orc_state *s, int l) {
+    int nsub = s->nsub[l - 1];
+    double rdt = 1 / s->c.dt;
+    free(s->tnn);
+    s->tnn = malloc(lvl_len(s, l) * sizeof(double));
+    s->tnn_level = l;
+    for (int u = 0; u < s->U; ++u) {
+        double M[3][3], Kd[3][3], ml[3], a[9], inv[9];
+        stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) a[i + 3 * j] = rdt * M[i][j] + Kd[i][j];
+        orc_findinv(3, a, inv);
+        for (int se = 0; se < nsub; ++se) {
+            size_t o = (size_t)3 * ((size_t)u * nsub + se);
+            const double *b = s->rhs[l - 1] + o;
+            for (int i = 0; i < 3; ++i) {
+                double x = inv[i] * b[0] + inv[i + 3] * b[1] + inv[i + 6] * b[2];
+                s->tnew[l - 1][o + i] = x;
+                s->tnn[o + i] = x;
+            }
+        }
+    }
+}
+
 /* ----------------------------------------------------------- public API */
 
 int orc_msh_count(const char *path) { return read_msh(path, NULL); }
@@ -668,6 +751,7 @@ void orc_get_residual(orc_state *s, int l) { get_residual(s, l); }
 void orc_restrictor(orc_state *s, int l) { restrictor(s, l); }
 void orc_prolongator(orc_state *s, int l) { prolongator(s, l); }
 void orc_update_overlaps(orc_state *s, int l) { update_overlaps(s, l); }
+void orc_direct_solve(orc_state *s, int l) { direct_solve(s, l); }
 
 /* :316-317 */
 void orc_begin_timestep(orc_state *s) {
@@ -684,8 +768,12 @@ void orc_vcycle(orc_state *s) {
         restrictor(s, l);
         get_residual(s, l);
     }
-    copy_to_tnn(s, L);
-    for (int i = 0; i < s->c.n_coarse; ++i) smoother(s, L);
+    if (s->c.coarse_solver == 1) {
+        direct_solve(s, L);
+    } else {
+        copy_to_tnn(s, L);
+        for (int i = 0; i < s->c.n_coarse; ++i) smoother(s, L);
+    }
     for (int l = L - 1; l >= 1; --l) {
         copy_to_tnn(s, l);
         prolongator(s, l);

@@ -298,6 +298,31 @@ double vcycle_coarse_bytes(pamg_handle *h) {
     return b + 104.0 * h->U * (L - 1);
 }
 
+// the exact local solve of level l (coarse_solver = 1): tnew = tnew_nonlin = A_e^-1 RHS, with
+// A_e^-1 from FINDInv, formed on first use
+int direct_solve(pamg_handle *h, int l) {
+    Level &L = h->lv[l];
+    if (!L.Ainv) {
+        int *d_err = nullptr;
+        CHK(dev_alloc(h, &L.Ainv, 9 * (size_t)std::max(h->U, 1)));
+        HIPCHK(h, hipMalloc((void **)&d_err, sizeof(int) * std::max(h->U, 1)));
+        HIPCHK(h, launch_block_ops(h->stream, L, h->U, 1 / h->p.dt, L.Ainv, d_err));
+        std::vector<int> err(std::max(h->U, 1));
+        HIPCHK(h, hipMemcpyAsync(err.data(), d_err, sizeof(int) * h->U, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(d_err);
+        for (int q = 0; q < h->U; ++q)
+            if (err[q]) {
+                h->err = "FINDInv: operator block of un_ele " + std::to_string(h->owned[q] + 1) + " on level " +
+                         std::to_string(l) + " is not invertible";
+                return PAMG_ERR_STATE;
+            }
+    }
+    h->tnn_level = l;
+    HIPCHK(h, launch_block_solve(h->stream, L, L.Ainv));
+    return PAMG_OK;
+}
+
 // one V-cycle as the per-step kernel sequence of transport_tri_semi.F90:319-379
 int vcycle_steps(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
@@ -305,7 +330,8 @@ int vcycle_steps(pamg_handle *h) {
         CHK(smooth(h, l, true, ns));
         CHK(restrict_residual(h, l));
     }
-    CHK(smooth(h, L, true, ns * h->p.n_coarse));   // :344-359
+    if (h->p.coarse_solver == 1) CHK(direct_solve(h, L));   // the direct path instead of :344-359
+    else CHK(smooth(h, L, true, ns * h->p.n_coarse));   // :344-359
     for (int l = L - 1; l >= 1; --l) {             // :363-378
         CHK(prolong(h, l, true));
         CHK(smooth(h, l, false, ns));
@@ -357,7 +383,7 @@ int vcycle_fused(pamg_handle *h, int n) {
 void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
         Level &L = h->lv[l];
-        dev_free(L.T); dev_free(L.stc); dev_free(L.subinfo); dev_free(L.children); dev_free(L.blocks);
+        dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.children); dev_free(L.blocks);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
         dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
@@ -396,7 +422,8 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
     *out = nullptr;
     if (p->multi_levels < 1 || p->multi_levels > p->n_split || p->n_split > kMaxLevels || p->n_split < 1 ||
         p->n_smooth < 0 || p->n_coarse < 0 || (p->solver < 1 || p->solver > 3) || !(p->dt > 0) ||
-        p->theta != 1.0 || (p->halo_mode != 0 && p->halo_mode != 1))
+        p->theta != 1.0 || (p->halo_mode != 0 && p->halo_mode != 1) ||
+        (p->coarse_solver != 0 && p->coarse_solver != 1))
         return PAMG_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PAMG_ERR_NODEV;
@@ -679,10 +706,42 @@ int pamg_vcycle(pamg_handle *h, int n) {
     if (!h || n < 0) return PAMG_ERR_ARG;
     CHK(check_level(h, 1));
     const int L = h->p.multi_levels;
-    if (h->p.fused && vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth))
+    if (h->p.fused && h->p.coarse_solver == 0 &&
+        vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth))
         return vcycle_fused(h, n);
     for (int c = 0; c < n; ++c) CHK(vcycle_steps(h));
     return PAMG_OK;
+}
+
+int pamg_direct_solve(pamg_handle *h, int level) {
+    if (!h) return PAMG_ERR_ARG;
+    CHK(check_level(h, level));
+    return direct_solve(h, level);
+}
+
+int pamg_block_inverse(pamg_handle *h, int n, long nb, const double *A, double *inv, int *errorflag) {
+    if (!h || n < 1 || n > 8 || nb < 0 || (nb > 0 && (!A || !inv || !errorflag))) return PAMG_ERR_ARG;
+    if (nb == 0) return PAMG_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    const size_t nd = (size_t)n * n * (size_t)nb;
+    double *dA = nullptr, *dI = nullptr;
+    int *dE = nullptr;
+    int rc = PAMG_OK;
+    if (hipMalloc((void **)&dA, nd * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&dI, nd * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&dE, (size_t)nb * sizeof(int)) != hipSuccess ||
+        hipMemcpyAsync(dA, A, nd * sizeof(double), hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+        launch_block_inverse(h->stream, n, nb, dA, dI, dE) != hipSuccess ||
+        hipMemcpyAsync(inv, dI, nd * sizeof(double), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        hipMemcpyAsync(errorflag, dE, (size_t)nb * sizeof(int), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess) {
+        h->err = "pamg_block_inverse: HIP error";
+        rc = PAMG_ERR_HIP;
+    }
+    (void)hipFree(dA);
+    (void)hipFree(dI);
+    (void)hipFree(dE);
+    return rc;
 }
 
 int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {

@@ -79,6 +79,7 @@ struct Level {
     double *stc = nullptr;            // U_local * kStcStride
     int2 *subinfo = nullptr;          // nsub: (irow, ipos) of get_str_info
     int4 *children = nullptr;         // nsub/4 (children of the next coarser level's sub-elements)
+    double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
     HaloPlan halo;
 };
@@ -164,6 +165,12 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
+// FINDInv (matrix_inversion.F90:50-148) batched, n <= 8, column-major (n, n, nb)
+hipError_t launch_block_inverse(hipStream_t s, int n, int64_t nb, const double *A, double *inv, int *err);
+// A_e = (1/dt) M + Kd per un_ele of level L and its FINDInv inverse (9 fp64 per un_ele)
+hipError_t launch_block_ops(hipStream_t s, const Level &L, int U, double rdt, double *Ainv, int *err);
+// direct local solve of level L: tnew = tnew_nonlin = A_e^-1 RHS
+hipError_t launch_block_solve(hipStream_t s, const Level &L, const double *Ainv);
 hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch);
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);

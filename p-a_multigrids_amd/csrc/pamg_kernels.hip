@@ -513,6 +513,123 @@ __global__ __launch_bounds__(kBlock) void k_sweep_stencil(const double *__restri
     for (int c = 0; c < 3; ++c) st2(out + c * pitch + s, make_double2(x0[c], x1[c]));
 }
 
+// FINDInv (matrix_inversion.F90:50-148), the reference's local block solve: Gauss-Jordan
+// on [A | I] without pivoting, a zero pivot repaired by adding the first lower row with a
+// nonzero entry in that column (:75-86) -- the search gives up at the first zero entry
+// (:87-92) -- errorflag -1 and inverse 0 for a singular matrix (:94-102). Column-major
+// n x n, the reference's operation order (bitwise equal to it, tests/test_block_inverse.py).
+template <int N>
+__device__ __forceinline__ int findinv(const double *__restrict__ A, double *__restrict__ inv) {
+    double ag[N][2 * N];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < 2 * N; ++j) ag[i][j] = j < N ? A[i + j * N] : (j - N == i ? 1.0 : 0.0);
+    int err = 0;
+#pragma unroll
+    for (int k = 0; k < N - 1; ++k) {
+        if (ag[k][k] == 0) {
+            bool found = false;
+#pragma unroll
+            for (int i = k + 1; i < N; ++i) {
+                if (found || err) continue;
+                if (ag[i][k] != 0) {
+#pragma unroll
+                    for (int j = 0; j < 2 * N; ++j) ag[k][j] = ag[k][j] + ag[i][j];
+                    found = true;
+                } else {
+                    err = -1;   // :87-92: the first zero entry ends the search
+                }
+            }
+        }
+        if (err) break;
+#pragma unroll
+        for (int j = k + 1; j < N; ++j) {
+            const double m = ag[j][k] / ag[k][k];
+#pragma unroll
+            for (int i = k; i < 2 * N; ++i) ag[j][i] = ag[j][i] - m * ag[k][i];
+        }
+    }
+    if (!err) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (ag[i][i] == 0) err = -1;
+    }
+    if (err) {
+#pragma unroll
+        for (int q = 0; q < N * N; ++q) inv[q] = 0.0;
+        return err;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const double m = ag[i][i];
+#pragma unroll
+        for (int j = i; j < 2 * N; ++j) ag[i][j] = ag[i][j] / m;
+    }
+#pragma unroll
+    for (int k = N - 2; k >= 0; --k)
+#pragma unroll
+        for (int i = 0; i <= k; ++i) {
+            const double m = ag[i][k + 1];
+#pragma unroll
+            for (int j = k; j < 2 * N; ++j) ag[i][j] = ag[i][j] - ag[k + 1][j] * m;
+        }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) inv[i + j * N] = ag[i][j + N];
+    return 0;
+}
+
+// one matrix per thread
+template <int N>
+__global__ __launch_bounds__(64) void k_block_inverse(const double *__restrict__ A, double *__restrict__ inv,
+                                                      int *__restrict__ err, int64_t nb) {
+    const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (q >= nb) return;
+    double a[N * N], o[N * N];
+#pragma unroll
+    for (int i = 0; i < N * N; ++i) a[i] = A[q * N * N + i];
+    err[q] = findinv<N>(a, o);
+#pragma unroll
+    for (int i = 0; i < N * N; ++i) inv[q * N * N + i] = o[i];
+}
+
+// the exact local solve of the smoother's operator: per un_ele, A_e = (1/dt) M + Kd
+// (get_A_x, transport_tri_semi.F90:412-448, as an assembled block; matrices.F90 block-CSR
+// with one block per block-row) and its FINDInv inverse, column-major at Ainv + 9 u
+__global__ __launch_bounds__(kBlock) void k_block_ops(const double *__restrict__ stc, double rdt,
+                                                      double *__restrict__ Ainv, int *__restrict__ err, int U) {
+    const int u = blockIdx.x * kBlock + threadIdx.x;
+    if (u >= U) return;
+    const double *r = stc + (int64_t)u * kStcStride;
+    double a[9], o[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a[i + 3 * j] = rdt * r[kStcM + 3 * i + j] + r[kStcK + 3 * i + j];
+    err[u] = findinv<3>(a, o);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) Ainv[9 * (int64_t)u + q] = o[q];
+}
+
+// direct solve of a level: tnew = tnew_nonlin = A_e^-1 RHS per sub-element
+__global__ __launch_bounds__(kBlock) void k_block_solve(double *__restrict__ T, double *__restrict__ TNN,
+                                                        const double *__restrict__ RHS,
+                                                        const double *__restrict__ Ainv, int64_t pitch, int64_t N,
+                                                        int nsub_log2) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= N) return;
+    const double *ai = Ainv + 9 * (s >> nsub_log2);
+    const double b[3] = {RHS[s], RHS[pitch + s], RHS[2 * pitch + s]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double x = ai[i] * b[0] + ai[i + 3] * b[1] + ai[i + 6] * b[2];
+        T[i * pitch + s] = x;
+        TNN[i * pitch + s] = x;
+    }
+}
+
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 inline int log2i(int v) { int r = 0; while ((1 << r) < v) ++r; return r; }
 
@@ -637,6 +754,36 @@ hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *t
     const int m = 1 << L.isplit;
     HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, send ? send : P.d_send, m};
     hipLaunchKernelGGL(k_overlap_static, dim3(grid_for((int64_t)U * 3 * m)), dim3(kBlock), 0, s, H, P.d_surf, U);
+    return hipGetLastError();
+}
+
+hipError_t launch_block_inverse(hipStream_t s, int n, int64_t nb, const double *A, double *inv, int *err) {
+    if (nb == 0) return hipSuccess;
+    const unsigned g = (unsigned)((nb + 63) / 64);
+    switch (n) {
+        case 1: hipLaunchKernelGGL(k_block_inverse<1>, dim3(g), dim3(64), 0, s, A, inv, err, nb); break;
+        case 2: hipLaunchKernelGGL(k_block_inverse<2>, dim3(g), dim3(64), 0, s, A, inv, err, nb); break;
+        case 3: hipLaunchKernelGGL(k_block_inverse<3>, dim3(g), dim3(64), 0, s, A, inv, err, nb); break;
+        case 4: hipLaunchKernelGGL(k_block_inverse<4>, dim3(g), dim3(64), 0, s, A, inv, err, nb); break;
+        case 5: hipLaunchKernelGGL(k_block_inverse<5>, dim3(g), dim3(64), 0, s, A, inv, err, nb); break;
+        case 6: hipLaunchKernelGGL(k_block_inverse<6>, dim3(g), dim3(64), 0, s, A, inv, err, nb); break;
+        case 7: hipLaunchKernelGGL(k_block_inverse<7>, dim3(g), dim3(64), 0, s, A, inv, err, nb); break;
+        case 8: hipLaunchKernelGGL(k_block_inverse<8>, dim3(g), dim3(64), 0, s, A, inv, err, nb); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_block_ops(hipStream_t s, const Level &L, int U, double rdt, double *Ainv, int *err) {
+    if (U == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_block_ops, dim3(grid_for(U)), dim3(kBlock), 0, s, L.stc, rdt, Ainv, err, U);
+    return hipGetLastError();
+}
+
+hipError_t launch_block_solve(hipStream_t s, const Level &L, const double *Ainv) {
+    if (L.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_block_solve, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.T, L.TNN, L.RHS, Ainv, L.pitch, L.N,
+                       log2i(L.nsub));
     return hipGetLastError();
 }
 

@@ -19,7 +19,8 @@ module pamg
     real(c_double) :: dt, k, omega, theta
     integer(c_int) :: halo_mode
     integer(c_int) :: fused
-    integer(c_int) :: reserved(6)
+    integer(c_int) :: coarse_solver
+    integer(c_int) :: reserved(5)
   end type pamg_params
 
   public :: pamg_default_params, pamg_msh_read, pamg_msh_size, pamg_msh_get, pamg_msh_free

@@ -28,7 +28,7 @@ class PamgParams(C.Structure):
     _fields_ = [("n_split", C.c_int), ("multi_levels", C.c_int), ("n_smooth", C.c_int),
                 ("n_coarse", C.c_int), ("solver", C.c_int), ("device", C.c_int),
                 ("dt", C.c_double), ("k", C.c_double), ("omega", C.c_double), ("theta", C.c_double),
-                ("halo_mode", C.c_int), ("fused", C.c_int), ("reserved", C.c_int * 6)]
+                ("halo_mode", C.c_int), ("fused", C.c_int), ("coarse_solver", C.c_int), ("reserved", C.c_int * 5)]
 
 
 class PamgError(RuntimeError):
@@ -79,6 +79,8 @@ def lib():
         "pamg_timing_reset": (I, [P]),
         "pamg_timing_read": (I, [P, I, C.POINTER(D), C.POINTER(C.c_long), C.POINTER(D)]),
         "pamg_sweep_bench": (I, [P, I, I, C.POINTER(D), C.POINTER(D)]),
+        "pamg_block_inverse": (I, [P, I, C.c_long, dp, dp, ip]),
+        "pamg_direct_solve": (I, [P, I]),
         "pamg_comm_unique_id": (I, [C.c_char_p]),
         "pamg_comm_init": (I, [P, I, I, C.c_char_p, I, ip]),
         "pamg_owned_count": (I, [P]),

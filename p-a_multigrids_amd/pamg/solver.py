@@ -87,12 +87,12 @@ class SemiImplicitIterative:
     """Device-resident multigrid state for one mesh (one GPU / rank)."""
 
     def __init__(self, mesh, n_split, multi_levels, n_smooth=4, solver=3, n_coarse=15, device=0,
-                 dt=1.0 * 0.0000125, k=1.0, omega=0.8, halo_mode=0, comm=None, fused=1):
+                 dt=1.0 * 0.0000125, k=1.0, omega=0.8, halo_mode=0, comm=None, fused=1, coarse_solver=0):
         self.L = lib()
         self.mesh = mesh
         self.params = default_params(n_split=n_split, multi_levels=multi_levels, n_smooth=n_smooth,
                                      solver=solver, n_coarse=n_coarse, device=device, dt=dt, k=k,
-                                     omega=omega, halo_mode=halo_mode, fused=fused)
+                                     omega=omega, halo_mode=halo_mode, fused=fused, coarse_solver=coarse_solver)
         h = C.c_void_p()
         _check("pamg_create", self.L.pamg_create(C.byref(self.params), C.byref(h)))
         self.h = h
@@ -158,6 +158,18 @@ class SemiImplicitIterative:
     def get_residual(self, level): self._call("pamg_get_residual", level)
     def prolongator(self, level): self._call("pamg_prolongator", level)
     def vcycle(self, n=1): self._call("pamg_vcycle", n)
+    def direct_solve(self, level): self._call("pamg_direct_solve", level)
+
+    def block_inverse(self, A):
+        """FINDInv (matrix_inversion.F90:50-148) of a batch A (n, n, nb), column-major as the
+        reference's matrix(n, n); returns (inverses (n, n, nb), errorflags (nb,))."""
+        A = np.asarray(A, np.float64)
+        n, nb = A.shape[0], A.shape[2]
+        a = np.ascontiguousarray(A.reshape(-1, order="F"))
+        inv = np.empty_like(a)
+        err = np.empty(nb, np.int32)
+        self._call("pamg_block_inverse", n, nb, a, inv, err)
+        return inv.reshape((n, n, nb), order="F"), err
     def run(self, ntime=2, n_multigrid=2): self._call("pamg_run", ntime, n_multigrid)
     def synchronize(self): self._call("pamg_synchronize")
 

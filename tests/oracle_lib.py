@@ -21,7 +21,7 @@ class OrcCfg(C.Structure):
     _fields_ = [("n_split", C.c_int), ("levels", C.c_int), ("n_smooth", C.c_int),
                 ("n_coarse", C.c_int), ("solver", C.c_int), ("ntime", C.c_int),
                 ("n_multigrid", C.c_int), ("dt", C.c_double), ("k", C.c_double),
-                ("omega", C.c_double), ("theta", C.c_double)]
+                ("omega", C.c_double), ("theta", C.c_double), ("coarse_solver", C.c_int)]
 
 
 _lib = None
@@ -51,8 +51,11 @@ def lib():
         L.orc_tnn_level.argtypes = [P]
         L.orc_get_overlap.argtypes = [P, dp, dp]
         L.orc_level_geometry.argtypes = [P, C.c_int, dp, dp, dp, dp]
+        dpc = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        L.orc_findinv.restype = C.c_int
+        L.orc_findinv.argtypes = [C.c_int, dpc, dpc]
         for name in ("orc_copy_to_tnn", "orc_smoother", "orc_get_residual", "orc_restrictor",
-                     "orc_prolongator", "orc_update_overlaps"):
+                     "orc_prolongator", "orc_update_overlaps", "orc_direct_solve"):
             getattr(L, name).argtypes = [P, C.c_int]
         for name in ("orc_begin_timestep", "orc_vcycle", "orc_run"):
             getattr(L, name).argtypes = [P]
@@ -83,10 +86,11 @@ def read_msh(path):
 
 class Oracle:
     def __init__(self, mesh, n_split, levels, n_smooth=4, solver=3, ntime=2, n_multigrid=2,
-                 n_coarse=15, dt=1.25e-5, k=1.0, omega=0.8, theta=1.0):
+                 n_coarse=15, dt=1.25e-5, k=1.0, omega=0.8, theta=1.0, coarse_solver=0):
         self.L = lib()
         self.mesh = mesh
-        self.cfg = OrcCfg(n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid, dt, k, omega, theta)
+        self.cfg = OrcCfg(n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid, dt, k, omega, theta,
+                          coarse_solver)
         self.h = self.L.orc_create(C.byref(self.cfg), mesh.U, mesh.X, mesh.region, mesh.neig,
                                    mesh.fneig, mesh.dir)
         if not self.h:
@@ -132,6 +136,7 @@ class Oracle:
     def restrictor(self, l): self.L.orc_restrictor(self.h, l)
     def prolongator(self, l): self.L.orc_prolongator(self.h, l)
     def update_overlaps(self, l): self.L.orc_update_overlaps(self.h, l)
+    def direct_solve(self, l): self.L.orc_direct_solve(self.h, l)
     def begin_timestep(self): self.L.orc_begin_timestep(self.h)
     def vcycle(self): self.L.orc_vcycle(self.h)
     def run(self): self.L.orc_run(self.h)
@@ -145,3 +150,16 @@ class Oracle:
             d[f"res_L{l}"] = self.get(RES, l)
         d["tnew_nonlin"] = self.get(TNN)
         return d
+
+
+def findinv(A):
+    """FINDInv restatement (oracle/pamg_oracle.c orc_findinv) of a batch A (n, n, nb)."""
+    A = np.asarray(A, np.float64)
+    n, nb = A.shape[0], A.shape[2]
+    inv = np.empty_like(A)
+    err = np.empty(nb, np.int32)
+    for q in range(nb):
+        o = np.empty(n * n)
+        err[q] = lib().orc_findinv(n, np.ascontiguousarray(A[:, :, q].reshape(-1, order="F")), o)
+        inv[:, :, q] = o.reshape((n, n), order="F")
+    return inv, err
