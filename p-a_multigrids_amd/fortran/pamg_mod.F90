@@ -27,7 +27,7 @@ module pamg
   public :: pamg_create, pamg_upload_mesh, pamg_set_state, pamg_get_state, pamg_get_overlap
   public :: pamg_begin_timestep, pamg_copy_to_nonlin, pamg_smoother, pamg_sweep, pamg_restrictor
   public :: pamg_get_residual, pamg_prolongator, pamg_vcycle, pamg_run, pamg_synchronize
-  public :: pamg_destroy, pamg_last_error, pamg_check, c_path
+  public :: pamg_destroy, pamg_last_error, pamg_check, c_path, pamg_block_inverse, pamg_direct_solve
 
   interface
     subroutine pamg_default_params(p) bind(C, name='pamg_default_params')
@@ -130,6 +130,20 @@ module pamg
     integer(c_int) function pamg_synchronize(h) bind(C, name='pamg_synchronize')
       import :: c_int, c_ptr
       type(c_ptr), value :: h
+    end function
+    integer(c_int) function pamg_block_inverse(h, n, nb, a, inv, errorflag) bind(C, name='pamg_block_inverse')
+      import :: c_int, c_ptr, c_double, c_long
+      type(c_ptr), value :: h
+      integer(c_int), value :: n
+      integer(c_long), value :: nb
+      real(c_double), intent(in) :: a(*)
+      real(c_double), intent(out) :: inv(*)
+      integer(c_int), intent(out) :: errorflag(*)
+    end function
+    integer(c_int) function pamg_direct_solve(h, level) bind(C, name='pamg_direct_solve')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+      integer(c_int), value :: level
     end function
     integer(c_int) function pamg_destroy(h) bind(C, name='pamg_destroy')
       import :: c_int, c_ptr

@@ -78,3 +78,25 @@ def test_gpu_direct_coarse_solve_matches_oracle(mesh_name, S, L):
     got, ref = s.state(), o.state()
     for k, v in ref.items():
         assert goldens.rel_err(got[k], v) <= 1e-10, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", (3, 6))
+def test_fortran_findinv_dropin_matches_reference(tmp_path, n):
+    """`use matrix_inversion; call FINDInv(a, inv, n, ierr)` as at a reference call site,
+    answered by the GPU (p-a_multigrids_amd/fortran/matrix_inversion.F90)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(goldens.HERE), "p-a_multigrids_amd", "bin", "findinv_host")
+    A, inv, err = FIX[f"n{n}_A"], FIX[f"n{n}_inv"], FIX[f"n{n}_err"]
+    cnt = A.shape[2]
+    with open(tmp_path / "findinv_in.bin", "wb") as f:
+        np.array([n, cnt], np.int32).tofile(f)
+        np.asfortranarray(A).reshape(-1, order="F").tofile(f)
+    r = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = (tmp_path / "findinv_out.bin").read_bytes()
+    got = np.frombuffer(raw[:8 * n * n * cnt], np.float64).reshape((n, n, cnt), order="F")
+    gerr = np.frombuffer(raw[8 * n * n * cnt:], np.int32)
+    np.testing.assert_array_equal(gerr, err)
+    assert same(got, inv)
+    assert r.stdout.count("Matrix is non - invertible") == int((err != 0).sum())
