@@ -13,8 +13,8 @@ every smoother call) over the whole mesh.
 N > 1 (python -m torch.distributed.run ... bench.py --gpus N): strong scaling
 of the same mesh, x-strip domain decomposition by unstructured element, one
 process per GPU, halo exchanged with RCCL (grouped ncclSend/ncclRecv over
-xGMI) after every smoother call. `value` = V-cycles of the whole mesh / max
-over ranks of the timed wall time.
+xGMI) once per V-cycle, overlapped with the next one. `value` = V-cycles of
+the whole mesh / max over ranks of the timed wall time.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
