@@ -225,3 +225,33 @@ def test_fused_vcycle_equals_kernel_sequence_bitwise(mesh, S, L, solver, ns):
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
     for x, y in zip(a.overlap(), b.overlap()):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("mesh,S,L", [("irregular.msh", 4, 3), ("untitled2048.msh", 5, 3), ("900_ele.msh", 3, 2)])
+def test_fused_vcycle_interleaved_with_call_sites_bitwise(mesh, S, L):
+    """Fused V-cycles mixed with the per-call entry points and state uploads: the fused path's
+    cached restriction (RHSN) and once-per-step halo words must follow every other writer."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    a = pamg.SemiImplicitIterative(m, S, L, fused=1)
+    b = pamg.SemiImplicitIterative(m, S, L, fused=0)
+    rng = np.random.default_rng(20251015)
+    res1 = rng.uniform(-1e-9, 1e-9, (3, a.nsub(1), a.U))
+    told = rng.uniform(-1e-6, 1e-6, (3, a.nsub(1), a.U))
+    for s in (a, b):
+        s.begin_timestep()
+        s.vcycle(1)
+        s.copy_to_tnn(1)
+        s.smoother(1)
+        s.get_residual(2)
+        s.vcycle(2)
+        s.set(pamg.RESIDUAL, 1, res1)
+        s.vcycle(1)
+        s.set(pamg.TOLD, 1, told)
+        s.vcycle(1)
+        s.begin_timestep()
+        s.vcycle(2)
+    sa, sb = a.state(), b.state()
+    for k in sb:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    for x, y in zip(a.overlap(), b.overlap()):
+        np.testing.assert_array_equal(x, y)
