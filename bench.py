@@ -46,7 +46,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the n_split=3 and sweep-kernel side measurements")
     ap.add_argument("--halo-mode", type=int, default=0)
-    ap.add_argument("--fused", type=int, default=1, help="1: one fused kernel per V-cycle (default); 0: per-step kernels")
+    ap.add_argument("--arith", type=int, default=1,
+                    help="1: contracted operator arithmetic (fma rows of A_e = M/dt + Kd; ~1e-15 of the reference, "
+                         "the north star's bar is 1e-10); 0: the reference's operation order (bitwise)")
+    ap.add_argument("--fused", type=int, default=1, help="1: two fused launches per V-cycle (default); 2: the same, concurrent on two streams; 0: per-step kernels")
     return ap.parse_args()
 
 
@@ -123,7 +126,7 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     device = local % ndev
     s = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
-                                   halo_mode=a.halo_mode, comm=comm, fused=a.fused)
+                                   halo_mode=a.halo_mode, comm=comm, fused=a.fused, arith=a.arith)
     s.begin_timestep()
     s.vcycle(a.warmup)
     s.synchronize()
@@ -183,19 +186,25 @@ def main():
                 ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
                 frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
         s.close()
-        # the same workload through the per-step kernel sequence (bitwise-identical result)
-        su = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
-                                        fused=1 - a.fused)
-        su.begin_timestep()
-        su.vcycle(a.warmup)
-        su.synchronize()
-        t0 = time.perf_counter()
-        su.vcycle(a.steps)
-        su.synchronize()
-        extra["fused0_vcycles_per_s" if a.fused else "fused1_vcycles_per_s"] = round(
-            a.steps / (time.perf_counter() - t0), 2)
-        su.close()
-        s3 = pamg.SemiImplicitIterative(mesh, 3, a.levels, n_smooth=a.nsmooth, solver=3, device=device)
+        # the same workload in the other schedules / arithmetic: the per-step kernel sequence
+        # (bitwise equal to the fused cycle), the concurrent fused launches, and the reference's
+        # operation order (bitwise equal to the reference)
+        for tag, kw in (("fused0", dict(fused=0, arith=a.arith)), ("fused2", dict(fused=2, arith=a.arith)),
+                        ("arith0", dict(fused=1, arith=0)), ("arith1", dict(fused=1, arith=1))):
+            if kw["fused"] == a.fused and kw["arith"] == a.arith:
+                continue
+            su = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
+                                            **kw)
+            su.begin_timestep()
+            su.vcycle(a.warmup)
+            su.synchronize()
+            t0 = time.perf_counter()
+            su.vcycle(a.steps)
+            su.synchronize()
+            extra[f"{tag}_vcycles_per_s"] = round(a.steps / (time.perf_counter() - t0), 2)
+            su.close()
+        s3 = pamg.SemiImplicitIterative(mesh, 3, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
+                                        arith=a.arith)
         s3.begin_timestep()
         s3.vcycle(a.warmup)
         s3.synchronize()
@@ -226,7 +235,9 @@ def main():
             "config": {"workload": f"untitled8192.msh n_split={a.nsplit} multi_levels={a.levels} "
                                    f"n_smooth={a.nsmooth} GS, 1 V-cycle per step",
                        "fine_sub_elements": mesh.U * 4 ** a.nsplit, "levels": a.levels,
-                       "parallelism": f"dd{world}", "halo_mode": a.halo_mode},
+                       "parallelism": f"dd{world}", "halo_mode": a.halo_mode,
+                       "arith": "contracted (fma, 1e-15 of the reference)" if a.arith else "reference order (bitwise)",
+                       "fused": a.fused},
             "roofline": {"bound": "hbm", "kernel": RK_DESC[rk],
                          "events": "timed region" if live_events else "post-pass of min(steps, 20) cycles",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

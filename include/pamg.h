@@ -77,12 +77,21 @@ typedef struct {
                          1: one launch per sweep, halo at every sweep (reference timing) */
     int fused;        /* 1: pamg_vcycle runs each V-cycle as two fused launches when supported
                          (solver 1/3, halo_mode 0, n_split <= 5, coarse_solver 0); 0: one kernel
-                         per step */
+                         per step; 2: the two fused launches of a cycle run concurrently on two
+                         streams (the coarse levels' fp64 work under level 1's HBM stream;
+                         state identical to 1) */
     int coarse_solver; /* 0: the reference's n_coarse smoother calls on the coarsest level (:351-353);
                           1: its exact local solve instead, tnew = tnew_nonlin = A_e^-1 RHS with
                           A_e = (1/dt) M + Kd inverted by FINDInv (matrix_inversion.F90:50-148) --
                           the direct path of SURVEY.md 8(f), not the reference's mode 9 */
-    int reserved[5];
+    int arith;        /* operator arithmetic of the smoother / residual kernels (solver 1/3):
+                         0: the reference's operation order, no contraction -- bitwise equal to the
+                            reference's fp64 build (get_A_x / solve_*, :412-507);
+                         1: contracted -- A_e = (1/dt) M + Kd assembled once per un_ele (fp64, host),
+                            one fma chain per row: 12 fp64 operations per sub-element sweep instead
+                            of 39; within 1e-13 relative of the reference (the north star's bar
+                            is 1e-10), bitwise equal between the fused and per-step schedules */
+    int reserved[4];
 } pamg_params;
 
 /* mode-9 defaults of the reference (main.F90:46-47, transport_tri_semi.F90:117-140) */

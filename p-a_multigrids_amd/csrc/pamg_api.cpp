@@ -356,27 +356,49 @@ int vcycle_fused(pamg_handle *h, int n) {
         if (two) HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, P1.d_send_b));
         h->overlap_static_l1 = true;
     }
+    // fused = 2: the coarse launch of cycle c (levels 2..L, fp64-issue-bound) runs on stream_c
+    // beside the level-1 launch of cycle c (HBM-bound). Their only shared data is level 2's
+    // RHSN, read by the coarse launch and written by the level-1 launch: double-buffered,
+    // so coarse(c) waits for level 1(c-1) (its RHS) and level 1(c) waits for coarse(c-1)
+    // (the reader of the buffer it overwrites). The level-1 launch's prolongator (:370)
+    // reads level 2's tnew, which coarse(c) may be rewriting: its result is dead (:550,
+    // SURVEY.md A3 iv) and never stored, so no state depends on the order.
+    const bool conc = h->p.fused == 2 && L > 1;
+    Level &L2 = h->lv[2];
+    if (conc) {
+        HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));   // everything issued before this call
+    }
     for (int c = 0; c < n; ++c) {
         const int buf = two ? 1 - P1.send_cur : 0;
         if (h->sent_pending[buf]) {   // the exchange that read this buffer two cycles ago
             HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[buf], 0));
             h->sent_pending[buf] = false;
         }
+        double *rhsn_w = conc ? (L2.RHSN == L2.RHSN_alt ? L2.T + 15 * L2.pitch : L2.RHSN_alt) : L2.RHSN;
+        if (conc) {
+            HIPCHK(h, hipStreamWaitEvent(h->stream_c, h->ev_fine, 0));
+            if (c > 0) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));
+        }
         if (L > 1) {   // levels 2..L first: the prolongator of level 1 reads their final tnew
-            Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h));
-            HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                           h->tovo));
+            const hipStream_t sc = conc ? h->stream_c : h->stream;
+            Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h), sc);
+            HIPCHK(h, launch_vcycle_coarse(sc, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
+                                           h->tovo, L2.RHSN));
+            if (conc) HIPCHK(h, hipEventRecord(h->ev_coarse, h->stream_c));
         }
         {
             Span sp(h, PAMG_K_VCYCLE, vcycle_fine_bytes(h));
             HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                         h->tovo, P1.send_buf(buf)));
+                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr));
+            if (conc) HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));
         }
+        if (L > 1) L2.RHSN = rhsn_w;   // the next cycle's level-2 RHS
         h->tnn_level = 1;
         // every halo word of the cycle was written by the level-1 launch (its remote ones
         // packed into `buf`): one exchange per cycle, in flight during the next one
         CHK(halo_async(h, buf));
     }
+    if (conc && n > 0) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));   // join
     return join_comm(h);
 }
 
@@ -423,7 +445,8 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
     if (p->multi_levels < 1 || p->multi_levels > p->n_split || p->n_split > kMaxLevels || p->n_split < 1 ||
         p->n_smooth < 0 || p->n_coarse < 0 || (p->solver < 1 || p->solver > 3) || !(p->dt > 0) ||
         p->theta != 1.0 || (p->halo_mode != 0 && p->halo_mode != 1) ||
-        (p->coarse_solver != 0 && p->coarse_solver != 1))
+        (p->coarse_solver != 0 && p->coarse_solver != 1) || p->fused < 0 || p->fused > 2 ||
+        (p->arith != 0 && p->arith != 1))
         return PAMG_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PAMG_ERR_NODEV;
@@ -436,7 +459,10 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
         hipStreamCreateWithFlags(&h->stream_comm, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_sent[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_sent[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->ev_sent[1], hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->stream_c, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_fine, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_coarse, hipEventDisableTiming) != hipSuccess) {
         delete h;
         return PAMG_ERR_HIP;
     }
@@ -518,15 +544,18 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
     for (int l = 1; l <= Lc; ++l) {
         Level &L = h->lv[l];
         L.isplit = S - l + 1;
+        L.arith = h->p.arith;
         L.nsub = 1 << (2 * L.isplit);
         L.N = (int64_t)L.nsub * Ul;
         L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64);
         double *base = nullptr;
-        CHK(dev_alloc(h, &base, 18 * (size_t)L.pitch));
-        HIPCHK(h, hipMemsetAsync(base, 0, 18 * (size_t)L.pitch * sizeof(double), h->stream));
+        const size_t planes = (l == 2) ? 21 : 18;   // level 2: RHSN_alt for the concurrent fused cycle
+        CHK(dev_alloc(h, &base, planes * (size_t)L.pitch));
+        HIPCHK(h, hipMemsetAsync(base, 0, planes * (size_t)L.pitch * sizeof(double), h->stream));
         L.T = base; L.TNN = base + 3 * L.pitch; L.RHS = base + 6 * L.pitch; L.RES = base + 9 * L.pitch;
         L.TOLD = base + 12 * L.pitch;
         L.RHSN = base + 15 * L.pitch;   // restriction of the zero residual: valid
+        L.RHSN_alt = (l == 2) ? base + 18 * L.pitch : nullptr;
         std::vector<double> stc((size_t)std::max(Ul, 1) * kStcStride, 0.0);
         for (int q = 0; q < Ul; ++q) {
             level_stencil(X + 6 * (size_t)h->owned[q], L.isplit, h->p.k, h->p.dt, h->p.omega,
@@ -830,9 +859,11 @@ int pamg_destroy(pamg_handle *h) {
         delete h->comm;
     }
     (void)hipStreamSynchronize(h->stream_comm);
-    for (hipEvent_t e : {h->ev_packed, h->ev_sent[0], h->ev_sent[1]})
+    if (h->stream_c) (void)hipStreamSynchronize(h->stream_c);
+    for (hipEvent_t e : {h->ev_packed, h->ev_sent[0], h->ev_sent[1], h->ev_fine, h->ev_coarse})
         if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(h->stream_comm);
+    if (h->stream_c) (void)hipStreamDestroy(h->stream_c);
     (void)hipStreamDestroy(h->stream);
     delete h;
     return PAMG_OK;

@@ -57,6 +57,52 @@ __device__ __forceinline__ void sweep(const Stc &S, double rdt, const double b[3
     for (int i = 0; i < 3; ++i) x[i] = x[i] + S.w[i] * (b[i] - A[i]);
 }
 
+// get_residual's residuale = A x - RHS (:869), reference order
+__device__ __forceinline__ void resid(const Stc &S, double rdt, const double x[3], const double b[3], double r[3]) {
+    double A[3];
+    apply_A(S, rdt, x, A);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r[i] = A[i] - b[i];
+}
+
+// Contracted operator (pamg_params.arith = 1): the element matrix A = (1/dt) M + Kd is
+// assembled once per un_ele on the host (operator record, kStcA) and every row is one
+// fma chain -- a sweep is 12 fp64 operations with a dependence depth of 4 (39 and 8 in
+// the reference's order). Same algebra as get_A_x / solve_Jacobi (:412-497); the
+// roundings differ (within 1e-13 relative of the reference, tests/test_gpu_parity.py).
+struct StcF {
+    double A[9], w[3];
+};
+
+__device__ __forceinline__ void load_stc(const double *__restrict__ rec, StcF &S) {
+#pragma unroll
+    for (int q = 0; q < 9; q += 1) S.A[q] = rec[kStcA + q];
+#pragma unroll
+    for (int q = 0; q < 3; q += 1) S.w[q] = rec[kStcW + q];
+}
+
+// x_i += w_i (b_i - sum_j A_ij x_j), all rows from the old x (Jacobi = Gauss-Seidel here)
+__device__ __forceinline__ void sweep(const StcF &S, double, const double b[3], double x[3]) {
+    double t[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        t[i] = __builtin_fma(-S.A[3 * i], x[0], b[i]);
+        t[i] = __builtin_fma(-S.A[3 * i + 1], x[1], t[i]);
+        t[i] = __builtin_fma(-S.A[3 * i + 2], x[2], t[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = __builtin_fma(S.w[i], t[i], x[i]);
+}
+
+__device__ __forceinline__ void resid(const StcF &S, double, const double x[3], const double b[3], double r[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double t = __builtin_fma(S.A[3 * i], x[0], -b[i]);
+        t = __builtin_fma(S.A[3 * i + 1], x[1], t);
+        r[i] = __builtin_fma(S.A[3 * i + 2], x[2], t);
+    }
+}
+
 // Halo words written by the smoother (update_overlaps, splitting.F90:1210-1397).
 struct HaloArgs {
     const int4 *hsub;     // per sub-element: position along faces 1, 2, 3 (0 = none)

@@ -15,11 +15,12 @@ constexpr int kMaxLevels = 12;
 constexpr int kMaxFusedLevels = 5;
 
 // Per (un_ele, level) operator record, fp64, 32 doubles = 256 B (two 128-B lines):
-// M (3x3 row-major) | Kd (3x3 row-major) | w = omega / D (3) | c = M_12 | pad.
+// M (3x3 row-major) | Kd (3x3 row-major) | w = omega / D (3) | c = M_12 |
+// A = (1/dt) M + Kd (3x3 row-major, the contracted operator of arith = 1) | pad.
 // M and Kd are get_un_ele_mass_stiff_diffvol (ShapFun_unstruc.F90:304-335) reduced as
 // transport_tri_semi.F90:592-607; D is get_diagonal (:481-486); M = c [[2,1,1],[1,2,1],[1,1,2]]
 // exactly (checked in level_stencil), which the smoother kernels use (pamg_device.h apply_A).
-constexpr int kStcM = 0, kStcK = 9, kStcW = 18, kStcC = 21, kStcStride = 32;
+constexpr int kStcM = 0, kStcK = 9, kStcW = 18, kStcC = 21, kStcA = 22, kStcStride = 32;
 
 // Level-1 geometry record per un_ele (get_splitting, Msh2Tri.F90:69-107):
 // x3, y3, v1x, v1y, v2x, v2y (v = edge / 2**i_split), pad to 8 doubles.
@@ -76,11 +77,15 @@ struct Level {
     // restrictor(l - 1) of the finer level's current residual, computed where that residual
     // is produced (fused V-cycle) and consumed as RHS by the next cycle (l >= 2)
     double *RHSN = nullptr;
+    // level 2 only: the second RHSN buffer of the concurrent fused cycle (fused = 2), whose
+    // level-1 launch writes the one the concurrent coarse launch is not reading
+    double *RHSN_alt = nullptr;
     double *stc = nullptr;            // U_local * kStcStride
     int2 *subinfo = nullptr;          // nsub: (irow, ipos) of get_str_info
     int4 *children = nullptr;         // nsub/4 (children of the next coarser level's sub-elements)
     double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
+    int arith = 0;                    // operator arithmetic of this level's kernels (pamg_params.arith)
     HaloPlan halo;
 };
 
@@ -119,6 +124,10 @@ struct pamg_handle {
     hipStream_t stream_comm = nullptr;
     hipEvent_t ev_packed = nullptr, ev_sent[2] = {nullptr, nullptr};
     bool sent_pending[2] = {false, false};
+    // fused = 2: the coarse-level launch of each cycle runs on stream_c beside the level-1
+    // launch on `stream`; ev_fine / ev_coarse order them across cycles (RHSN of level 2)
+    hipStream_t stream_c = nullptr;
+    hipEvent_t ev_fine = nullptr, ev_coarse = nullptr;
     // RHSN of every level holds the restriction of the finer level's current residual
     bool rhsn_valid = true;
     bool mesh_ready = false;
@@ -158,11 +167,13 @@ hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *t
                                  double *send = nullptr);
 // fused V-cycle (pamg_vcycle.hip); lv is the handle's 1-based level array
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth);
+// levels 2..L; the level-2 RHS is taken from rhsn2 (level 2's RHSN or RHSN_alt)
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                                int n_coarse, double rdt, double *tov, double *tovo);   // levels 2..L
-// level 1; its remote halo words packed into send1 (one of level 1's two send buffers)
+                                int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2);
+// level 1; its remote halo words packed into send1 (one of level 1's two send buffers), the
+// restriction of its residual into rhsn2
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                              int n_coarse, double rdt, double *tov, double *tovo, double *send1);
+                              int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 // FINDInv (matrix_inversion.F90:50-148) batched, n <= 8, column-major (n, n, nb)

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kBlock) void k_overlap_static(HaloArgs H, const int
 // tnew_nonlin the last one. `src` may alias T or TNN (each thread reads its
 // own words before writing them). UNIFORM: every wave lies inside one un_ele
 // (nsub >= 128), so the operator record is read through the scalar unit.
-template <bool RICHARDSON, bool UNIFORM>
+template <bool RICHARDSON, bool UNIFORM, class ST = Stc>
 __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T, double *TNN,
                                                    const double *__restrict__ RHS,
                                                    const double *__restrict__ stc, int64_t pitch,
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T,
             }
         }
     } else {
-        Stc S;
+        ST S;
         load_stc(stc + u * kStcStride, S);
         for (int it = 0; it < sweeps; ++it) {
 #pragma unroll
@@ -133,6 +133,7 @@ __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T,
 }
 
 // get_residual (:725-873): residuale = A x - RHS (note the sign, :869).
+template <class ST>
 __global__ __launch_bounds__(kBlock) void k_residual(const double *__restrict__ T, const double *__restrict__ RHS,
                                                      double *__restrict__ RES, const double *__restrict__ stc,
                                                      int64_t pitch, int64_t npairs, int nsub_log2, double rdt) {
@@ -145,15 +146,15 @@ __global__ __launch_bounds__(kBlock) void k_residual(const double *__restrict__ 
         xv[c] = ld2(T + c * pitch + s);
         bv[c] = ld2(RHS + c * pitch + s);
     }
-    Stc S;
+    ST S;
     load_stc(stc + (s >> nsub_log2) * kStcStride, S);
     const double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
-    double A0[3], A1[3];
-    apply_A(S, rdt, x0, A0);
-    apply_A(S, rdt, x1, A1);
     const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
+    double r0[3], r1[3];
+    resid(S, rdt, x0, b0, r0);
+    resid(S, rdt, x1, b1, r1);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) st2(RES + c * pitch + s, make_double2(A0[c] - b0[c], A1[c] - b1[c]));
+    for (int c = 0; c < 3; ++c) st2(RES + c * pitch + s, make_double2(r0[c], r1[c]));
 }
 
 // Level-1 right-hand side + time-step start (:316-317, :593, get_RHS :452-464):
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(kBlock) void k_restrict_tile(const double *__restri
 // restricted into RHS_{l+1}; then the new residual A tnew - RHS overwrites it.
 // ITER = tile / 512: every thread issues all its loads (old residual, tnew,
 // RHS) before the tile barrier, so the three streams are in flight together.
-template <bool UNIFORM, int ITER>
+template <bool UNIFORM, int ITER, class ST = Stc>
 __global__ __launch_bounds__(kBlock) void k_restrict_residual(const double *__restrict__ T,
                                                               const double *__restrict__ RHS, double *RES,
                                                               double *__restrict__ RHSc,
@@ -409,14 +410,15 @@ __global__ __launch_bounds__(kBlock) void k_restrict_residual(const double *__re
         const int64_t s = f0 + j;
         int64_t u = s >> nsubf_log2;
         if (UNIFORM) u = __builtin_amdgcn_readfirstlane((int)u);
-        Stc S;
+        ST S;
         load_stc(stc + u * kStcStride, S);
         const double x0[3] = {x[it][0].x, x[it][1].x, x[it][2].x}, x1[3] = {x[it][0].y, x[it][1].y, x[it][2].y};
-        double A0[3], A1[3];
-        apply_A(S, rdt, x0, A0);
-        apply_A(S, rdt, x1, A1);
+        const double b0[3] = {b[it][0].x, b[it][1].x, b[it][2].x}, b1[3] = {b[it][0].y, b[it][1].y, b[it][2].y};
+        double r0[3], r1[3];
+        resid(S, rdt, x0, b0, r0);
+        resid(S, rdt, x1, b1, r1);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) st2(RES + c * pitch_f + s, make_double2(A0[c] - b[it][c].x, A1[c] - b[it][c].y));
+        for (int c = 0; c < 3; ++c) st2(RES + c * pitch_f + s, make_double2(r0[c], r1[c]));
     }
 }
 
@@ -646,23 +648,27 @@ hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int s
     if (diag_nohalo) H.hsub = nullptr;
     const int lg = log2i(L.nsub);
     const dim3 g(grid_for(npairs)), b(kBlock);
-    if (solver == 2)
-        hipLaunchKernelGGL((k_smooth<true, false>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg,
-                           sweeps, rdt, omega, H);
-    else if (L.nsub >= 128 && !diag_nouniform)
-        hipLaunchKernelGGL((k_smooth<false, true>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg,
-                           sweeps, rdt, omega, H);
-    else
-        hipLaunchKernelGGL((k_smooth<false, false>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg,
-                           sweeps, rdt, omega, H);
+#define PAMG_SM(R, U, ST) \
+    hipLaunchKernelGGL((k_smooth<R, U, ST>), g, b, 0, s, src, L.T, L.TNN, L.RHS, L.stc, L.pitch, npairs, lg, sweeps, \
+                       rdt, omega, H)
+    const bool uni = L.nsub >= 128 && !diag_nouniform;
+    if (solver == 2) PAMG_SM(true, false, Stc);
+    else if (L.arith == 1) { if (uni) PAMG_SM(false, true, StcF); else PAMG_SM(false, false, StcF); }
+    else if (uni) PAMG_SM(false, true, Stc);
+    else PAMG_SM(false, false, Stc);
+#undef PAMG_SM
     return hipGetLastError();
 }
 
 hipError_t launch_residual(hipStream_t s, const Level &L, double rdt) {
     const int64_t npairs = L.N / 2;
     if (npairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_residual, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.RHS, L.RES, L.stc, L.pitch,
-                       npairs, log2i(L.nsub), rdt);
+    if (L.arith == 1)
+        hipLaunchKernelGGL(k_residual<StcF>, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.RHS, L.RES, L.stc,
+                           L.pitch, npairs, log2i(L.nsub), rdt);
+    else
+        hipLaunchKernelGGL(k_residual<Stc>, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.RHS, L.RES, L.stc,
+                           L.pitch, npairs, log2i(L.nsub), rdt);
     return hipGetLastError();
 }
 
@@ -692,11 +698,12 @@ hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Leve
     const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
     const size_t lds = (size_t)3 * 8 << tl;
     const int lg = log2i(fine.nsub);
-#define PAMG_RR(U, IT)                                                                                          \
-    hipLaunchKernelGGL((k_restrict_residual<U, IT>), dim3(grid), dim3(kBlock), lds, s, fine.T, fine.RHS, fine.RES, \
-                       coarse.RHS, fine.stc, fine.children, fine.pitch, coarse.pitch, fine.N, lg, rdt)
-    if (fine.nsub >= 128) PAMG_RR(true, 2);
-    else PAMG_RR(false, 2);
+#define PAMG_RR(U, IT, ST)                                                                                      \
+    hipLaunchKernelGGL((k_restrict_residual<U, IT, ST>), dim3(grid), dim3(kBlock), lds, s, fine.T, fine.RHS,       \
+                       fine.RES, coarse.RHS, fine.stc, fine.children, fine.pitch, coarse.pitch, fine.N, lg, rdt)
+    if (fine.arith == 1) { if (fine.nsub >= 128) PAMG_RR(true, 2, StcF); else PAMG_RR(false, 2, StcF); }
+    else if (fine.nsub >= 128) PAMG_RR(true, 2, Stc);
+    else PAMG_RR(false, 2, Stc);
 #undef PAMG_RR
     return hipGetLastError();
 }

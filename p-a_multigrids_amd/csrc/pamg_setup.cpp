@@ -145,6 +145,7 @@ void level_stencil(const double *X, int i_split, double k, double dt, double ome
         }
         double D = rdt * ml[i] + Kd[i][i] + 0.0;
         rec[kStcW + i] = omega / D;
+        for (int j = 0; j < 3; ++j) rec[kStcA + 3 * i + j] = rdt * M[i][j] + Kd[i][j];
     }
     rec[kStcC] = M[0][1];
 }

@@ -70,6 +70,7 @@ struct VArgs {
     int64_t U;
     int n_smooth, n_coarse;
     double rdt;
+    double *rhsn2;          // level 2's RHSN buffer: read by the coarse launch, written by the level-1 launch
     long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
 };
 
@@ -147,13 +148,15 @@ __device__ __forceinline__ void static_for(F &&f) {
 
 // operator record of un_ele u; wave-uniform records come through the scalar cache
 // (uni is a compile-time constant at every call site once the level loops are unrolled)
-__device__ __forceinline__ void stencil(bool uni, const double *__restrict__ stc, uint32_t u, Stc &S) {
+template <class ST>
+__device__ __forceinline__ void stencil(bool uni, const double *__restrict__ stc, uint32_t u, ST &S) {
     if (uni) u = __builtin_amdgcn_readfirstlane(u);
     load_stc(stc + u * (uint32_t)kStcStride, S);
 }
 
 // two sub-elements of one un_ele, interleaved
-__device__ __forceinline__ void sweeps2(const Stc &S, double rdt, int n, const double b0[3], const double b1[3],
+template <class ST>
+__device__ __forceinline__ void sweeps2(const ST &S, double rdt, int n, const double b0[3], const double b1[3],
                                         double x0[3], double x1[3], double p0[3], double p1[3]) {
     for (int it = 0; it < n; ++it) {
         copy3(p0, x0);
@@ -164,8 +167,8 @@ __device__ __forceinline__ void sweeps2(const Stc &S, double rdt, int n, const d
 }
 
 // N sub-elements of one un_ele, interleaved
-template <int N>
-__device__ __forceinline__ void sweepsN(const Stc &S, double rdt, int n, const double b[N][3], double x[N][3],
+template <int N, class ST>
+__device__ __forceinline__ void sweepsN(const ST &S, double rdt, int n, const double b[N][3], double x[N][3],
                                         double p[N][3]) {
     for (int it = 0; it < n; ++it) {
 #pragma unroll
@@ -175,12 +178,9 @@ __device__ __forceinline__ void sweepsN(const Stc &S, double rdt, int n, const d
     }
 }
 
-__device__ __forceinline__ void residual(const Stc &S, double rdt, const double p[3], const double b[3],
-                                         double r[3]) {
-    double a[3];
-    apply_A(S, rdt, p, a);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) r[c] = a[c] - b[c];
+template <class ST>
+__device__ __forceinline__ void residual(const ST &S, double rdt, const double p[3], const double b[3], double r[3]) {
+    resid(S, rdt, p, b, r);
 }
 
 // ---- halo words of one sub-element (update_overlaps, :555)
@@ -267,7 +267,7 @@ struct CGeo {
     static constexpr int total = M(C) > 0 ? M(C) : 1;
 };
 
-template <int S, int L>
+template <int S, int L, class ST>
 __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__restrict__ sp1,
                                                        const double *__restrict__ sp2, const double *__restrict__ sp3,
                                                        const double *__restrict__ sp4) {
@@ -299,14 +299,14 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     }
     // operator records, fetched once: one per level when the tile's level lies in one un_ele
     // (scalar registers), else one per chunk (vector registers when the chunk spans un_eles)
-    Stc SL[C + 1], SC[N];
+    ST SL[C + 1], SC[N];
 #pragma unroll
     for (int l = 1; l <= C; ++l)
         if (Q::one(l)) stencil(Q::uni(l), SP[l], ((uint32_t)u0 << G::lg(l)) >> G::lg(l), SL[l]);
 #pragma unroll
     for (int j = 0; j < N; ++j)
         if (!Q::one(Q::lev(j))) stencil(Q::uni(Q::lev(j)), SP[Q::lev(j)], gx[j] >> G::lg(Q::lev(j)), SC[j]);
-    auto stc_of = [&](int j, Stc &St) { St = Q::one(Q::lev(j)) ? SL[Q::lev(j)] : SC[j]; };
+    auto stc_of = [&](int j, ST &St) { St = Q::one(Q::lev(j)) ? SL[Q::lev(j)] : SC[j]; };
     // ---- prologue: tnew of every level (tnew_nonlin := tnew, :327 / :348), halo positions,
     //      and the restrictor (:336) of every level: RHS_l := RHSN_l, the restriction of the
     //      PREVIOUS cycle's residual, computed when that residual was (below, and in the
@@ -318,7 +318,8 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
         load3(A.lv[l].T(), A.lv[l].pitch, gx[j], x[j]);
     }
 #pragma unroll
-    for (int j = 0; j < N; ++j) load3(A.lv[Q::lev(j)].RHSN(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
+    for (int j = 0; j < N; ++j)
+        load3(Q::lev(j) == 1 ? A.rhsn2 : A.lv[Q::lev(j)].RHSN(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
 #pragma unroll
     for (int j = 0; j < N; ++j)
         if (ok[j]) store3(A.lv[Q::lev(j)].RHS(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     for (int it = 0; it < ns; ++it) {
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            Stc St;
+            ST St;
             stc_of(j, St);
             copy3(p[j], x[j]);
             sweep(St, rdt, b[j], x[j]);
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     for (int j = 0; j < N; ++j) {
         const int l = Q::lev(j);
         const VLevel &V = A.lv[l];
-        Stc St;
+        ST St;
         stc_of(j, St);
         double r[3];
         residual(St, rdt, p[j], b[j], r);
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     for (int it = 0; it < min(ns, nB); ++it) {
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            Stc St;
+            ST St;
             stc_of(j, St);
             copy3(p[j], x[j]);
             sweep(St, rdt, b[j], x[j]);
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
 #pragma unroll
         for (int j = 0; j < N; ++j) {
             if (Q::lev(j) < C) continue;
-            Stc St;
+            ST St;
             stc_of(j, St);
             copy3(p[j], x[j]);
             sweep(St, rdt, b[j], x[j]);
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
 // ===================================================================== level 0
 // Ownership: the adjacent pair 2t, 2t+1 of the tile (16-byte accesses, one un_ele,
 // one operator record); for the prolongator, level-1 sub-element t.
-template <int S, int L>
+template <int S, int L, class ST>
 __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0) {
     using G = Geo<S, L>;
     constexpr int C = G::C;
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     double x0[2][3], b0[2][3], p0[2][3];
     load3p(V0.T(), V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
     load3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
-    Stc St;
+    ST St;
     stencil(G::uni(0), sp0, w0, St);
     // ---- restriction leg: smoother (:331), get_residual (:338)
     sweeps2(St, rdt, ns, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
@@ -509,41 +510,47 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
                 prolong_cascade(F0, 1024, fi, y1);
             } else {
                 const double rn[3] = {M0[base + c4.z], M0[base + c4.w], M0[base + c4.x]};
-                store3(A.lv[1].RHSN(), A.lv[1].pitch, s1, rn);
+                store3(A.rhsn2, A.lv[1].pitch, s1, rn);
             }
         }
     }
     stamp<kMTf>(A, 7);
 }
 
-template <int S, int L>
-hipError_t launch_sl(hipStream_t s, const VArgs &A, unsigned grid, bool coarse) {
+template <int S, int L, class ST>
+hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, bool coarse) {
     if (coarse) {
         if constexpr (L >= 2)
-            hipLaunchKernelGGL((k_vc_coarse<S, L>), dim3(grid), dim3(kMTc), 0, s, A, A.lv[1].stc, A.lv[2].stc,
+            hipLaunchKernelGGL((k_vc_coarse<S, L, ST>), dim3(grid), dim3(kMTc), 0, s, A, A.lv[1].stc, A.lv[2].stc,
                                A.lv[3].stc, A.lv[4].stc);
         else
             return hipErrorInvalidValue;
     } else {
-        hipLaunchKernelGGL((k_vc_fine<S, L>), dim3(grid), dim3(kMTf), 0, s, A, A.lv[0].stc);
+        hipLaunchKernelGGL((k_vc_fine<S, L, ST>), dim3(grid), dim3(kMTf), 0, s, A, A.lv[0].stc);
     }
     return hipGetLastError();
 }
 
+// operator arithmetic (pamg_params.arith): the reference's order, or the contracted form
+template <int S, int L>
+hipError_t launch_sl(hipStream_t s, const VArgs &A, unsigned grid, bool coarse, int arith) {
+    return arith == 1 ? launch_slt<S, L, StcF>(s, A, grid, coarse) : launch_slt<S, L, Stc>(s, A, grid, coarse);
+}
+
 template <int S>
-hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, bool coarse) {
+hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, bool coarse, int ar) {
     switch (L) {
-        case 1: return launch_sl<S, 1>(s, A, grid, coarse);
-        case 2: if constexpr (S >= 2) return launch_sl<S, 2>(s, A, grid, coarse); break;
-        case 3: if constexpr (S >= 3) return launch_sl<S, 3>(s, A, grid, coarse); break;
-        case 4: if constexpr (S >= 4) return launch_sl<S, 4>(s, A, grid, coarse); break;
-        case 5: if constexpr (S >= 5) return launch_sl<S, 5>(s, A, grid, coarse); break;
+        case 1: return launch_sl<S, 1>(s, A, grid, coarse, ar);
+        case 2: if constexpr (S >= 2) return launch_sl<S, 2>(s, A, grid, coarse, ar); break;
+        case 3: if constexpr (S >= 3) return launch_sl<S, 3>(s, A, grid, coarse, ar); break;
+        case 4: if constexpr (S >= 4) return launch_sl<S, 4>(s, A, grid, coarse, ar); break;
+        case 5: if constexpr (S >= 5) return launch_sl<S, 5>(s, A, grid, coarse, ar); break;
     }
     return hipErrorInvalidValue;
 }
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
-                       double rdt, double *tov, double *tovo, double *send1, bool coarse) {
+                       double rdt, double *tov, double *tovo, double *send1, double *rhsn2, bool coarse) {
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
     VArgs A{};
     for (int l = 0; l < L; ++l) {
@@ -552,8 +559,9 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
         if ((uint64_t)V.pitch * 3 >= (1ull << 29)) return hipErrorInvalidValue;   // 32-bit byte offsets
         VLevel &o = A.lv[l];
         if (V.TNN != V.T + 3 * V.pitch || V.RHS != V.T + 6 * V.pitch || V.RES != V.T + 9 * V.pitch ||
-            V.RHSN != V.T + 15 * V.pitch)
+            (l != 1 && V.RHSN != V.T + 15 * V.pitch))
             return hipErrorInvalidValue;
+        if (l == 1 && rhsn2 != V.T + 15 * V.pitch && (!V.RHSN_alt || rhsn2 != V.RHSN_alt)) return hipErrorInvalidValue;
         o.base = V.T; o.stc = V.stc;
         o.children = (l > 0) ? lv[l].children : nullptr;   // children of level l+1 in level l
         o.pitch = V.pitch;
@@ -565,6 +573,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.n_smooth = n_smooth;
     A.n_coarse = n_coarse;
     A.rdt = rdt;
+    A.rhsn2 = rhsn2;
     // tile: 1024 level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
     const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : 10 - 2 * n_split;
     const unsigned grid = (unsigned)(((int64_t)U + (1 << GL) - 1) >> GL);
@@ -581,11 +590,11 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     }
     hipError_t e = hipErrorInvalidValue;
     switch (n_split) {
-        case 1: e = launch_s<1>(s, A, grid, L, coarse); break;
-        case 2: e = launch_s<2>(s, A, grid, L, coarse); break;
-        case 3: e = launch_s<3>(s, A, grid, L, coarse); break;
-        case 4: e = launch_s<4>(s, A, grid, L, coarse); break;
-        case 5: e = launch_s<5>(s, A, grid, L, coarse); break;
+        case 1: e = launch_s<1>(s, A, grid, L, coarse, lv[1].arith); break;
+        case 2: e = launch_s<2>(s, A, grid, L, coarse, lv[1].arith); break;
+        case 3: e = launch_s<3>(s, A, grid, L, coarse, lv[1].arith); break;
+        case 4: e = launch_s<4>(s, A, grid, L, coarse, lv[1].arith); break;
+        case 5: e = launch_s<5>(s, A, grid, L, coarse, lv[1].arith); break;
     }
     if (stamp_path) {
         std::vector<long long> hst(nst);
@@ -611,14 +620,16 @@ bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mo
 }
 
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                                int n_coarse, double rdt, double *tov, double *tovo) {
+                                int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2) {
     if (L < 2) return hipSuccess;
-    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, nullptr, true);
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, nullptr, const_cast<double *>(rhsn2),
+                       true);
 }
 
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                              int n_coarse, double rdt, double *tov, double *tovo, double *send1) {
-    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, false);
+                              int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2) {
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, L > 1 ? rhsn2 : nullptr,
+                       false);
 }
 
 }  // namespace pamg

@@ -28,7 +28,8 @@ class PamgParams(C.Structure):
     _fields_ = [("n_split", C.c_int), ("multi_levels", C.c_int), ("n_smooth", C.c_int),
                 ("n_coarse", C.c_int), ("solver", C.c_int), ("device", C.c_int),
                 ("dt", C.c_double), ("k", C.c_double), ("omega", C.c_double), ("theta", C.c_double),
-                ("halo_mode", C.c_int), ("fused", C.c_int), ("coarse_solver", C.c_int), ("reserved", C.c_int * 5)]
+                ("halo_mode", C.c_int), ("fused", C.c_int), ("coarse_solver", C.c_int), ("arith", C.c_int),
+                ("reserved", C.c_int * 4)]
 
 
 class PamgError(RuntimeError):
