@@ -10,6 +10,15 @@ omega = 0.8). One step = one V-cycle of transport_tri_semi.F90:319-379
 (restriction leg, 15 coarse smoother calls, prolongation leg, halo after
 every smoother call) over the whole mesh.
 
+Defaults: the pipelined fused schedule (fused = 3: a call of K cycles is one
+coarse-level launch, K - 1 launches of [level 1 of cycle c + levels 2..L of
+cycle c+1] and one level-1 launch; state identical to the per-step kernel
+sequence, bit for bit) and the contracted operator arithmetic (arith = 1: fma
+rows of A_e = M/dt + Kd; ~1e-15 relative to the reference on the solution, the
+north star's bar being 1e-10). The other schedules and the reference's own
+operation order (arith = 0, bitwise equal to the reference) are timed on the
+same workload and reported under "extra".
+
 N > 1 (python -m torch.distributed.run ... bench.py --gpus N): strong scaling
 of the same mesh, x-strip domain decomposition by unstructured element, one
 process per GPU, halo exchanged with RCCL (grouped ncclSend/ncclRecv over
@@ -49,7 +58,10 @@ def parse():
     ap.add_argument("--arith", type=int, default=1,
                     help="1: contracted operator arithmetic (fma rows of A_e = M/dt + Kd; ~1e-15 of the reference, "
                          "the north star's bar is 1e-10); 0: the reference's operation order (bitwise)")
-    ap.add_argument("--fused", type=int, default=1, help="1: two fused launches per V-cycle (default); 2: the same, concurrent on two streams; 0: per-step kernels")
+    ap.add_argument("--fused", type=int, default=3,
+                    help="3: pipelined fused launches, level 1 of cycle c + coarse levels of cycle c+1 in one "
+                         "launch (default); 1: two fused launches per V-cycle; 2: the same, concurrent on two "
+                         "streams; 0: per-step kernels")
     return ap.parse_args()
 
 
@@ -97,7 +109,9 @@ def pmc_traffic(kernel, nsplit, levels):
     return None
 
 
-RK_DESC = {"vcycle": "k_vc_fine (fused V-cycle, level-1 launch: both smoother calls, residual, prolongator; "
+RK_DESC = {"vcycle_pipe": "k_vc_fine<.., true> (pipelined fused V-cycle: level 1 of cycle c -- both smoother "
+                          "calls, residual, restrictor, prolongator -- and levels 2..L of cycle c+1, per tile)",
+           "vcycle": "k_vc_fine (fused V-cycle, level-1 launch: both smoother calls, residual, prolongator; "
                      "the coarse levels run in k_vc_coarse just before it)",
            "smooth_L1": "k_smooth (level-1 smoother call, n_smooth sweeps fused)"}
 
@@ -134,7 +148,7 @@ def main():
     # each rank's share of a cycle is ~1/N as long and the events would be a visible part of
     # it, so there they are recorded in a short pass after the timed region
     live_events = world == 1
-    s.timing_enable(0x37F if live_events else 0)  # every class but sweep_bench
+    s.timing_enable(0x77F if live_events else 0)  # every class but sweep_bench
     s.timing_reset()
 
     def barrier():
@@ -156,7 +170,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if not live_events:
-        s.timing_enable(0x37F)
+        s.timing_enable(0x77F)
         s.timing_reset()
         s.vcycle(max(1, min(a.steps, 20)))
         s.synchronize()
@@ -165,7 +179,7 @@ def main():
     # dominant kernel by total time inside the timed region
     dom = max((k for k in tm if tm[k]["launches"] > 0 and k != "sweep_bench"), key=lambda k: tm[k]["ms"])
     # roofline kernel: the fused V-cycle when it ran, else the level-1 smoother
-    rk = "vcycle" if tm["vcycle"]["launches"] else "smooth_L1"
+    rk = next(k for k in ("vcycle_pipe", "vcycle", "smooth_L1") if tm[k]["launches"])
     kinfo = tm[rk]
     ms_per_launch = kinfo["ms"] / max(1, kinfo["launches"])
     bytes_per_launch = kinfo["bytes"] / max(1, kinfo["launches"])
@@ -189,8 +203,9 @@ def main():
         # the same workload in the other schedules / arithmetic: the per-step kernel sequence
         # (bitwise equal to the fused cycle), the concurrent fused launches, and the reference's
         # operation order (bitwise equal to the reference)
-        for tag, kw in (("fused0", dict(fused=0, arith=a.arith)), ("fused2", dict(fused=2, arith=a.arith)),
-                        ("arith0", dict(fused=1, arith=0)), ("arith1", dict(fused=1, arith=1))):
+        for tag, kw in (("fused0", dict(fused=0, arith=a.arith)), ("fused1", dict(fused=1, arith=a.arith)),
+                        ("fused2", dict(fused=2, arith=a.arith)), ("fused3", dict(fused=3, arith=a.arith)),
+                        ("arith0", dict(fused=a.fused, arith=0)), ("arith1", dict(fused=a.fused, arith=1))):
             if kw["fused"] == a.fused and kw["arith"] == a.arith:
                 continue
             su = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,

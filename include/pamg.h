@@ -57,7 +57,8 @@ extern "C" {
 #define PAMG_K_SWEEP_BENCH 7
 #define PAMG_K_VCYCLE 8          /* fused V-cycle, level-1 launch */
 #define PAMG_K_VCYCLE_COARSE 9   /* fused V-cycle, levels 2..L launch */
-#define PAMG_K_COUNT 10
+#define PAMG_K_VCYCLE_PIPE 10    /* pipelined fused V-cycle: level 1 of cycle c + levels 2..L of cycle c+1 */
+#define PAMG_K_COUNT 11
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;
@@ -75,11 +76,13 @@ typedef struct {
     double theta;     /* time weighting, :117 (only 1.0 is accepted) */
     int halo_mode;    /* 0: halo written once per smoother call (state-identical),
                          1: one launch per sweep, halo at every sweep (reference timing) */
-    int fused;        /* 1: pamg_vcycle runs each V-cycle as two fused launches when supported
+    int fused;        /* default 3. 1: pamg_vcycle runs each V-cycle as two fused launches when supported
                          (solver 1/3, halo_mode 0, n_split <= 5, coarse_solver 0); 0: one kernel
                          per step; 2: the two fused launches of a cycle run concurrently on two
                          streams (the coarse levels' fp64 work under level 1's HBM stream;
-                         state identical to 1) */
+                         state identical to 1); 3: pipelined -- one launch per cycle
+                         runs level 1 of cycle c and the coarse levels of cycle c+1 tile by tile
+                         (level 2's RHS stays in LDS; state identical to 1) */
     int coarse_solver; /* 0: the reference's n_coarse smoother calls on the coarsest level (:351-353);
                           1: its exact local solve instead, tnew = tnew_nonlin = A_e^-1 RHS with
                           A_e = (1/dt) M + Kd inverted by FINDInv (matrix_inversion.F90:50-148) --

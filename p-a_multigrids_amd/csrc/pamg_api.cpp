@@ -297,6 +297,11 @@ double vcycle_coarse_bytes(pamg_handle *h) {
     for (int l = 2; l <= L; ++l) b += (120.0 + (l >= 3 ? 24.0 : 0.0)) * h->lv[l].N;
     return b + 104.0 * h->U * (L - 1);
 }
+//   pipelined launch: both, less level 2's RHSN (written and read: 48 B) and its tnew read
+//                     by the coarse part (the level-1 part's read serves both: 24 B)
+double vcycle_pipe_bytes(pamg_handle *h) {
+    return vcycle_fine_bytes(h) + vcycle_coarse_bytes(h) - 72.0 * h->lv[2].N;
+}
 
 // the exact local solve of level l (coarse_solver = 1): tnew = tnew_nonlin = A_e^-1 RHS, with
 // A_e^-1 from FINDInv, formed on first use
@@ -364,9 +369,18 @@ int vcycle_fused(pamg_handle *h, int n) {
     // reads level 2's tnew, which coarse(c) may be rewriting: its result is dead (:550,
     // SURVEY.md A3 iv) and never stored, so no state depends on the order.
     const bool conc = h->p.fused == 2 && L > 1;
+    // fused = 3: coarse(1), then [level 1 (c) + coarse levels (c+1)] for c < n, then level 1 (n)
+    // (pamg_vcycle.hip, "pipelined tail"): nothing outside the call sees the coarse levels
+    // one cycle ahead, and the last launch brings level 1 (and level 2's RHSN) level with them
+    const bool pipe = h->p.fused == 3 && L > 1;
     Level &L2 = h->lv[2];
     if (conc) {
         HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));   // everything issued before this call
+    }
+    if (pipe && n > 0) {
+        Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h));
+        HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
+                                       h->tovo, L2.RHSN));
     }
     for (int c = 0; c < n; ++c) {
         const int buf = two ? 1 - P1.send_cur : 0;
@@ -379,7 +393,7 @@ int vcycle_fused(pamg_handle *h, int n) {
             HIPCHK(h, hipStreamWaitEvent(h->stream_c, h->ev_fine, 0));
             if (c > 0) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));
         }
-        if (L > 1) {   // levels 2..L first: the prolongator of level 1 reads their final tnew
+        if (L > 1 && !pipe) {   // levels 2..L first: the prolongator of level 1 reads their final tnew
             const hipStream_t sc = conc ? h->stream_c : h->stream;
             Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h), sc);
             HIPCHK(h, launch_vcycle_coarse(sc, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
@@ -387,9 +401,10 @@ int vcycle_fused(pamg_handle *h, int n) {
             if (conc) HIPCHK(h, hipEventRecord(h->ev_coarse, h->stream_c));
         }
         {
-            Span sp(h, PAMG_K_VCYCLE, vcycle_fine_bytes(h));
+            const bool pc = pipe && c + 1 < n;   // also the coarse levels of cycle c + 1
+            Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE, pc ? vcycle_pipe_bytes(h) : vcycle_fine_bytes(h));
             HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr));
+                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr, pc));
             if (conc) HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));
         }
         if (L > 1) L2.RHSN = rhsn_w;   // the next cycle's level-2 RHS
@@ -436,7 +451,7 @@ void pamg_default_params(pamg_params *p) {
     p->omega = 0.8;          // :140
     p->theta = 1.;           // :117
     p->halo_mode = 0;
-    p->fused = 1;
+    p->fused = 3;
 }
 
 int pamg_create(const pamg_params *p, pamg_handle **out) {
@@ -445,7 +460,7 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
     if (p->multi_levels < 1 || p->multi_levels > p->n_split || p->n_split > kMaxLevels || p->n_split < 1 ||
         p->n_smooth < 0 || p->n_coarse < 0 || (p->solver < 1 || p->solver > 3) || !(p->dt > 0) ||
         p->theta != 1.0 || (p->halo_mode != 0 && p->halo_mode != 1) ||
-        (p->coarse_solver != 0 && p->coarse_solver != 1) || p->fused < 0 || p->fused > 2 ||
+        (p->coarse_solver != 0 && p->coarse_solver != 1) || p->fused < 0 || p->fused > 3 ||
         (p->arith != 0 && p->arith != 1))
         return PAMG_ERR_ARG;
     int ndev = 0;

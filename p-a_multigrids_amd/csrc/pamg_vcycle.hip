@@ -424,15 +424,131 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     stamp<kMTc>(A, 7);
 }
 
+// ===================================================================== pipelined tail
+// The coarse levels of the NEXT cycle, for the same tile, at the end of the level-1 launch
+// (PIPE). The coarse-level work of cycle c+1 depends on cycle c only through level 2's RHS
+// (the restrictor of cycle c's level-1 residual, :336) and on the coarse levels' own state,
+// so the launch that finishes level 1 of cycle c can run the coarse levels of cycle c+1:
+// level 2's RHS stays in the registers of the thread that restricts it and then smooths
+// that sub-element, and level 2's tnew, read once, serves both the prolongator of cycle c
+// (:370, its final value) and the start of cycle c+1 (:348). A call
+// of n cycles is launched as coarse(1), [level 1 (c) + coarse (c+1)] for c < n, level 1 (n).
+// Thread -> coarse element: level 2 on threads 0..255 (the owners of y1), level l >= 3 on
+// the wave 4 + (l - 3), so a wave holds one level; the phases are the coarse launch's:
+//   A: RHS_l := restrictor (:336), the restriction-leg call (:331), get_residual (:338);
+//   B: restrictor of the new residuals into RHSN (next cycle), the prolongation-leg call
+//      (:376) or, on the coarsest level, the 1 + n_coarse calls (:351-353), tnew stored;
+//      then the prolongator cascade into the next finer level's image (:370; dead, :550).
+template <int S, int L>
+struct PGeo {
+    using G = Geo<S, L>;
+    static constexpr int C = G::C;
+    static constexpr int nt(int l) { return G::nt(l); }
+    static constexpr int T0(int l) { return l == 1 ? 0 : 256 + 64 * (l - 2); }
+    static constexpr int NTH(int l) { return l == 1 ? 256 : 64; }
+    // LDS images in the F0 | M0 region: F_l, M_l (1 <= l < C)
+    static constexpr int F(int l) { int o = 0; for (int i = 1; i < l; ++i) o += 3 * nt(i); return o; }
+    static constexpr int M(int l) { int o = F(C); for (int i = 1; i < l; ++i) o += nt(i); return o; }
+    static_assert(M(C) <= 4 * 1024, "coarse images exceed the level-1 image region");
+};
+
+template <int S, int L, class ST>
+__device__ __forceinline__ void coarse_next(const VArgs &A, const double *__restrict__ const *SP, int t, int64_t u0, int nue,
+                                            const double y1[3], const double rn1[3], double *lds) {
+    using G = Geo<S, L>;
+    using P = PGeo<S, L>;
+    constexpr int C = G::C;
+    const double rdt = A.rdt;
+    const int ns = A.n_smooth;
+    double x[3], b[3], p[3];
+    ST St;
+    bool v = false;
+    uint32_t gx = 0;
+    int i = 0;
+    int4 c4 = make_int4(0, 0, 0, 0);
+    __syncthreads();   // the level-1 images are dead
+    // ---- phase A
+    static_for<1, C + 1>([&](auto lc) {
+        constexpr int l = decltype(lc)::value;
+        if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l)) return;   // wave-uniform
+        const VLevel &V = A.lv[l];
+        i = t - P::T0(l);
+        v = i < P::nt(l) && i < (nue << G::lg(l));
+        gx = ((uint32_t)u0 << G::lg(l)) + (uint32_t)(v ? i : 0);
+        if constexpr (l == 1) {
+            copy3(x, y1);   // final tnew of the previous cycle (:348 tnew_nonlin := tnew)
+            copy3(b, rn1);  // the restriction of level 1's residual (:336)
+        } else {
+            load3(V.T(), V.pitch, gx, x);
+            load3(V.RHSN(), V.pitch, gx, b);
+        }
+        if (v) store3(V.RHS(), V.pitch, gx, b);
+        stencil(G::uni(l), SP[l], gx >> G::lg(l), St);
+        if constexpr (l >= 2) c4 = V.children[gx & ((1 << G::lg(l)) - 1)];
+        for (int it = 0; it < ns; ++it) {
+            copy3(p, x);
+            sweep(St, rdt, b, x);
+        }
+        double r[3];
+        residual(St, rdt, p, b, r);
+        if (v) store3(V.RES(), V.pitch, gx, r);
+        if constexpr (l < C) {
+            if (v) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) lds[P::F(l) + c * P::nt(l) + i] = p[c];
+                lds[P::M(l) + i] = (r[0] + r[1] + r[2]) / 3.;
+            }
+        }
+        copy3(x, p);   // tnew_nonlin := tnew (:348 coarsest, :367 the others)
+    });
+    __syncthreads();
+    // ---- phase B
+    static_for<1, C + 1>([&](auto lc) {
+        constexpr int l = decltype(lc)::value;
+        if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l)) return;
+        const VLevel &V = A.lv[l];
+        const int base = (i >> G::lg(l)) << G::lg(l - 1);
+        if constexpr (l >= 2) {   // restrictor of the next cycle (splitting.F90:10-32, 146-151)
+            if (v) {
+                const double rn[3] = {lds[P::M(l - 1) + base + c4.z], lds[P::M(l - 1) + base + c4.w],
+                                      lds[P::M(l - 1) + base + c4.x]};
+                store3(V.RHSN(), V.pitch, gx, rn);
+            }
+        }
+        const int nB = l == C ? ns * A.n_coarse : ns;
+        for (int it = 0; it < nB; ++it) {
+            copy3(p, x);
+            sweep(St, rdt, b, x);
+        }
+        if (v) {
+            store3(V.T(), V.pitch, gx, p);
+            // ---- prolongator into level l - 1 (:370; result dead, :550) by the owner of the
+            //      coarse sub-element, from its final tnew, on the restriction-leg image of
+            //      level l - 1 (complete since the phase-A barrier; each child has one parent)
+            if constexpr (l >= 2) {
+                const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+                prolong_cascade(lds + P::F(l - 1), P::nt(l - 1), fi, p);
+            }
+        }
+    });
+}
+
 // ===================================================================== level 0
 // Ownership: the adjacent pair 2t, 2t+1 of the tile (16-byte accesses, one un_ele,
 // one operator record); for the prolongator, level-1 sub-element t.
-template <int S, int L, class ST>
-__global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0) {
+template <int S, int L, class ST, bool PIPE>
+__global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0,
+                                                                      const double *__restrict__ sp1,
+                                                                      const double *__restrict__ sp2,
+                                                                      const double *__restrict__ sp3,
+                                                                      const double *__restrict__ sp4) {
     using G = Geo<S, L>;
     constexpr int C = G::C;
-    __shared__ __attribute__((aligned(16))) double F0[C > 0 ? 3 * 1024 : 1];   // restriction-leg tnew image
-    __shared__ __attribute__((aligned(16))) double M0[C > 0 ? 1024 : 1];       // residual means (restrictor input)
+    static_assert(!PIPE || C > 0, "the pipelined launch needs a coarse level");
+    // F0 | M0: restriction-leg tnew image and residual means (restrictor input) of level 1;
+    // the pipelined tail reuses the region for the coarse levels' images
+    __shared__ __attribute__((aligned(16))) double F0[C > 0 ? 4 * 1024 : 1];
+    double *const M0 = F0 + 3 * 1024;
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
@@ -501,6 +617,9 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     stamp<kMTf>(A, 4);
     // ---- prolongator (:370) on the LDS image (its result is dead, :550), and the restrictor
     //      of the next cycle (:336) from this cycle's residual (splitting.F90:10-32)
+    //      (PIPE: both on the owner of level-2 sub-element t, which keeps the restriction as
+    //      its RHS for the next cycle's coarse levels)
+    double rn[3] = {0.0, 0.0, 0.0};
     if constexpr (C > 0) {
         __syncthreads();
         if (v1) {
@@ -508,49 +627,66 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
             if (casc) {
                 const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
                 prolong_cascade(F0, 1024, fi, y1);
-            } else {
-                const double rn[3] = {M0[base + c4.z], M0[base + c4.w], M0[base + c4.x]};
-                store3(A.rhsn2, A.lv[1].pitch, s1, rn);
+            }
+            if (PIPE ? casc : !casc) {
+                rn[0] = M0[base + c4.z];
+                rn[1] = M0[base + c4.w];
+                rn[2] = M0[base + c4.x];
+                if constexpr (!PIPE) store3(A.rhsn2, A.lv[1].pitch, s1, rn);
             }
         }
+    }
+    if constexpr (PIPE) {
+        const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
+        coarse_next<S, L, ST>(A, SP, t, u0, nue, y1, rn, F0);
     }
     stamp<kMTf>(A, 7);
 }
 
+// part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
 template <int S, int L, class ST>
-hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, bool coarse) {
-    if (coarse) {
+hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
+    if (part == 1) {
         if constexpr (L >= 2)
             hipLaunchKernelGGL((k_vc_coarse<S, L, ST>), dim3(grid), dim3(kMTc), 0, s, A, A.lv[1].stc, A.lv[2].stc,
                                A.lv[3].stc, A.lv[4].stc);
         else
             return hipErrorInvalidValue;
+    } else if (part == 2) {
+        if constexpr (L >= 2)
+            hipLaunchKernelGGL((k_vc_fine<S, L, ST, true>), dim3(grid), dim3(kMTf), 0, s, A, A.lv[0].stc,
+                               A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+        else
+            return hipErrorInvalidValue;
     } else {
-        hipLaunchKernelGGL((k_vc_fine<S, L, ST>), dim3(grid), dim3(kMTf), 0, s, A, A.lv[0].stc);
+        hipLaunchKernelGGL((k_vc_fine<S, L, ST, false>), dim3(grid), dim3(kMTf), 0, s, A, A.lv[0].stc, nullptr,
+                           nullptr, nullptr, nullptr);
     }
     return hipGetLastError();
 }
 
 // operator arithmetic (pamg_params.arith): the reference's order, or the contracted form
 template <int S, int L>
-hipError_t launch_sl(hipStream_t s, const VArgs &A, unsigned grid, bool coarse, int arith) {
-    return arith == 1 ? launch_slt<S, L, StcF>(s, A, grid, coarse) : launch_slt<S, L, Stc>(s, A, grid, coarse);
+hipError_t launch_sl(hipStream_t s, const VArgs &A, unsigned grid, int part, int arith) {
+    return arith == 1 ? launch_slt<S, L, StcF>(s, A, grid, part) : launch_slt<S, L, Stc>(s, A, grid, part);
 }
 
 template <int S>
-hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, bool coarse, int ar) {
+hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, int part, int ar) {
     switch (L) {
-        case 1: return launch_sl<S, 1>(s, A, grid, coarse, ar);
-        case 2: if constexpr (S >= 2) return launch_sl<S, 2>(s, A, grid, coarse, ar); break;
-        case 3: if constexpr (S >= 3) return launch_sl<S, 3>(s, A, grid, coarse, ar); break;
-        case 4: if constexpr (S >= 4) return launch_sl<S, 4>(s, A, grid, coarse, ar); break;
-        case 5: if constexpr (S >= 5) return launch_sl<S, 5>(s, A, grid, coarse, ar); break;
+        case 1: return launch_sl<S, 1>(s, A, grid, part, ar);
+        case 2: if constexpr (S >= 2) return launch_sl<S, 2>(s, A, grid, part, ar); break;
+        case 3: if constexpr (S >= 3) return launch_sl<S, 3>(s, A, grid, part, ar); break;
+        case 4: if constexpr (S >= 4) return launch_sl<S, 4>(s, A, grid, part, ar); break;
+        case 5: if constexpr (S >= 5) return launch_sl<S, 5>(s, A, grid, part, ar); break;
     }
     return hipErrorInvalidValue;
 }
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
-                       double rdt, double *tov, double *tovo, double *send1, double *rhsn2, bool coarse) {
+                       double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part) {
+    const bool coarse = part == 1;
+    if (part == 2 && L < 2) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
     VArgs A{};
     for (int l = 0; l < L; ++l) {
@@ -590,11 +726,11 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     }
     hipError_t e = hipErrorInvalidValue;
     switch (n_split) {
-        case 1: e = launch_s<1>(s, A, grid, L, coarse, lv[1].arith); break;
-        case 2: e = launch_s<2>(s, A, grid, L, coarse, lv[1].arith); break;
-        case 3: e = launch_s<3>(s, A, grid, L, coarse, lv[1].arith); break;
-        case 4: e = launch_s<4>(s, A, grid, L, coarse, lv[1].arith); break;
-        case 5: e = launch_s<5>(s, A, grid, L, coarse, lv[1].arith); break;
+        case 1: e = launch_s<1>(s, A, grid, L, part, lv[1].arith); break;
+        case 2: e = launch_s<2>(s, A, grid, L, part, lv[1].arith); break;
+        case 3: e = launch_s<3>(s, A, grid, L, part, lv[1].arith); break;
+        case 4: e = launch_s<4>(s, A, grid, L, part, lv[1].arith); break;
+        case 5: e = launch_s<5>(s, A, grid, L, part, lv[1].arith); break;
     }
     if (stamp_path) {
         std::vector<long long> hst(nst);
@@ -623,13 +759,14 @@ hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, in
                                 int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2) {
     if (L < 2) return hipSuccess;
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, nullptr, const_cast<double *>(rhsn2),
-                       true);
+                       1);
 }
 
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                              int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2) {
+                              int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
+                              bool pipe) {
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, L > 1 ? rhsn2 : nullptr,
-                       false);
+                       pipe ? 2 : 0);
 }
 
 }  // namespace pamg

@@ -87,7 +87,7 @@ class SemiImplicitIterative:
     """Device-resident multigrid state for one mesh (one GPU / rank)."""
 
     def __init__(self, mesh, n_split, multi_levels, n_smooth=4, solver=3, n_coarse=15, device=0,
-                 dt=1.0 * 0.0000125, k=1.0, omega=0.8, halo_mode=0, comm=None, fused=1, coarse_solver=0,
+                 dt=1.0 * 0.0000125, k=1.0, omega=0.8, halo_mode=0, comm=None, fused=3, coarse_solver=0,
                  arith=0):
         self.L = lib()
         self.mesh = mesh

@@ -15,7 +15,7 @@ mesh = pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "untitled8192.msh"))
 cases = [tuple(int(x) for x in c.split(",")) for c in (sys.argv[1:] or ["5,3,4", "3,3,4"])]
 for S, L, ns in cases:
     for rep in range(1):
-        for fused, arith in ((1, 0), (2, 0), (1, 1), (2, 1)):
+        for fused, arith in ((1, 0), (3, 0), (1, 1), (2, 1), (3, 1)):
             s = pamg.SemiImplicitIterative(mesh, S, L, n_smooth=ns, solver=3, fused=fused, arith=arith)
             s.begin_timestep()
             s.vcycle(5)
@@ -25,7 +25,7 @@ for S, L, ns in cases:
             s.vcycle(n)
             s.synchronize()
             wall = (time.perf_counter() - t0) / n * 1e3
-            s.timing_enable(0x37F)
+            s.timing_enable(0x77F)
             s.timing_reset()
             t0 = time.perf_counter()
             s.vcycle(n)

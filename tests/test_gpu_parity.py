@@ -196,8 +196,8 @@ def test_timing_counts_launches():
 
 def test_fused_vcycle_counts_one_launch_per_cycle():
     meta, _ = goldens.load("u8_s3_l3_gs")
-    s = gpu_solver(meta)
-    s.timing_enable(0x3FF)
+    s = gpu_solver(meta, fused=1)
+    s.timing_enable(0x7FF)
     s.timing_reset()
     s.run(2, 3)
     t = s.timing()
@@ -206,18 +206,31 @@ def test_fused_vcycle_counts_one_launch_per_cycle():
     assert t["rhs"]["launches"] == 2
 
 
+def test_pipelined_vcycle_launches():
+    """fused = 3: a call of n cycles is coarse(1), n - 1 pipelined launches, level 1 (n)."""
+    meta, _ = goldens.load("u8_s3_l3_gs")
+    s = gpu_solver(meta, fused=3)
+    s.timing_enable(0x7FF)
+    s.timing_reset()
+    s.run(2, 3)
+    t = s.timing()
+    assert t["vcycle_coarse"]["launches"] == 2 and t["vcycle_pipe"]["launches"] == 4
+    assert t["vcycle"]["launches"] == 2 and t["smooth_L1"]["launches"] == 0
+
+
 @pytest.mark.parametrize("mesh,S,L,solver,ns", [
     ("untitled8.msh", 1, 1, 3, 1), ("untitled8.msh", 2, 2, 3, 2), ("untitled8.msh", 3, 3, 1, 1),
     ("irregular.msh", 3, 3, 3, 1), ("900_ele.msh", 2, 2, 3, 3), ("900_ele.msh", 4, 4, 1, 1),
     ("untitled2048.msh", 5, 5, 3, 1), ("untitled8192.msh", 5, 3, 3, 4), ("test_sn2.msh", 4, 2, 3, 2)])
-@pytest.mark.parametrize("fused", [1, 2])
+@pytest.mark.parametrize("fused", [1, 2, 3])
 def test_fused_vcycle_equals_kernel_sequence_bitwise(mesh, S, L, solver, ns, fused):
     """The one-launch V-cycle (pamg_vcycle.hip) computes the same operations in
     the same order as the per-step kernels: every field of every level and the
     halo arrays agree bit for bit, including partial tiles (U not a multiple of
     the tile's element count) and meshes with boundary faces. fused = 2 runs the
     coarse-level and level-1 launches of a cycle concurrently (double-buffered
-    level-2 RHSN across three consecutive cycles)."""
+    level-2 RHSN across three consecutive cycles); fused = 3 pipelines them (level 1 of
+    cycle c with the coarse levels of cycle c + 1 in one launch)."""
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
     a = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, fused=fused)
     b = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, fused=0)
@@ -231,7 +244,7 @@ def test_fused_vcycle_equals_kernel_sequence_bitwise(mesh, S, L, solver, ns, fus
 
 
 @pytest.mark.parametrize("mesh,S,L", [("irregular.msh", 4, 3), ("untitled2048.msh", 5, 3), ("900_ele.msh", 3, 2)])
-@pytest.mark.parametrize("fused", [1, 2])
+@pytest.mark.parametrize("fused", [1, 2, 3])
 def test_fused_vcycle_interleaved_with_call_sites_bitwise(mesh, S, L, fused):
     """Fused V-cycles mixed with the per-call entry points and state uploads: the fused path's
     cached restriction (RHSN) and once-per-step halo words must follow every other writer."""
@@ -310,7 +323,7 @@ def test_contracted_time_loop_matches_reference(name):
     def err_of(k, v):
         return goldens.rel_err(v, d[k]) if k in d else goldens.compare_sampled(d, k, v)
 
-    for fused in (0, 1, 2):
+    for fused in (0, 1, 2, 3):
         s = gpu_solver(meta, arith=1, fused=fused)
         s.run(meta["ntime"], meta["n_multigrid"])
         st = s.state()
@@ -320,9 +333,9 @@ def test_contracted_time_loop_matches_reference(name):
 
 @pytest.mark.parametrize("mesh,S,L", [("untitled8192.msh", 5, 3), ("irregular.msh", 6, 3), ("900_ele.msh", 3, 3)])
 def test_contracted_full_size_against_oracle(mesh, S, L):
-    """BASELINE sizes, one time step of two V-cycles, the concurrent fused schedule."""
+    """BASELINE sizes, one time step of two V-cycles, the pipelined fused schedule."""
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
-    s = pamg.SemiImplicitIterative(m, S, L, arith=1, fused=2)
+    s = pamg.SemiImplicitIterative(m, S, L, arith=1, fused=3)
     s.run(1, 2)
     om = O.read_msh(os.path.join(goldens.MESHES, mesh))
     o = O.Oracle(om, S, L, ntime=1, n_multigrid=2)
@@ -335,7 +348,7 @@ def test_contracted_full_size_against_oracle(mesh, S, L):
 
 @pytest.mark.parametrize("mesh,S,L,ns", [("untitled8.msh", 3, 3, 1), ("irregular.msh", 3, 3, 4),
                                          ("900_ele.msh", 4, 4, 2), ("untitled2048.msh", 5, 5, 3)])
-@pytest.mark.parametrize("fused", [1, 2])
+@pytest.mark.parametrize("fused", [1, 2, 3])
 def test_contracted_fused_equals_kernel_sequence_bitwise(mesh, S, L, ns, fused):
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
     a = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, arith=1, fused=fused)
