@@ -107,6 +107,8 @@ struct Geo {
 };
 
 // field access: wave-uniform plane base (SGPRs) + 32-bit sub-element index (one VGPR for all planes)
+// 8-byte accesses stay plain: non-temporal 8-B lanes measured 15 % slower on the pipelined
+// launch (their lines are not merged in L1)
 __device__ __forceinline__ void load3(const double *f, int64_t pitch, uint32_t s, double v[3]) {
     const uint32_t o = s << 3;
 #pragma unroll
@@ -118,11 +120,14 @@ __device__ __forceinline__ void store3(double *f, int64_t pitch, uint32_t s, con
     for (int c = 0; c < 3; ++c) *reinterpret_cast<double *>(reinterpret_cast<char *>(f + c * pitch) + o) = v[c];
 }
 // the adjacent pair s, s+1 (s even) with 16-byte accesses
+// streamed with non-temporal 16-byte loads and stores (pamg_device.h PAMG_NT)
+typedef double v2d __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void load3p(const double *f, int64_t pitch, uint32_t s, double a[3], double b[3]) {
     const uint32_t o = s << 3;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const double2 v = *reinterpret_cast<const double2 *>(reinterpret_cast<const char *>(f + c * pitch) + o);
+        const v2d *q = reinterpret_cast<const v2d *>(reinterpret_cast<const char *>(f + c * pitch) + o);
+        const v2d v = PAMG_NT ? __builtin_nontemporal_load(q) : *q;
         a[c] = v.x;
         b[c] = v.y;
     }
@@ -130,8 +135,12 @@ __device__ __forceinline__ void load3p(const double *f, int64_t pitch, uint32_t 
 __device__ __forceinline__ void store3p(double *f, int64_t pitch, uint32_t s, const double a[3], const double b[3]) {
     const uint32_t o = s << 3;
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
-        *reinterpret_cast<double2 *>(reinterpret_cast<char *>(f + c * pitch) + o) = make_double2(a[c], b[c]);
+    for (int c = 0; c < 3; ++c) {
+        v2d *q = reinterpret_cast<v2d *>(reinterpret_cast<char *>(f + c * pitch) + o);
+        const v2d v = {a[c], b[c]};
+        if (PAMG_NT) __builtin_nontemporal_store(v, q);
+        else *q = v;
+    }
 }
 __device__ __forceinline__ void copy3(double d[3], const double s[3]) {
 #pragma unroll
@@ -575,13 +584,14 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     if (v0) {
         if constexpr (C > 0)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) st2(F0 + c * 1024 + 2 * t, make_double2(p0[0][c], p0[1][c]));
+            for (int c = 0; c < 3; ++c) *reinterpret_cast<double2 *>(F0 + c * 1024 + 2 * t) = make_double2(p0[0][c], p0[1][c]);
         double r[2][3];
 #pragma unroll
         for (int k = 0; k < 2; ++k) residual(St, rdt, p0[k], b0[k], r[k]);
         store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
         if constexpr (C > 0)   // restrictor input: mean of the residual components (splitting.F90:146-151)
-            st2(M0 + 2 * t, make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.));
+            *reinterpret_cast<double2 *>(M0 + 2 * t) =
+                make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
     }
     stamp<kMTf>(A, 2);
     // level-1 sub-element t: its final tnew (coarse launch) for the prolongator, its children
