@@ -21,9 +21,12 @@ same workload and reported under "extra".
 
 N > 1 (python -m torch.distributed.run ... bench.py --gpus N): strong scaling
 of the same mesh, x-strip domain decomposition by unstructured element, one
-process per GPU, halo exchanged with RCCL (grouped ncclSend/ncclRecv over
-xGMI) once per V-cycle, overlapped with the next one. `value` = V-cycles of
-the whole mesh / max over ranks of the timed wall time.
+process per GPU, halo words of remote neighbours packed by the level-1 launch
+and exchanged with RCCL (grouped ncclSend/ncclRecv over xGMI) after the last
+cycle of each pamg_vcycle call (every cycle rewrites every halo word and
+nothing inside the call reads them; --halo-exchange 1 exchanges after every
+cycle, overlapped with the next). `value` = V-cycles of the whole mesh / max
+over ranks of the timed wall time.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -55,6 +58,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the n_split=3 and sweep-kernel side measurements")
     ap.add_argument("--halo-mode", type=int, default=0)
+    ap.add_argument("--halo-exchange", type=int, default=0,
+                    help="multi-rank: 0 exchange the level-1 halo once per pamg_vcycle call (after its last "
+                         "cycle), 1 after every cycle")
     ap.add_argument("--arith", type=int, default=1,
                     help="1: contracted operator arithmetic (fma rows of A_e = M/dt + Kd; ~1e-15 of the reference, "
                          "the north star's bar is 1e-10); 0: the reference's operation order (bitwise)")
@@ -140,7 +146,8 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     device = local % ndev
     s = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
-                                   halo_mode=a.halo_mode, comm=comm, fused=a.fused, arith=a.arith)
+                                   halo_mode=a.halo_mode, comm=comm, fused=a.fused, arith=a.arith,
+                                   halo_exchange=a.halo_exchange)
     s.begin_timestep()
     s.vcycle(a.warmup)
     s.synchronize()
@@ -252,7 +259,7 @@ def main():
                        "fine_sub_elements": mesh.U * 4 ** a.nsplit, "levels": a.levels,
                        "parallelism": f"dd{world}", "halo_mode": a.halo_mode,
                        "arith": "contracted (fma, 1e-15 of the reference)" if a.arith else "reference order (bitwise)",
-                       "fused": a.fused},
+                       "fused": a.fused, "halo_exchange": "per call" if a.halo_exchange == 0 else "per cycle"},
             "roofline": {"bound": "hbm", "kernel": RK_DESC[rk],
                          "events": "timed region" if live_events else "post-pass of min(steps, 20) cycles",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -94,7 +94,12 @@ typedef struct {
                             one fma chain per row: 12 fp64 operations per sub-element sweep instead
                             of 39; within 1e-13 relative of the reference (the north star's bar
                             is 1e-10), bitwise equal between the fused and per-step schedules */
-    int reserved[4];
+    int halo_exchange; /* multi-rank fused V-cycle: 0 (default) the RCCL exchange of the level-1 halo
+                          words runs once per pamg_vcycle call, after its last cycle -- every cycle
+                          rewrites every halo word and nothing in the cycle reads t_overlap, so only
+                          the last cycle's words are observable (state identical to 1); 1: after
+                          every cycle, overlapped with the next one */
+    int reserved[3];
 } pamg_params;
 
 /* mode-9 defaults of the reference (main.F90:46-47, transport_tri_semi.F90:117-140) */

@@ -410,8 +410,10 @@ int vcycle_fused(pamg_handle *h, int n) {
         if (L > 1) L2.RHSN = rhsn_w;   // the next cycle's level-2 RHS
         h->tnn_level = 1;
         // every halo word of the cycle was written by the level-1 launch (its remote ones
-        // packed into `buf`): one exchange per cycle, in flight during the next one
-        CHK(halo_async(h, buf));
+        // packed into `buf`); the next cycle rewrites every one of them and nothing reads
+        // t_overlap in between: halo_exchange = 0 exchanges the last cycle's words only,
+        // 1 every cycle's, in flight during the next one
+        if (h->p.halo_exchange == 1 || c + 1 == n) CHK(halo_async(h, buf));
     }
     if (conc && n > 0) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));   // join
     return join_comm(h);
@@ -461,7 +463,7 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
         p->n_smooth < 0 || p->n_coarse < 0 || (p->solver < 1 || p->solver > 3) || !(p->dt > 0) ||
         p->theta != 1.0 || (p->halo_mode != 0 && p->halo_mode != 1) ||
         (p->coarse_solver != 0 && p->coarse_solver != 1) || p->fused < 0 || p->fused > 3 ||
-        (p->arith != 0 && p->arith != 1))
+        (p->arith != 0 && p->arith != 1) || (p->halo_exchange != 0 && p->halo_exchange != 1))
         return PAMG_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PAMG_ERR_NODEV;

@@ -21,7 +21,8 @@ module pamg
     integer(c_int) :: fused
     integer(c_int) :: coarse_solver
     integer(c_int) :: arith
-    integer(c_int) :: reserved(4)
+    integer(c_int) :: halo_exchange
+    integer(c_int) :: reserved(3)
   end type pamg_params
 
   public :: pamg_default_params, pamg_msh_read, pamg_msh_size, pamg_msh_get, pamg_msh_free

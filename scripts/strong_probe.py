@@ -16,7 +16,7 @@ S = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 base = None
 for n in (1, 2, 4, 8):
     comm = None if n == 1 else (n, 0, None, mesh.x_strip_owner(n))
-    s = pamg.SemiImplicitIterative(mesh, S, 3, n_smooth=4, solver=3, comm=comm)
+    s = pamg.SemiImplicitIterative(mesh, S, 3, n_smooth=4, solver=3, comm=comm, arith=1)
     s.begin_timestep()
     s.vcycle(5)
     s.synchronize()

@@ -138,16 +138,19 @@ def test_full_size_against_oracle(mesh, S, L):
         assert goldens.rel_err(x, y) <= TOL
 
 
-def test_partitioned_run_matches_single_gpu():
+@pytest.mark.parametrize("fused,exch", [(3, 0), (3, 1), (1, 0), (0, 0)])
+def test_partitioned_run_matches_single_gpu(fused, exch):
     """Two partitions of untitled8192 (x-strips) on one GPU, halo exchanged by
-    the loopback path (the same packed segments RCCL carries between ranks)."""
+    the loopback path (the same packed segments RCCL carries between ranks);
+    exch = 0 packs the exchange once per pamg_vcycle call, 1 after every cycle."""
     mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
     full = pamg.SemiImplicitIterative(mesh, 3, 3)
-    full.run(1, 2)
+    full.run(1, 3)
     owner = mesh.x_strip_owner(2)
-    parts = [pamg.SemiImplicitIterative(mesh, 3, 3, comm=(2, r, None, owner)) for r in range(2)]
+    parts = [pamg.SemiImplicitIterative(mesh, 3, 3, comm=(2, r, None, owner), fused=fused, halo_exchange=exch)
+             for r in range(2)]
     for p in parts:
-        p.run(1, 2)
+        p.run(1, 3)
     halo_loopback(parts, 1)
     ref_state = full.state()
     ref_ov = full.overlap()
