@@ -129,6 +129,12 @@ int pamg_get_state(pamg_handle *h, int level, int what, double *host);
 /* halo buffers meshList(:)%t_overlap / t_overlap_old as (2**n_split*3, 3, U) */
 int pamg_get_overlap(pamg_handle *h, double *t_overlap, double *t_overlap_old);
 int pamg_tnn_level(pamg_handle *h);
+/* VTU of the level-1 solution: replaces get_vtu (get_vtk_files.F90:10-165, called at
+ * transport_tri_semi.F90:301-311) -- the same cells (one triangle per level-1 sub-element
+ * with its own 3 DG nodes) and point data ("Tracer" = tnew, "error" = |tnew - sin(x+y)|,
+ * "analytical" = sin(x+y)) at full fp64 precision; ascii = 0 raw appended binary, 1 ascii.
+ * Multi-rank: each rank writes its own elements (one file per rank). */
+int pamg_write_vtu(pamg_handle *h, const char *path, int ascii);
 
 /* ---- the hot path, one entry per reference call site ---- */
 /* :316-317 told := tnew, tnew_nonlin := tnew, plus level-1 RHS (get_RHS :452-464) */

@@ -531,6 +531,9 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         for (int g = 0; g < U; ++g) h->owned.push_back(g);
     }
     h->U = (int)h->owned.size();
+    h->Xo.resize(6 * h->owned.size());
+    for (size_t q = 0; q < h->owned.size(); ++q)
+        for (int c = 0; c < 6; ++c) h->Xo[6 * q + c] = X[6 * (size_t)h->owned[q] + c];
     for (int g = 0; g < U; ++g)
         for (int f = 0; f < 3; ++f) {
             const int n = neig[3 * g + f];

@@ -110,6 +110,7 @@ struct pamg_handle {
     int U = 0;                 // local un_ele count
     int U_global = 0;
     std::vector<int> owned;    // global ids (0-based) of local un_eles, ascending
+    std::vector<double> Xo;    // X(2,3) of the local un_eles (pamg_write_vtu)
     pamg::Level lv[pamg::kMaxLevels + 1];   // 1-based
     double *geo1 = nullptr;    // U * kGeoStride
     double *tov = nullptr, *tovo = nullptr; // (slots, 3, U) t_overlap / t_overlap_old

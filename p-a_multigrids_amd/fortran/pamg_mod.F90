@@ -30,6 +30,7 @@ module pamg
   public :: pamg_begin_timestep, pamg_copy_to_nonlin, pamg_smoother, pamg_sweep, pamg_restrictor
   public :: pamg_get_residual, pamg_prolongator, pamg_vcycle, pamg_run, pamg_synchronize
   public :: pamg_destroy, pamg_last_error, pamg_check, c_path, pamg_block_inverse, pamg_direct_solve
+  public :: pamg_write_vtu
 
   interface
     subroutine pamg_default_params(p) bind(C, name='pamg_default_params')
@@ -146,6 +147,12 @@ module pamg
       import :: c_int, c_ptr
       type(c_ptr), value :: h
       integer(c_int), value :: level
+    end function
+    integer(c_int) function pamg_write_vtu(h, path, ascii) bind(C, name='pamg_write_vtu')
+      import :: c_int, c_ptr, c_char
+      type(c_ptr), value :: h
+      character(kind=c_char), intent(in) :: path(*)
+      integer(c_int), value :: ascii
     end function
     integer(c_int) function pamg_destroy(h) bind(C, name='pamg_destroy')
       import :: c_int, c_ptr

@@ -10,9 +10,12 @@
 ! (default pamg_run.nml):
 !   &transport mesh_file='untitled8.msh', n_split=3, multi_levels=3, n_smooth=4,
 !             solver=3, ntime=2, n_multigrid=2, device=0, dump='out.bin',
-!             call_sites=1 /
+!             call_sites=1, vtk_interval=0 /
 ! call_sites=1 drives the fine-grained entry points exactly at the reference
 ! call sites; call_sites=0 calls pamg_run (the same sequence inside libpamg).
+! vtk_interval > 0 writes Tracer_<itime>.vtu at the start of every vtk_interval-th
+! step as the reference's get_vtu call site does (:301-311; main.F90:46 passes 1),
+! through pamg_write_vtu (full precision, raw appended binary).
 program pamg_transport
   use iso_c_binding
   use pamg
@@ -22,9 +25,10 @@ program pamg_transport
 
   character(len=512) :: mesh_file = 'untitled8.msh', dump = ''
   integer :: n_split = 1, multi_levels = 1, n_smooth = 4, solver = 3, ntime = 2, n_multigrid = 2
-  integer :: device = 0, call_sites = 1, facade_sweeps = 0
+  integer :: device = 0, call_sites = 1, facade_sweeps = 0, vtk_interval = 0, vtk_io
+  character(len=64) :: vtu_name
   namelist /transport/ mesh_file, n_split, multi_levels, n_smooth, solver, ntime, n_multigrid, device, dump, &
-       call_sites, facade_sweeps
+       call_sites, facade_sweeps, vtk_interval
 
   character(len=512) :: cfg
   type(c_ptr) :: m = c_null_ptr, h = c_null_ptr
@@ -86,7 +90,13 @@ program pamg_transport
   if (call_sites == 0) then
     call pamg_check(pamg_run(h, int(ntime, c_int), int(n_multigrid, c_int)), h, 'pamg_run')
   else
+    vtk_io = vtk_interval                                   ! :132
     do itime = 1, ntime                                     ! :299
+      if (vtk_interval > 0 .and. vtk_io <= itime) then      ! :301-311
+        write(vtu_name, '(a,i0,a)') 'Tracer_', itime, '.vtu'
+        call pamg_check(pamg_write_vtu(h, c_path(vtu_name), 0_c_int), h, 'pamg_write_vtu')
+        vtk_io = vtk_io + vtk_interval
+      end if
       call pamg_check(pamg_begin_timestep(h), h, 'begin_timestep')     ! :316-317
       do multigrid = 1, n_multigrid                         ! :319
         do ilevel = 1, multi_levels                         ! restriction leg :323-340

@@ -82,6 +82,7 @@ def lib():
         "pamg_sweep_bench": (I, [P, I, I, C.POINTER(D), C.POINTER(D)]),
         "pamg_block_inverse": (I, [P, I, C.c_long, dp, dp, ip]),
         "pamg_direct_solve": (I, [P, I]),
+        "pamg_write_vtu": (I, [P, C.c_char_p, I]),
         "pamg_comm_unique_id": (I, [C.c_char_p]),
         "pamg_comm_init": (I, [P, I, I, C.c_char_p, I, ip]),
         "pamg_owned_count": (I, [P]),

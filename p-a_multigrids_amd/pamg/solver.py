@@ -7,6 +7,7 @@ smoother, restrictor, get_residual, prolongator, plus the driver loop. Field
 arrays use the reference's Fortran shape (3, nsub, U), fp64.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -161,6 +162,10 @@ class SemiImplicitIterative:
     def prolongator(self, level): self._call("pamg_prolongator", level)
     def vcycle(self, n=1): self._call("pamg_vcycle", n)
     def direct_solve(self, level): self._call("pamg_direct_solve", level)
+
+    def write_vtu(self, path, ascii=False):
+        """get_vtu (get_vtk_files.F90:10-165) of the level-1 solution at full precision."""
+        self._call("pamg_write_vtu", os.fsencode(path), 1 if ascii else 0)
 
     def block_inverse(self, A):
         """FINDInv (matrix_inversion.F90:50-148) of a batch A (n, n, nb), column-major as the
