@@ -47,7 +47,16 @@ namespace {
 
 using namespace detail;
 
-constexpr int kMTf = 512;   // threads per workgroup, level-0 kernel (one adjacent pair each)
+// level-1 launch: a tile of 2**TL level-0 sub-elements (whole un_eles, TL >= 2 n_split) on
+// 2**(TL-1) threads, one adjacent pair each. TL = max(2 n_split, PAMG_FINE_TL_MIN) = 10: 1024
+// sub-elements, 512 threads (one un_ele at n_split = 5). Measured (scripts/ab2.sh): 256-element
+// tiles (PAMG_FINE_TL_MIN=8, 4x the workgroups at n_split <= 4) are 7-9 % slower at n_split = 3
+// and 4, and forcing 8 waves per SIMD (PAMG_FINE_WAVES=8, <= 64 VGPRs) 0.5-50 % slower.
+#ifndef PAMG_FINE_TL_MIN
+#define PAMG_FINE_TL_MIN 10
+#endif
+constexpr int fine_tl(int S) { return 2 * S > PAMG_FINE_TL_MIN ? 2 * S : PAMG_FINE_TL_MIN; }
+constexpr int fine_mt(int S) { return 1 << (fine_tl(S) - 1); }
 constexpr int kMTc = 64;    // threads per workgroup, coarse-level kernel (one wave per tile)
 
 // the planes of a level are one allocation (pamg_api.cpp): tnew, tnew_nonlin, RHS,
@@ -95,13 +104,16 @@ __device__ __forceinline__ void stamp_hwid(const VArgs &A) {
 }
 
 // tile geometry (0-based level l): 4**(S-l) sub-elements per un_ele; a tile holds
-// 1024 >> 2l sub-elements of level l (1024 / 4**S un_eles)
+// T >> 2l sub-elements of level l (T / 4**S un_eles), T = 2**TL
 template <int S, int L>
 struct Geo {
     static constexpr int C = L - 1;                                // coarsest level
-    static constexpr int GL = 10 - 2 * S;                          // log2 un_eles per tile
+    static constexpr int TL = fine_tl(S);
+    static constexpr int T = 1 << TL;                              // level-0 sub-elements per tile
+    static constexpr int MT = T / 2;                               // threads of the level-1 launch
+    static constexpr int GL = TL - 2 * S;                          // log2 un_eles per tile
     static constexpr int lg(int l) { return 2 * (S - l); }
-    static constexpr int nt(int l) { return 1024 >> (2 * l); }
+    static constexpr int nt(int l) { return T >> (2 * l); }
     // each wave inside one un_ele (a wave spans 128 level-0 sub-elements, 64 of any other level)
     static constexpr bool uni(int l) { return lg(l) >= (l == 0 ? 7 : 6); }
 };
@@ -442,8 +454,9 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
 // that sub-element, and level 2's tnew, read once, serves both the prolongator of cycle c
 // (:370, its final value) and the start of cycle c+1 (:348). A call
 // of n cycles is launched as coarse(1), [level 1 (c) + coarse (c+1)] for c < n, level 1 (n).
-// Thread -> coarse element: level 2 on threads 0..255 (the owners of y1), level l >= 3 on
-// the wave 4 + (l - 3), so a wave holds one level; the phases are the coarse launch's:
+// Thread -> coarse element: level 2 on threads 0..nt(1)-1 (the owners of y1), the levels
+// l >= 3 packed behind it (one wave for all of them at n_split = 5); the phases are the
+// coarse launch's:
 //   A: RHS_l := restrictor (:336), the restriction-leg call (:331), get_residual (:338);
 //   B: restrictor of the new residuals into RHSN (next cycle), the prolongation-leg call
 //      (:376) or, on the coarsest level, the 1 + n_coarse calls (:351-353), tnew stored;
@@ -453,12 +466,13 @@ struct PGeo {
     using G = Geo<S, L>;
     static constexpr int C = G::C;
     static constexpr int nt(int l) { return G::nt(l); }
-    static constexpr int T0(int l) { return l == 1 ? 0 : 256 + 64 * (l - 2); }
-    static constexpr int NTH(int l) { return l == 1 ? 256 : 64; }
+    static constexpr int T0(int l) { int o = 0; for (int i = 1; i < l; ++i) o += nt(i); return o; }
+    static constexpr int NTH(int l) { return nt(l); }
+    static_assert(T0(C + 1) <= G::MT, "coarse sub-elements exceed the threads of the tile");
     // LDS images in the F0 | M0 region: F_l, M_l (1 <= l < C)
     static constexpr int F(int l) { int o = 0; for (int i = 1; i < l; ++i) o += 3 * nt(i); return o; }
     static constexpr int M(int l) { int o = F(C); for (int i = 1; i < l; ++i) o += nt(i); return o; }
-    static_assert(M(C) <= 4 * 1024, "coarse images exceed the level-1 image region");
+    static_assert(M(C) <= 4 * G::T, "coarse images exceed the level-1 image region");
 };
 
 template <int S, int L, class ST>
@@ -546,7 +560,10 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
 // Ownership: the adjacent pair 2t, 2t+1 of the tile (16-byte accesses, one un_ele,
 // one operator record); for the prolongator, level-1 sub-element t.
 template <int S, int L, class ST, bool PIPE>
-__global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0,
+#ifndef PAMG_FINE_WAVES
+#define PAMG_FINE_WAVES 4
+#endif
+__global__ __launch_bounds__(fine_mt(S), (S >= 3) ? PAMG_FINE_WAVES : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0,
                                                                       const double *__restrict__ sp1,
                                                                       const double *__restrict__ sp2,
                                                                       const double *__restrict__ sp3,
@@ -556,15 +573,16 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     static_assert(!PIPE || C > 0, "the pipelined launch needs a coarse level");
     // F0 | M0: restriction-leg tnew image and residual means (restrictor input) of level 1;
     // the pipelined tail reuses the region for the coarse levels' images
-    __shared__ __attribute__((aligned(16))) double F0[C > 0 ? 4 * 1024 : 1];
-    double *const M0 = F0 + 3 * 1024;
+    constexpr int T = G::T, MT = G::MT;
+    __shared__ __attribute__((aligned(16))) double F0[C > 0 ? 4 * T : 1];
+    double *const M0 = F0 + 3 * T;
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
     const int64_t u0 = (int64_t)blockIdx.x << G::GL;
     const int nue = G::GL == 0 ? 1 : (int)min((int64_t)1 << G::GL, A.U - u0);   // un_eles in this tile
-    stamp<kMTf>(A, 0);
-    stamp_hwid<kMTf>(A);
+    stamp<MT>(A, 0);
+    stamp_hwid<MT>(A);
     const VLevel &V0 = A.lv[0];
     const bool v0 = 2 * t < (nue << G::lg(0));
     const uint32_t s0 = ((uint32_t)u0 << G::lg(0)) + (v0 ? 2 * t : 0);   // clamped: loads stay in bounds
@@ -580,11 +598,11 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     stencil(G::uni(0), sp0, w0, St);
     // ---- restriction leg: smoother (:331), get_residual (:338)
     sweeps2(St, rdt, ns, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
-    stamp<kMTf>(A, 1);
+    stamp<MT>(A, 1);
     if (v0) {
         if constexpr (C > 0)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) *reinterpret_cast<double2 *>(F0 + c * 1024 + 2 * t) = make_double2(p0[0][c], p0[1][c]);
+            for (int c = 0; c < 3; ++c) *reinterpret_cast<double2 *>(F0 + c * T + 2 * t) = make_double2(p0[0][c], p0[1][c]);
         double r[2][3];
 #pragma unroll
         for (int k = 0; k < 2; ++k) residual(St, rdt, p0[k], b0[k], r[k]);
@@ -593,10 +611,11 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
             *reinterpret_cast<double2 *>(M0 + 2 * t) =
                 make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
     }
-    stamp<kMTf>(A, 2);
+    stamp<MT>(A, 2);
     // level-1 sub-element t: its final tnew (coarse launch) for the prolongator, its children
     // for the prolongator and the restrictor, fetched behind the prolongation-leg sweeps
-    // (threads 0..255: prolongator of sub-element t; threads 256..511: restrictor of t - 256)
+    // (threads 0..nt(1)-1: prolongator of sub-element t; the others: restrictor of t - nt(1);
+    //  PIPE: both on threads 0..nt(1)-1)
     const int j1 = t & (G::nt(1) - 1);
     const bool casc = t < G::nt(1);
     bool v1 = false;
@@ -614,7 +633,7 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
     copy3(x0[0], p0[0]);
     copy3(x0[1], p0[1]);
     sweeps2(St, rdt, C > 0 ? ns : ns * A.n_coarse, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
-    stamp<kMTf>(A, 3);
+    stamp<MT>(A, 3);
     if (v0) {
         // the cycle's halo words (update_overlaps, :555), all written here (see the header);
         // halo records by vector loads: the boundary lanes are few, and scalar copies of the
@@ -624,7 +643,7 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
         store3p(V0.T(), V0.pitch, s0, p0[0], p0[1]);
         store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
     }
-    stamp<kMTf>(A, 4);
+    stamp<MT>(A, 4);
     // ---- prolongator (:370) on the LDS image (its result is dead, :550), and the restrictor
     //      of the next cycle (:336) from this cycle's residual (splitting.F90:10-32)
     //      (PIPE: both on the owner of level-2 sub-element t, which keeps the restriction as
@@ -636,7 +655,7 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
             const int base = (j1 >> G::lg(1)) << G::lg(0);
             if (casc) {
                 const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
-                prolong_cascade(F0, 1024, fi, y1);
+                prolong_cascade(F0, T, fi, y1);
             }
             if (PIPE ? casc : !casc) {
                 rn[0] = M0[base + c4.z];
@@ -650,7 +669,7 @@ __global__ __launch_bounds__(kMTf, (S >= 3) ? 4 : 2) void k_vc_fine(VArgs A, con
         const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
         coarse_next<S, L, ST>(A, SP, t, u0, nue, y1, rn, F0);
     }
-    stamp<kMTf>(A, 7);
+    stamp<MT>(A, 7);
 }
 
 // part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
@@ -664,12 +683,12 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
             return hipErrorInvalidValue;
     } else if (part == 2) {
         if constexpr (L >= 2)
-            hipLaunchKernelGGL((k_vc_fine<S, L, ST, true>), dim3(grid), dim3(kMTf), 0, s, A, A.lv[0].stc,
+            hipLaunchKernelGGL((k_vc_fine<S, L, ST, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
                                A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         else
             return hipErrorInvalidValue;
     } else {
-        hipLaunchKernelGGL((k_vc_fine<S, L, ST, false>), dim3(grid), dim3(kMTf), 0, s, A, A.lv[0].stc, nullptr,
+        hipLaunchKernelGGL((k_vc_fine<S, L, ST, false>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc, nullptr,
                            nullptr, nullptr, nullptr);
     }
     return hipGetLastError();
@@ -720,13 +739,13 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.n_coarse = n_coarse;
     A.rdt = rdt;
     A.rhsn2 = rhsn2;
-    // tile: 1024 level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
-    const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : 10 - 2 * n_split;
+    // tile: 2**fine_tl level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
+    const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : fine_tl(n_split) - 2 * n_split;
     const unsigned grid = (unsigned)(((int64_t)U + (1 << GL) - 1) >> GL);
     if (grid == 0) return hipSuccess;
     // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_VCYCLE_STAMPS") : nullptr;
-    const int waves = (coarse ? kMTc : kMTf) / 64;
+    const int waves = coarse ? kMTc / 64 : (1 << fine_tl(n_split)) / 128;
     const size_t nst = (size_t)grid * waves * kStampSlots;
     if (stamp_path) {
         hipError_t e = hipMalloc(&A.stamps, nst * sizeof(long long));

@@ -13,10 +13,11 @@ import pamg  # noqa: E402
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 mesh = pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "untitled8192.msh"))
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+FUSED = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 base = None
 for n in (1, 2, 4, 8):
     comm = None if n == 1 else (n, 0, None, mesh.x_strip_owner(n))
-    s = pamg.SemiImplicitIterative(mesh, S, 3, n_smooth=4, solver=3, comm=comm, arith=1)
+    s = pamg.SemiImplicitIterative(mesh, S, 3, n_smooth=4, solver=3, comm=comm, arith=1, fused=FUSED)
     s.begin_timestep()
     s.vcycle(5)
     s.synchronize()
@@ -33,6 +34,6 @@ for n in (1, 2, 4, 8):
         res.append((dt, {kk: round(v["ms"] / k, 4) for kk, v in tm.items() if v["launches"]}))
     if base is None:
         base = res[0][0]
-    print(f"N={n}: {res[0][0]:.4f} ms/cycle (ideal {base / n:.4f}, eff {base / n / res[0][0]:.2f}); "
+    print(f"fused={FUSED} N={n}: {res[0][0]:.4f} ms/cycle (ideal {base / n:.4f}, eff {base / n / res[0][0]:.2f}); "
           f"timed {res[1][0]:.4f} {res[1][1]}", flush=True)
     s.close()
