@@ -40,6 +40,8 @@ import sys
 import tempfile
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "p-a_multigrids_amd"))
 MESH = os.path.join(ROOT, "tests", "meshes", "untitled8192.msh")
@@ -206,6 +208,22 @@ def main():
             extra["sweep_assembled" if asm else "sweep_stencil"] = dict(
                 ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
                 frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
+        # the matrices.F90 SpMV (csr_mul_array, 3 entries per row) over the level-1 operator's
+        # size in the reference's block numbering: 3 N1 rows, 52 B per row (3 x (4 B column +
+        # 8 B value), 8 B result, 8 B of the gathered vector)
+        nrows = 3 * mesh.U * 4 ** a.nsplit
+        base = 3 * (np.arange(nrows, dtype=np.int32) // 3)
+        jloc = (base[:, None] + np.arange(1, 4, dtype=np.int32)[None, :]).reshape(-1)
+        del base
+        sp = pamg.Sparse(s, np.arange(1, 3 * nrows, 3, dtype=np.int32), jloc,
+                         np.random.default_rng(20251015).uniform(-1, 1, 3 * nrows))
+        del jloc
+        ms = sp.bench(nrows, 20)
+        by = 52.0 * nrows
+        extra["csr_mul_array"] = dict(rows=nrows, ms=round(ms, 4), bytes_per_launch=by,
+                                      gbs=round(by / (ms * 1e-3) / 1e9, 1),
+                                      frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
+        sp.close()
         s.close()
         # the same workload in the other schedules / arithmetic: the per-step kernel sequence
         # (bitwise equal to the fused cycle), the concurrent fused launches, and the reference's

@@ -180,6 +180,21 @@ int pamg_block_inverse(pamg_handle *h, int n, long nb, const double *A, double *
 /* tnew = tnew_nonlin = A_e^-1 RHS on `level` (the coarse_solver = 1 step, callable per level) */
 int pamg_direct_solve(pamg_handle *h, int level);
 
+/* ---- the matrices.F90 SpMV: replaces csr_mul_array (matrices.F90:172-193) ----
+ * The reference's `type sparse` (Structures.F90:196-201): nrows = size(g_iloc) rows (its
+ * values are not read), g_jloc 1-based columns and val in storage order; the routine
+ * consumes 3 entries per row in that order, so nnz >= 3 nrows. Uploaded once by
+ * pamg_csr_create; pamg_csr_mul_array(h, m, n, array(n), result(nrows)) is the call site's
+ * `call csr_mul_array(sparse_matrix, array, result)`, bitwise equal to it. */
+typedef struct pamg_csr pamg_csr;
+int pamg_csr_create(pamg_handle *h, long nrows, long nnz, const int *g_jloc, const double *val, pamg_csr **m);
+int pamg_csr_mul_array(pamg_handle *h, pamg_csr *m, long n, const double *array, double *result);
+/* the same on device-resident vectors (ordered on the handle's stream, no synchronisation) */
+int pamg_csr_mul_array_device(pamg_handle *h, pamg_csr *m, long n, const double *d_array, double *d_result);
+int pamg_csr_free(pamg_csr *m);
+/* roofline measurement of the csr kernel: average of `reps` launches on device vectors */
+int pamg_csr_bench(pamg_handle *h, pamg_csr *m, long n, int reps, double *ms_avg);
+
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---- */
 int pamg_comm_unique_id(char out[128]);
 /* owner[U] = rank (0-based) owning each un_ele; call before pamg_upload_mesh.

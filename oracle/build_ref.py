@@ -35,7 +35,9 @@ Produces pamg_ref_fp64 (-fdefault-real-8 -fdefault-double-8: the parity
 target), pamg_ref_fp32 (default real, as shipped) and
 findinv_ref_fp64 (the reference's FINDInv, matrix_inversion.F90, unmodified,
 behind oracle/ref_hooks/findinv_driver.F90: golden vectors of the local
-block inverse, tests/make_golden_findinv.py).
+block inverse, tests/make_golden_findinv.py) and csr_ref_fp64 (the reference's
+csr_mul_array, matrices.F90:172-193, behind oracle/ref_hooks/csr_driver.F90:
+golden vectors of the matrices.F90 SpMV, tests/make_golden_csr.py).
 """
 import argparse
 import os
@@ -160,8 +162,10 @@ PATCHERS = {
 }
 
 
-def build(ref, out, fp64, verbose=False):
-    name = "pamg_ref_fp64" if fp64 else "pamg_ref_fp32"
+def build(ref, out, fp64, verbose=False, driver=None):
+    """driver: link oracle/ref_hooks/<driver>.F90 as the program instead of the
+    reference's main (csr_driver: the reference's csr_mul_array, matrices.F90:172-193)."""
+    name = driver.replace("_driver", "_ref_fp64") if driver else ("pamg_ref_fp64" if fp64 else "pamg_ref_fp32")
     flags = ["-O2"] + (["-fdefault-real-8", "-fdefault-double-8"] if fp64 else [])
     tmp = tempfile.mkdtemp(prefix="pamg_refbuild_")
     try:
@@ -176,6 +180,9 @@ def build(ref, out, fp64, verbose=False):
                 f.write(text)
         shutil.copy(os.path.join(HERE, "ref_hooks", "pamg_ref_hooks.F90"), tmp)
         order = SOURCES[:9] + ["pamg_ref_hooks"] + SOURCES[9:]
+        if driver:
+            shutil.copy(os.path.join(HERE, "ref_hooks", driver + ".F90"), tmp)
+            order = order[:-1] + [driver]   # the driver program replaces main
         objs = []
         for s in order:
             cmd = [FLANG, "-c"] + flags + [s + ".F90", "-o", s + ".o"]
@@ -238,6 +245,7 @@ def main():
             continue
         build(a.ref, a.out, fp64, verbose=True)
     build_findinv(a.ref, a.out, verbose=True)
+    build(a.ref, a.out, True, verbose=True, driver="csr_driver")
 
 
 if __name__ == "__main__":

@@ -788,3 +788,17 @@ void orc_run(orc_state *s) {
         for (int mg = 0; mg < s->c.n_multigrid; ++mg) orc_vcycle(s);
     }
 }
+
+/* matrices.F90:172-193 csr_mul_array: the entries are consumed in storage order, three per
+ * row, for nrows = size(g_iloc) rows (g_iloc's values are never read); result(r) starts at
+ * 0 and accumulates val(c) * array(g_jloc(c)) in that order; g_jloc is 1-based. */
+void orc_csr_mul_array(long nrows, const int *g_jloc, const double *val, const double *array, double *result) {
+    long c2 = 0;
+    for (long r = 0; r < nrows; ++r) {
+        result[r] = 0.0;
+        for (int n = 0; n < 3; ++n) {
+            result[r] = result[r] + val[c2] * array[g_jloc[c2] - 1];
+            c2 = c2 + 1;
+        }
+    }
+}

@@ -30,7 +30,7 @@ module pamg
   public :: pamg_begin_timestep, pamg_copy_to_nonlin, pamg_smoother, pamg_sweep, pamg_restrictor
   public :: pamg_get_residual, pamg_prolongator, pamg_vcycle, pamg_run, pamg_synchronize
   public :: pamg_destroy, pamg_last_error, pamg_check, c_path, pamg_block_inverse, pamg_direct_solve
-  public :: pamg_write_vtu
+  public :: pamg_write_vtu, pamg_csr_create, pamg_csr_mul_array, pamg_csr_free
 
   interface
     subroutine pamg_default_params(p) bind(C, name='pamg_default_params')
@@ -147,6 +147,25 @@ module pamg
       import :: c_int, c_ptr
       type(c_ptr), value :: h
       integer(c_int), value :: level
+    end function
+    integer(c_int) function pamg_csr_create(h, nrows, nnz, g_jloc, val, m) bind(C, name='pamg_csr_create')
+      import :: c_int, c_ptr, c_long, c_double
+      type(c_ptr), value :: h
+      integer(c_long), value :: nrows, nnz
+      integer(c_int), intent(in) :: g_jloc(*)
+      real(c_double), intent(in) :: val(*)
+      type(c_ptr), intent(out) :: m
+    end function
+    integer(c_int) function pamg_csr_mul_array(h, m, n, array, result) bind(C, name='pamg_csr_mul_array')
+      import :: c_int, c_ptr, c_long, c_double
+      type(c_ptr), value :: h, m
+      integer(c_long), value :: n
+      real(c_double), intent(in) :: array(*)
+      real(c_double), intent(inout) :: result(*)
+    end function
+    integer(c_int) function pamg_csr_free(m) bind(C, name='pamg_csr_free')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: m
     end function
     integer(c_int) function pamg_write_vtu(h, path, ascii) bind(C, name='pamg_write_vtu')
       import :: c_int, c_ptr, c_char

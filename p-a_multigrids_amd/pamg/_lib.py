@@ -83,6 +83,11 @@ def lib():
         "pamg_block_inverse": (I, [P, I, C.c_long, dp, dp, ip]),
         "pamg_direct_solve": (I, [P, I]),
         "pamg_write_vtu": (I, [P, C.c_char_p, I]),
+        "pamg_csr_create": (I, [P, C.c_long, C.c_long, ip, dp, C.POINTER(P)]),
+        "pamg_csr_mul_array": (I, [P, P, C.c_long, dp, dp]),
+        "pamg_csr_mul_array_device": (I, [P, P, C.c_long, C.c_void_p, C.c_void_p]),
+        "pamg_csr_free": (I, [P]),
+        "pamg_csr_bench": (I, [P, P, C.c_long, I, C.POINTER(D)]),
         "pamg_comm_unique_id": (I, [C.c_char_p]),
         "pamg_comm_init": (I, [P, I, I, C.c_char_p, I, ip]),
         "pamg_owned_count": (I, [P]),

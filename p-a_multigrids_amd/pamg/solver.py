@@ -198,6 +198,52 @@ class SemiImplicitIterative:
         return ms.value, by.value
 
 
+class Sparse:
+    """The reference's `type sparse` (Structures.F90:196-201) resident on a handle's device:
+    csr_mul_array (matrices.F90:172-193) as .mul_array(array) -> result(nrows)."""
+
+    def __init__(self, solver, g_iloc, g_jloc, val):
+        self.s = solver
+        self.nrows = int(np.asarray(g_iloc).size)
+        j = np.ascontiguousarray(g_jloc, np.int32)
+        v = np.ascontiguousarray(val, np.float64)
+        m = C.c_void_p()
+        solver._call("pamg_csr_create", self.nrows, j.size, j, v, C.byref(m))
+        self.m = m
+
+    def mul_array(self, array):
+        a = np.ascontiguousarray(array, np.float64)
+        out = np.empty(self.nrows)
+        self.s._call("pamg_csr_mul_array", self.m, a.size, a, out)
+        return out
+
+    def mul_array_device(self, n, d_array, d_result):
+        """device pointers (e.g. torch tensors' data_ptr()), ordered on the handle's stream"""
+        self.s._call("pamg_csr_mul_array_device", self.m, n, C.c_void_p(d_array), C.c_void_p(d_result))
+
+    def bench(self, n, reps=20):
+        """average ms per launch of the device kernel (HIP events)"""
+        ms = C.c_double()
+        self.s._call("pamg_csr_bench", self.m, n, reps, C.byref(ms))
+        return ms.value
+
+    def close(self):
+        if getattr(self, "m", None):
+            self.s.L.pamg_csr_free(self.m)
+            self.m = None
+
+    def __del__(self):
+        self.close()
+
+
+def csr_mul_array(solver, sparse_matrix, array):
+    """matrices.F90:172 `call csr_mul_array(sparse_matrix, array, result)`; sparse_matrix is
+    (g_iloc, g_jloc, val) or a Sparse."""
+    if not isinstance(sparse_matrix, Sparse):
+        sparse_matrix = Sparse(solver, *sparse_matrix)
+    return sparse_matrix.mul_array(array)
+
+
 def unique_id():
     buf = C.create_string_buffer(128)
     _check("pamg_comm_unique_id", lib().pamg_comm_unique_id(buf))

@@ -54,6 +54,9 @@ def lib():
         dpc = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
         L.orc_findinv.restype = C.c_int
         L.orc_findinv.argtypes = [C.c_int, dpc, dpc]
+        ipc = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+        L.orc_csr_mul_array.restype = None
+        L.orc_csr_mul_array.argtypes = [C.c_long, ipc, dpc, dpc, dpc]
         for name in ("orc_copy_to_tnn", "orc_smoother", "orc_get_residual", "orc_restrictor",
                      "orc_prolongator", "orc_update_overlaps", "orc_direct_solve"):
             getattr(L, name).argtypes = [P, C.c_int]
@@ -150,6 +153,14 @@ class Oracle:
             d[f"res_L{l}"] = self.get(RES, l)
         d["tnew_nonlin"] = self.get(TNN)
         return d
+
+
+def csr_mul_array(nrows, jloc, val, array):
+    """csr_mul_array restatement (oracle/pamg_oracle.c orc_csr_mul_array)."""
+    out = np.empty(nrows)
+    lib().orc_csr_mul_array(nrows, np.ascontiguousarray(jloc, np.int32), np.ascontiguousarray(val, np.float64),
+                            np.ascontiguousarray(array, np.float64), out)
+    return out
 
 
 def findinv(A):
