@@ -99,7 +99,13 @@ typedef struct {
                           rewrites every halo word and nothing in the cycle reads t_overlap, so only
                           the last cycle's words are observable (state identical to 1); 1: after
                           every cycle, overlapped with the next one */
-    int reserved[3];
+    int cycle;        /* 0 (default): the reference's V-cycle with all its quirks;
+                         1: the corrected V-cycle of SURVEY.md 8(f) rank 2 -- the restrictor acts on
+                         the fresh residual b - A x, coarse levels start from zero, the prolonged
+                         correction (P1 interpolation of the coarse iterate) is added to the iterate
+                         the next smoother call starts from; per-step kernels; no reference output
+                         exists, pinned to the oracle's restatement */
+    int reserved[2];
 } pamg_params;
 
 /* mode-9 defaults of the reference (main.F90:46-47, transport_tri_semi.F90:117-140) */

@@ -781,6 +781,83 @@ void orc_vcycle(orc_state *s) {
     }
 }
 
+/* ---- the corrected V-cycle (the build's opt-in, no reference
+ * output exists): the reference's levels, operators, smoother, restrictor weights and
+ * interpolation weights, with the cycle's three defects of A3 fixed -- (iii) the
+ * restrictor acts on the FRESH residual, (i)/(iv) the prolonged coarse correction is
+ * added to the iterate the next smoother call starts from, and the residual has the
+ * b - A x sign; coarse levels start from zero every cycle. The iterate of a level after
+ * a smoother call is tnew_nonlin (the last sweep), copied to tnew. */
+
+/* res_l = RHS_l - A_l tnew_l (get_residual's products, :725-873, with the b - A x sign) */
+static void residual_corrected(orc_state *s, int l) {
+    int nsub = s->nsub[l - 1];
+    double rdt = 1 / s->c.dt;
+    double *T = s->tnew[l - 1], *To = s->told[l - 1], *R = s->rhs[l - 1];
+    for (int u = 0; u < s->U; ++u) {
+        double M[3][3], Kd[3][3], ml[3];
+        stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+        for (int se = 1; se <= nsub; ++se) {
+            size_t o = (size_t)3 * ((size_t)u * nsub + se - 1);
+            double A[3], mo[3];
+            get_A_x(s, M, Kd, rdt, T + o, To + o, A, mo);
+            for (int i = 0; i < 3; ++i) s->res[l - 1][o + i] = R[o + i] - A[i];
+        }
+    }
+}
+
+/* tnew_l += P tnew_{l+1}: the P1 interpolation the prolongator's cascade (splitting.F90:59-88)
+ * encodes -- each child node gets a coarse vertex value or an edge midpoint -- applied to the
+ * coarse correction alone (the cascade also feeds already-updated fine values forward) */
+static void interp_add(orc_state *s, int l) {
+    int i_split = s->c.n_split - l + 1, nf = s->nsub[l - 1], nc = s->nsub[l];
+    double *F = s->tnew[l - 1];
+    const double *Y = s->tnew[l];
+    for (int u = 0; u < s->U; ++u)
+        for (int c = 1; c <= nc; ++c) {
+            int fin[4];
+            element_conversion(fin, c, i_split - 1);
+            const double *y = Y + (size_t)3 * ((size_t)u * nc + c - 1);
+            const double m20 = 0.5 * y[2] + 0.5 * y[0], m12 = 0.5 * y[1] + 0.5 * y[2], m01 = 0.5 * y[0] + 0.5 * y[1];
+            const double add[4][3] = {{m20, m12, y[2]}, {m12, m20, m01}, {y[0], m01, m20}, {m01, y[1], m12}};
+            for (int q = 0; q < 4; ++q) {
+                double *f = F + (size_t)3 * ((size_t)u * nf + fin[q] - 1);
+                for (int i = 0; i < 3; ++i) f[i] = f[i] + add[q][i];
+            }
+        }
+}
+
+static void smooth_to_tnew(orc_state *s, int l, int calls) {
+    copy_to_tnn(s, l);
+    for (int i = 0; i < calls; ++i) smoother(s, l);
+    memcpy(s->tnew[l - 1], s->tnn, lvl_len(s, l) * sizeof(double));
+}
+
+void orc_vcycle_corrected(orc_state *s) {
+    int L = s->c.levels;
+    for (int l = 1; l < L; ++l) {
+        if (l > 1) memset(s->tnew[l - 1], 0, lvl_len(s, l) * sizeof(double));
+        smooth_to_tnew(s, l, 1);
+        residual_corrected(s, l);
+        restrictor(s, l);
+    }
+    memset(s->tnew[L - 1], 0, lvl_len(s, L) * sizeof(double));
+    if (L == 1) {
+        smooth_to_tnew(s, 1, 1);
+        residual_corrected(s, 1);
+    } else if (s->c.coarse_solver == 1) {
+        copy_to_tnn(s, L);
+        direct_solve(s, L);
+    } else {
+        smooth_to_tnew(s, L, s->c.n_coarse);
+    }
+    for (int l = L - 1; l >= 1; --l) {
+        interp_add(s, l);
+        smooth_to_tnew(s, l, 1);
+    }
+    if (L > 1) residual_corrected(s, 1);   /* the fine residual after the cycle */
+}
+
 /* :299-381 the time loop */
 void orc_run(orc_state *s) {
     for (int it = 0; it < s->c.ntime; ++it) {

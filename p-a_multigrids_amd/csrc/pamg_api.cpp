@@ -344,6 +344,54 @@ int vcycle_steps(pamg_handle *h) {
     return PAMG_OK;
 }
 
+// the corrected V-cycle (params.cycle = 1; oracle orc_vcycle_corrected):
+// the reference's smoother, restrictor and levels with the cycle's defects fixed -- the
+// restrictor acts on the fresh residual b - A x, coarse levels start from zero, the prolonged
+// correction is added to the iterate the next smoother call starts from. A level's iterate
+// after a smoother call is its tnew_nonlin (the last sweep), copied to tnew.
+int smooth_to_tnew(pamg_handle *h, int l, int sweeps) {
+    Level &L = h->lv[l];
+    CHK(smooth(h, l, true, sweeps));
+    HIPCHK(h, launch_copy(h->stream, L.TNN, L.T, 3 * L.pitch));
+    return PAMG_OK;
+}
+
+int residual_corrected(pamg_handle *h, int l) {
+    h->rhsn_valid = false;
+    Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)h->lv[l].N + 168.0 * h->U);
+    HIPCHK(h, launch_residual(h->stream, h->lv[l], 1 / h->p.dt, true));
+    return PAMG_OK;
+}
+
+int vcycle_corrected(pamg_handle *h) {
+    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    h->overlap_static_l1 = false;   // the smoother calls rewrite the halo words
+    for (int l = 1; l < L; ++l) {
+        if (l > 1) HIPCHK(h, hipMemsetAsync(h->lv[l].T, 0, 3 * (size_t)h->lv[l].pitch * sizeof(double), h->stream));
+        CHK(smooth_to_tnew(h, l, ns));
+        CHK(residual_corrected(h, l));
+        CHK(restrict_(h, l));
+    }
+    Level &C = h->lv[L];
+    HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));
+    if (L == 1) {
+        CHK(smooth_to_tnew(h, 1, ns));
+        CHK(residual_corrected(h, 1));
+    } else if (h->p.coarse_solver == 1) {
+        CHK(direct_solve(h, L));
+    } else {
+        CHK(smooth_to_tnew(h, L, ns * h->p.n_coarse));
+    }
+    for (int l = L - 1; l >= 1; --l) {
+        Span sp(h, PAMG_K_PROLONG, 216.0 * (double)h->lv[l + 1].N);
+        HIPCHK(h, launch_interp_add(h->stream, h->lv[l], h->lv[l + 1]));
+        CHK(smooth_to_tnew(h, l, ns));
+    }
+    if (L > 1) CHK(residual_corrected(h, 1));   // the fine residual after the cycle
+    h->tnn_level = 1;
+    return PAMG_OK;
+}
+
 // n V-cycles as two fused launches each (pamg_vcycle.hip)
 int vcycle_fused(pamg_handle *h, int n) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
@@ -463,7 +511,8 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
         p->n_smooth < 0 || p->n_coarse < 0 || (p->solver < 1 || p->solver > 3) || !(p->dt > 0) ||
         p->theta != 1.0 || (p->halo_mode != 0 && p->halo_mode != 1) ||
         (p->coarse_solver != 0 && p->coarse_solver != 1) || p->fused < 0 || p->fused > 3 ||
-        (p->arith != 0 && p->arith != 1) || (p->halo_exchange != 0 && p->halo_exchange != 1))
+        (p->arith != 0 && p->arith != 1) || (p->halo_exchange != 0 && p->halo_exchange != 1) ||
+        (p->cycle != 0 && p->cycle != 1) || (p->cycle == 1 && p->solver == 2))
         return PAMG_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PAMG_ERR_NODEV;
@@ -755,6 +804,10 @@ int pamg_vcycle(pamg_handle *h, int n) {
     if (!h || n < 0) return PAMG_ERR_ARG;
     CHK(check_level(h, 1));
     const int L = h->p.multi_levels;
+    if (h->p.cycle == 1) {
+        for (int c = 0; c < n; ++c) CHK(vcycle_corrected(h));
+        return PAMG_OK;
+    }
     if (h->p.fused && h->p.coarse_solver == 0 &&
         vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth))
         return vcycle_fused(h, n);

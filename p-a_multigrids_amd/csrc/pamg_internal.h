@@ -157,7 +157,9 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
 namespace pamg {
 hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int sweeps, int solver,
                          double rdt, double omega, double *tov, double *tovo);
-hipError_t launch_residual(hipStream_t s, const Level &L, double rdt);
+hipError_t launch_residual(hipStream_t s, const Level &L, double rdt, bool neg = false);
+// corrected cycle: fine.T += P coarse.T (P1 interpolation weights of splitting.F90:59-88)
+hipError_t launch_interp_add(hipStream_t s, const Level &fine, const Level &coarse);
 hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U, double *out = nullptr);
 hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn);
 hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, bool start_of_step);

@@ -132,8 +132,9 @@ __global__ __launch_bounds__(kBlock) void k_smooth(const double *src, double *T,
     halo_write(H, hp, p0, p1);
 }
 
-// get_residual (:725-873): residuale = A x - RHS (note the sign, :869).
-template <class ST>
+// get_residual (:725-873): residuale = A x - RHS (note the sign, :869); NEG: RHS - A x (the
+// corrected cycle's residual, pamg_params.cycle = 1)
+template <class ST, bool NEG = false>
 __global__ __launch_bounds__(kBlock) void k_residual(const double *__restrict__ T, const double *__restrict__ RHS,
                                                      double *__restrict__ RES, const double *__restrict__ stc,
                                                      int64_t pitch, int64_t npairs, int nsub_log2, double rdt) {
@@ -154,7 +155,27 @@ __global__ __launch_bounds__(kBlock) void k_residual(const double *__restrict__ 
     resid(S, rdt, x0, b0, r0);
     resid(S, rdt, x1, b1, r1);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) st2(RES + c * pitch + s, make_double2(r0[c], r1[c]));
+    for (int c = 0; c < 3; ++c) st2(RES + c * pitch + s, NEG ? make_double2(-r0[c], -r1[c]) : make_double2(r0[c], r1[c]));
+}
+
+// corrected cycle: tnew_l += P tnew_{l+1}, the P1 interpolation the prolongator's cascade
+// (splitting.F90:59-88) encodes, applied to the coarse correction alone; one thread per
+// coarse sub-element (its four children are its own)
+__global__ __launch_bounds__(kBlock) void k_interp_add(double *T, const double *__restrict__ Tc,
+                                                       const int4 *__restrict__ children, int64_t pitch_f,
+                                                       int64_t pitch_c, int64_t Nc, int nsubc_log2) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= Nc) return;
+    const double y0 = Tc[c], y1 = Tc[pitch_c + c], y2 = Tc[2 * pitch_c + c];
+    const double m20 = 0.5 * y2 + 0.5 * y0, m12 = 0.5 * y1 + 0.5 * y2, m01 = 0.5 * y0 + 0.5 * y1;
+    const double add[4][3] = {{m20, m12, y2}, {m12, m20, m01}, {y0, m01, m20}, {m01, y1, m12}};
+    const int4 ch = children[c & ((1ll << nsubc_log2) - 1)];
+    const int64_t fb = (c >> nsubc_log2) << (nsubc_log2 + 2);
+    const int64_t f[4] = {fb + ch.x, fb + ch.y, fb + ch.z, fb + ch.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) T[i * pitch_f + f[q]] = T[i * pitch_f + f[q]] + add[q][i];
 }
 
 // Level-1 right-hand side + time-step start (:316-317, :593, get_RHS :452-464):
@@ -660,15 +681,23 @@ hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int s
     return hipGetLastError();
 }
 
-hipError_t launch_residual(hipStream_t s, const Level &L, double rdt) {
+hipError_t launch_residual(hipStream_t s, const Level &L, double rdt, bool neg) {
     const int64_t npairs = L.N / 2;
     if (npairs == 0) return hipSuccess;
-    if (L.arith == 1)
-        hipLaunchKernelGGL(k_residual<StcF>, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.RHS, L.RES, L.stc,
-                           L.pitch, npairs, log2i(L.nsub), rdt);
-    else
-        hipLaunchKernelGGL(k_residual<Stc>, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.RHS, L.RES, L.stc,
-                           L.pitch, npairs, log2i(L.nsub), rdt);
+#define PAMG_RES(ST, NEG)                                                                                          \
+    hipLaunchKernelGGL((k_residual<ST, NEG>), dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.RHS, L.RES, L.stc, \
+                       L.pitch, npairs, log2i(L.nsub), rdt)
+    if (L.arith == 1) { if (neg) PAMG_RES(StcF, true); else PAMG_RES(StcF, false); }
+    else if (neg) PAMG_RES(Stc, true);
+    else PAMG_RES(Stc, false);
+#undef PAMG_RES
+    return hipGetLastError();
+}
+
+hipError_t launch_interp_add(hipStream_t s, const Level &fine, const Level &coarse) {
+    if (coarse.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_interp_add, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.T, coarse.T, fine.children,
+                       fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub));
     return hipGetLastError();
 }
 

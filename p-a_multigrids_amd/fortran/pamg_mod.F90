@@ -22,7 +22,8 @@ module pamg
     integer(c_int) :: coarse_solver
     integer(c_int) :: arith
     integer(c_int) :: halo_exchange
-    integer(c_int) :: reserved(3)
+    integer(c_int) :: cycle
+    integer(c_int) :: reserved(2)
   end type pamg_params
 
   public :: pamg_default_params, pamg_msh_read, pamg_msh_size, pamg_msh_get, pamg_msh_free

@@ -25,10 +25,10 @@ program pamg_transport
 
   character(len=512) :: mesh_file = 'untitled8.msh', dump = ''
   integer :: n_split = 1, multi_levels = 1, n_smooth = 4, solver = 3, ntime = 2, n_multigrid = 2
-  integer :: device = 0, call_sites = 1, facade_sweeps = 0, vtk_interval = 0, vtk_io
+  integer :: device = 0, call_sites = 1, facade_sweeps = 0, vtk_interval = 0, vtk_io, cycle = 0
   character(len=64) :: vtu_name
   namelist /transport/ mesh_file, n_split, multi_levels, n_smooth, solver, ntime, n_multigrid, device, dump, &
-       call_sites, facade_sweeps, vtk_interval
+       call_sites, facade_sweeps, vtk_interval, cycle
 
   character(len=512) :: cfg
   type(c_ptr) :: m = c_null_ptr, h = c_null_ptr
@@ -66,6 +66,7 @@ program pamg_transport
   p%n_smooth = n_smooth
   p%solver = solver
   p%device = device
+  p%cycle = cycle                 ! 1: the corrected V-cycle (pamg.h), used by pamg_run (call_sites = 0)
   call pamg_check(pamg_create(p, h), c_null_ptr, 'pamg_create')
   call pamg_check(pamg_upload_mesh(h, U, X, region, neig, fneig, dir), h, 'pamg_upload_mesh')
 

@@ -60,7 +60,7 @@ def lib():
         for name in ("orc_copy_to_tnn", "orc_smoother", "orc_get_residual", "orc_restrictor",
                      "orc_prolongator", "orc_update_overlaps", "orc_direct_solve"):
             getattr(L, name).argtypes = [P, C.c_int]
-        for name in ("orc_begin_timestep", "orc_vcycle", "orc_run"):
+        for name in ("orc_begin_timestep", "orc_vcycle", "orc_run", "orc_vcycle_corrected"):
             getattr(L, name).argtypes = [P]
         _lib = L
     return _lib
@@ -142,6 +142,7 @@ class Oracle:
     def direct_solve(self, l): self.L.orc_direct_solve(self.h, l)
     def begin_timestep(self): self.L.orc_begin_timestep(self.h)
     def vcycle(self): self.L.orc_vcycle(self.h)
+    def vcycle_corrected(self): self.L.orc_vcycle_corrected(self.h)
     def run(self): self.L.orc_run(self.h)
 
     def state(self):
