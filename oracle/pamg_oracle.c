@@ -76,7 +76,7 @@ static void get_str_info(int n_split, int ele, int *irow, int *ipos, int *orient
 static void get_splitting(const double *un_x, int n_split, int str_ele, double str_x[3][2]) {
     double p = (double)(1 << n_split);
     double v1[2], v2[2];
-    int irow, ipos, orient;
+    int irow = 0, ipos = 0, orient = 0;
     v1[0] = (un_x[0] - un_x[4]) / p;
     v1[1] = (un_x[1] - un_x[5]) / p;
     v2[0] = (un_x[2] - un_x[4]) / p;
@@ -101,7 +101,7 @@ static double boundary(double a, double b) { return sin(a + b); }
 
 /* splitting.F90:97-140 element_conversion; fin_ele 1-based */
 static void element_conversion(int fin[4], int coarse_ele, int i_split) {
-    int irow, ipos, orient, counter, tot_fine = 0;
+    int irow = 0, ipos = 0, orient = 0, counter, tot_fine = 0;
     int rowx = (1 << (i_split + 1)) * 2 - 1;
     get_str_info(i_split, coarse_ele, &irow, &ipos, &orient);
     if (orient == 1) {
@@ -380,7 +380,7 @@ static void update_overlaps(orc_state *s, int l) {
         for (int fo = 0; fo < 3; ++fo) {
             int f = face_order[fo];
             for (int i = 1; i <= m; ++i) {
-                int se = surf[(i - 1) + (f - 1) * m], irow, ipos, orient;
+                int se = surf[(i - 1) + (f - 1) * m], irow = 0, ipos = 0, orient = 0;
                 get_str_info(i_split, se, &irow, &ipos, &orient);
                 int npos = s->neig[3 * u + f - 1];
                 double xl[3][2];
