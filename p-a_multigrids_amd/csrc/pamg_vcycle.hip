@@ -51,7 +51,11 @@ using namespace detail;
 // 2**(TL-1) threads, one adjacent pair each. TL = max(2 n_split, PAMG_FINE_TL_MIN) = 10: 1024
 // sub-elements, 512 threads (one un_ele at n_split = 5). Measured (scripts/ab2.sh): 256-element
 // tiles (PAMG_FINE_TL_MIN=8, 4x the workgroups at n_split <= 4) are 7-9 % slower at n_split = 3
-// and 4, and forcing 8 waves per SIMD (PAMG_FINE_WAVES=8, <= 64 VGPRs) 0.5-50 % slower.
+// and 4. Occupancy: the kernel wants 71 VGPRs (7 waves per SIMD, 3 workgroups per CU); bounded
+// to 64 (W8: 8 waves, 4 workgroups per CU) it is 0.8 % slower on a full mesh but fits 1,024
+// workgroups -- a rank's share of untitled8192 on 8 GPUs -- in one round instead of two
+// (0.0350 -> 0.0312 ms per cycle, scripts/ab_strong.sh): launches of at most
+// PAMG_W8_MAX_GRID workgroups use the W8 instance (n_split >= 3).
 #ifndef PAMG_FINE_TL_MIN
 #define PAMG_FINE_TL_MIN 10
 #endif
@@ -559,11 +563,8 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
 // ===================================================================== level 0
 // Ownership: the adjacent pair 2t, 2t+1 of the tile (16-byte accesses, one un_ele,
 // one operator record); for the prolongator, level-1 sub-element t.
-template <int S, int L, class ST, bool PIPE>
-#ifndef PAMG_FINE_WAVES
-#define PAMG_FINE_WAVES 4
-#endif
-__global__ __launch_bounds__(fine_mt(S), (S >= 3) ? PAMG_FINE_WAVES : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0,
+template <int S, int L, class ST, bool PIPE, bool W8>
+__global__ __launch_bounds__(fine_mt(S), (S >= 3) ? (W8 ? 8 : 4) : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0,
                                                                       const double *__restrict__ sp1,
                                                                       const double *__restrict__ sp2,
                                                                       const double *__restrict__ sp3,
@@ -673,8 +674,8 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? PAMG_FINE_WAVES : 2) void k_
 }
 
 // part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
-template <int S, int L, class ST>
-hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
+template <int S, int L, class ST, bool W8>
+hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     if (part == 1) {
         if constexpr (L >= 2)
             hipLaunchKernelGGL((k_vc_coarse<S, L, ST>), dim3(grid), dim3(kMTc), 0, s, A, A.lv[1].stc, A.lv[2].stc,
@@ -683,15 +684,26 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
             return hipErrorInvalidValue;
     } else if (part == 2) {
         if constexpr (L >= 2)
-            hipLaunchKernelGGL((k_vc_fine<S, L, ST, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
+            hipLaunchKernelGGL((k_vc_fine<S, L, ST, true, W8>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
                                A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         else
             return hipErrorInvalidValue;
     } else {
-        hipLaunchKernelGGL((k_vc_fine<S, L, ST, false>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc, nullptr,
+        hipLaunchKernelGGL((k_vc_fine<S, L, ST, false, W8>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc, nullptr,
                            nullptr, nullptr, nullptr);
     }
     return hipGetLastError();
+}
+
+#ifndef PAMG_W8_MAX_GRID
+#define PAMG_W8_MAX_GRID 1024
+#endif
+template <int S, int L, class ST>
+hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
+    static const long w8_max = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : PAMG_W8_MAX_GRID;
+    if constexpr (S >= 3)
+        if (part != 1 && (long)grid <= w8_max) return launch_sltw<S, L, ST, true>(s, A, grid, part);
+    return launch_sltw<S, L, ST, false>(s, A, grid, part);
 }
 
 // operator arithmetic (pamg_params.arith): the reference's order, or the contracted form
