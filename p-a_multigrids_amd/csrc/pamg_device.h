@@ -15,21 +15,21 @@ constexpr int kBlock = 256;
 // The state planes are streamed once per launch (1.2 GB per cycle at n_split = 5, far past the
 // 256 MiB Infinity Cache): 16-byte lanes use non-temporal loads and stores (global_load /
 // global_store ... nt). Measured on MI355X: the pipelined V-cycle launch 0.244 -> 0.207 ms
-// (4.9 -> 6.1 TB/s), the per-step sequence 0.87 -> 0.76 ms per cycle. PAMG_NT=0 builds the
-// plain form for A/B timing.
+// (4.9 -> 6.1 TB/s), the per-step sequence 0.87 -> 0.76 ms per cycle. PAMG_NT is a mask for
+// A/B builds: bit 0 non-temporal loads, bit 1 non-temporal stores (0: plain).
 #ifndef PAMG_NT
-#define PAMG_NT 1
+#define PAMG_NT 3
 #endif
 typedef double v2d_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double2 ld2(const double *p) {
-    if (PAMG_NT) {
+    if (PAMG_NT & 1) {
         const v2d_t v = __builtin_nontemporal_load(reinterpret_cast<const v2d_t *>(p));
         return make_double2(v.x, v.y);
     }
     return *reinterpret_cast<const double2 *>(p);
 }
 __device__ __forceinline__ void st2(double *p, double2 v) {
-    if (PAMG_NT) {
+    if (PAMG_NT & 2) {
         const v2d_t w = {v.x, v.y};
         __builtin_nontemporal_store(w, reinterpret_cast<v2d_t *>(p));
         return;

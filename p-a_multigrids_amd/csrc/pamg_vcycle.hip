@@ -143,7 +143,7 @@ __device__ __forceinline__ void load3p(const double *f, int64_t pitch, uint32_t 
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const v2d *q = reinterpret_cast<const v2d *>(reinterpret_cast<const char *>(f + c * pitch) + o);
-        const v2d v = PAMG_NT ? __builtin_nontemporal_load(q) : *q;
+        const v2d v = (PAMG_NT & 1) ? __builtin_nontemporal_load(q) : *q;
         a[c] = v.x;
         b[c] = v.y;
     }
@@ -154,7 +154,7 @@ __device__ __forceinline__ void store3p(double *f, int64_t pitch, uint32_t s, co
     for (int c = 0; c < 3; ++c) {
         v2d *q = reinterpret_cast<v2d *>(reinterpret_cast<char *>(f + c * pitch) + o);
         const v2d v = {a[c], b[c]};
-        if (PAMG_NT) __builtin_nontemporal_store(v, q);
+        if (PAMG_NT & 2) __builtin_nontemporal_store(v, q);
         else *q = v;
     }
 }
