@@ -208,6 +208,13 @@ def main():
             extra["sweep_assembled" if asm else "sweep_stencil"] = dict(
                 ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
                 frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
+        # the time loop as the reference drives it (:299-381): ntime steps of begin_timestep
+        # (told, tnew_nonlin, level-1 RHS) + n_multigrid = 2 V-cycles each
+        s.synchronize()
+        t0 = time.perf_counter()
+        s.run(10, 2)
+        s.synchronize()
+        extra["time_loop_ntime10_nmg2_vcycles_per_s"] = round(20 / (time.perf_counter() - t0), 1)
         # the matrices.F90 SpMV (csr_mul_array, 3 entries per row) over the level-1 operator's
         # size in the reference's block numbering: 3 N1 rows, 52 B per row (3 x (4 B column +
         # 8 B value), 8 B result, 8 B of the gathered vector)
