@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the n_split=3 and sweep-kernel side measurements")
     ap.add_argument("--halo-mode", type=int, default=0)
+    ap.add_argument("--comm", choices=["rccl", "detached"], default="rccl",
+                    help="detached: partitions without the RCCL exchange -- a check of the multi-process "
+                         "orchestration on a one-GPU box (ranks share the GPU; timings are not a result)")
     ap.add_argument("--halo-exchange", type=int, default=0,
                     help="multi-rank: 0 exchange the level-1 halo once per pamg_vcycle call (after its last "
                          "cycle), 1 after every cycle")
@@ -141,7 +144,9 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     mesh = pamg.Mesh.read(a.mesh)
     comm = None
-    if world > 1:
+    if world > 1 and a.comm == "detached":   # orchestration check on one GPU: no RCCL, no exchange
+        comm = (world, rank, None, mesh.x_strip_owner(world))
+    elif world > 1:
         obj = [pamg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = (world, rank, obj[0], mesh.x_strip_owner(world))
@@ -284,7 +289,8 @@ def main():
                        "fine_sub_elements": mesh.U * 4 ** a.nsplit, "levels": a.levels,
                        "parallelism": f"dd{world}", "halo_mode": a.halo_mode,
                        "arith": "contracted (fma, 1e-15 of the reference)" if a.arith else "reference order (bitwise)",
-                       "fused": a.fused, "halo_exchange": "per call" if a.halo_exchange == 0 else "per cycle"},
+                       "fused": a.fused, "halo_exchange": "per call" if a.halo_exchange == 0 else "per cycle",
+                       "comm": a.comm if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": RK_DESC[rk],
                          "events": "timed region" if live_events else "post-pass of min(steps, 20) cycles",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
