@@ -13,8 +13,11 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 mesh = pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "untitled8192.msh"))
 out = []
 for c in sys.argv[1:] or ["5,3,3,1"]:
-    S, L, fused, arith = (int(x) for x in c.split(","))
-    s = pamg.SemiImplicitIterative(mesh, S, L, n_smooth=4, solver=3, fused=fused, arith=arith)
+    v = [int(x) for x in c.split(",")]
+    S, L, fused, arith = v[:4]
+    N = v[4] if len(v) > 4 else 1   # rank 0's x-strip partition of N (detached, no exchange)
+    comm = None if N == 1 else (N, 0, None, mesh.x_strip_owner(N))
+    s = pamg.SemiImplicitIterative(mesh, S, L, n_smooth=4, solver=3, fused=fused, arith=arith, comm=comm)
     s.begin_timestep()
     s.vcycle(5)
     s.synchronize()
