@@ -138,17 +138,19 @@ def test_full_size_against_oracle(mesh, S, L):
         assert goldens.rel_err(x, y) <= TOL
 
 
-@pytest.mark.parametrize("fused,exch", [(3, 0), (3, 1), (1, 0), (0, 0)])
-def test_partitioned_run_matches_single_gpu(fused, exch):
-    """Two partitions of untitled8192 (x-strips) on one GPU, halo exchanged by
-    the loopback path (the same packed segments RCCL carries between ranks);
-    exch = 0 packs the exchange once per pamg_vcycle call, 1 after every cycle."""
+@pytest.mark.parametrize("S,nparts,fused,exch", [(3, 2, 3, 0), (3, 2, 3, 1), (3, 2, 1, 0), (3, 2, 0, 0),
+                                                 (5, 8, 3, 0), (5, 8, 1, 1)])
+def test_partitioned_run_matches_single_gpu(S, nparts, fused, exch):
+    """Partitions of untitled8192 (x-strips) on one GPU, halo exchanged by the loopback
+    path (the same packed segments RCCL carries between ranks); exch = 0 packs the
+    exchange once per pamg_vcycle call, 1 after every cycle. n_split = 5 in 8 parts is
+    the 8-GPU bench's per-rank launch (1,024 workgroups: the 64-VGPR instance)."""
     mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
-    full = pamg.SemiImplicitIterative(mesh, 3, 3)
+    full = pamg.SemiImplicitIterative(mesh, S, 3)
     full.run(1, 3)
-    owner = mesh.x_strip_owner(2)
-    parts = [pamg.SemiImplicitIterative(mesh, 3, 3, comm=(2, r, None, owner), fused=fused, halo_exchange=exch)
-             for r in range(2)]
+    owner = mesh.x_strip_owner(nparts)
+    parts = [pamg.SemiImplicitIterative(mesh, S, 3, comm=(nparts, r, None, owner), fused=fused,
+                                        halo_exchange=exch) for r in range(nparts)]
     for p in parts:
         p.run(1, 3)
     halo_loopback(parts, 1)
