@@ -54,8 +54,7 @@ using namespace detail;
 // and 4. Occupancy: the kernel wants 71 VGPRs (7 waves per SIMD, 3 workgroups per CU); bounded
 // to 64 (W8: 8 waves, 4 workgroups per CU) it is 0.8 % slower on a full mesh but fits 1,024
 // workgroups -- a rank's share of untitled8192 on 8 GPUs -- in one round instead of two
-// (0.0350 -> 0.0312 ms per cycle, scripts/ab_strong.sh): launches of at most
-// PAMG_W8_MAX_GRID workgroups use the W8 instance (n_split >= 3).
+// (0.0350 -> 0.0312 ms per cycle, scripts/ab_strong.sh): see launch_slt.
 #ifndef PAMG_FINE_TL_MIN
 #define PAMG_FINE_TL_MIN 10
 #endif
@@ -695,14 +694,21 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     return hipGetLastError();
 }
 
-#ifndef PAMG_W8_MAX_GRID
-#define PAMG_W8_MAX_GRID 1024
-#endif
+// the 64-VGPR instance only where it saves a round: more workgroups than 3 per CU, at most 4
+// (at n_split = 3 the launch fits one round either way and the bounded instance is 50 %
+// slower; PAMG_W8_MAX_GRID=<n> overrides the upper bound for A/B runs)
 template <int S, int L, class ST>
 hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
-    static const long w8_max = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : PAMG_W8_MAX_GRID;
+    static const long n_cu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 256;
+        return (long)n;
+    }();
+    static const long w8_max = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : 4 * n_cu;
     if constexpr (S >= 3)
-        if (part != 1 && (long)grid <= w8_max) return launch_sltw<S, L, ST, true>(s, A, grid, part);
+        if (part != 1 && fine_mt(S) == 512 && (long)grid > 3 * n_cu && (long)grid <= w8_max)
+            return launch_sltw<S, L, ST, true>(s, A, grid, part);
     return launch_sltw<S, L, ST, false>(s, A, grid, part);
 }
 
