@@ -152,6 +152,8 @@ def main():
         comm = (world, rank, obj[0], mesh.x_strip_owner(world))
     ndev = max(1, torch.cuda.device_count())
     device = local % ndev
+    if torch.cuda.is_available():
+        torch.cuda.set_device(device)   # torch's own synchronize() then stays on this rank's GPU
     s = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
                                    halo_mode=a.halo_mode, comm=comm, fused=a.fused, arith=a.arith,
                                    halo_exchange=a.halo_exchange)
