@@ -59,7 +59,16 @@ using namespace detail;
 #define PAMG_FINE_TL_MIN 10
 #endif
 constexpr int fine_tl(int S) { return 2 * S > PAMG_FINE_TL_MIN ? 2 * S : PAMG_FINE_TL_MIN; }
-constexpr int fine_mt(int S) { return 1 << (fine_tl(S) - 1); }
+// level-0 sub-elements per thread: an adjacent pair (16-byte accesses); one at n_split <=
+// PAMG_NP1_MAX_S (A/B builds: twice the waves for the single-round launches of small n_split).
+// Measured (scripts/ab2.sh, parity-tested): equal at n_split = 2 and 3 (those launches stream
+// at ~5.3 TB/s plus ~2.8 us of launch overhead, scripts/micro/launch.hip), 37 % slower at
+// n_split = 4, L = 4 -- the pair stays everywhere
+#ifndef PAMG_NP1_MAX_S
+#define PAMG_NP1_MAX_S 0
+#endif
+constexpr int fine_np(int S) { return S <= PAMG_NP1_MAX_S ? 1 : 2; }
+constexpr int fine_mt(int S) { return (1 << fine_tl(S)) / fine_np(S); }
 constexpr int kMTc = 64;    // threads per workgroup, coarse-level kernel (one wave per tile)
 
 // the planes of a level are one allocation (pamg_api.cpp): tnew, tnew_nonlin, RHS,
@@ -113,12 +122,13 @@ struct Geo {
     static constexpr int C = L - 1;                                // coarsest level
     static constexpr int TL = fine_tl(S);
     static constexpr int T = 1 << TL;                              // level-0 sub-elements per tile
-    static constexpr int MT = T / 2;                               // threads of the level-1 launch
+    static constexpr int NP = fine_np(S);                          // level-0 sub-elements per thread
+    static constexpr int MT = T / NP;                              // threads of the level-1 launch
     static constexpr int GL = TL - 2 * S;                          // log2 un_eles per tile
     static constexpr int lg(int l) { return 2 * (S - l); }
     static constexpr int nt(int l) { return T >> (2 * l); }
-    // each wave inside one un_ele (a wave spans 128 level-0 sub-elements, 64 of any other level)
-    static constexpr bool uni(int l) { return lg(l) >= (l == 0 ? 7 : 6); }
+    // each wave inside one un_ele (a wave spans 64 NP level-0 sub-elements, 64 of any other level)
+    static constexpr bool uni(int l) { return lg(l) >= (l == 0 ? (NP == 2 ? 7 : 6) : 6); }
 };
 
 // field access: wave-uniform plane base (SGPRs) + 32-bit sub-element index (one VGPR for all planes)
@@ -563,7 +573,7 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
 // Ownership: the adjacent pair 2t, 2t+1 of the tile (16-byte accesses, one un_ele,
 // one operator record); for the prolongator, level-1 sub-element t.
 template <int S, int L, class ST, bool PIPE, bool W8>
-__global__ __launch_bounds__(fine_mt(S), (S >= 3) ? (W8 ? 8 : 4) : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0,
+__global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8 : 4) : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0,
                                                                       const double *__restrict__ sp1,
                                                                       const double *__restrict__ sp2,
                                                                       const double *__restrict__ sp3,
@@ -573,7 +583,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? (W8 ? 8 : 4) : 2) void k_vc_
     static_assert(!PIPE || C > 0, "the pipelined launch needs a coarse level");
     // F0 | M0: restriction-leg tnew image and residual means (restrictor input) of level 1;
     // the pipelined tail reuses the region for the coarse levels' images
-    constexpr int T = G::T, MT = G::MT;
+    constexpr int T = G::T, MT = G::MT, NP = G::NP;
     __shared__ __attribute__((aligned(16))) double F0[C > 0 ? 4 * T : 1];
     double *const M0 = F0 + 3 * T;
     const int t = threadIdx.x;
@@ -584,32 +594,47 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? (W8 ? 8 : 4) : 2) void k_vc_
     stamp<MT>(A, 0);
     stamp_hwid<MT>(A);
     const VLevel &V0 = A.lv[0];
-    const bool v0 = 2 * t < (nue << G::lg(0));
-    const uint32_t s0 = ((uint32_t)u0 << G::lg(0)) + (v0 ? 2 * t : 0);   // clamped: loads stay in bounds
-    const uint32_t w0 = s0 >> G::lg(0);                                  // un_ele of the pair
+    const bool v0 = NP * t < (nue << G::lg(0));
+    const uint32_t s0 = ((uint32_t)u0 << G::lg(0)) + (v0 ? NP * t : 0);   // clamped: loads stay in bounds
+    const uint32_t w0 = s0 >> G::lg(0);                                   // un_ele of the thread's sub-elements
     // ---- prologue
-    int h0[2];
+    int h0[NP];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) h0[k] = v0 ? hs_pack(V0.H.hsub[(s0 + k) & ((1 << G::lg(0)) - 1)]) : 0;
-    double x0[2][3], b0[2][3], p0[2][3];
-    load3p(V0.T(), V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
-    load3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
+    for (int k = 0; k < NP; ++k) h0[k] = v0 ? hs_pack(V0.H.hsub[(s0 + k) & ((1 << G::lg(0)) - 1)]) : 0;
+    double x0[NP][3], b0[NP][3], p0[NP][3];
+    if constexpr (NP == 2) {
+        load3p(V0.T(), V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
+        load3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
+    } else {
+        load3(V0.T(), V0.pitch, s0, x0[0]);
+        load3(V0.RHS(), V0.pitch, s0, b0[0]);
+    }
     ST St;
     stencil(G::uni(0), sp0, w0, St);
     // ---- restriction leg: smoother (:331), get_residual (:338)
-    sweeps2(St, rdt, ns, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
+    if constexpr (NP == 2) sweeps2(St, rdt, ns, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
+    else sweepsN<1>(St, rdt, ns, b0, x0, p0);
     stamp<MT>(A, 1);
     if (v0) {
-        if constexpr (C > 0)
+        double r[NP][3];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) *reinterpret_cast<double2 *>(F0 + c * T + 2 * t) = make_double2(p0[0][c], p0[1][c]);
-        double r[2][3];
+        for (int k = 0; k < NP; ++k) residual(St, rdt, p0[k], b0[k], r[k]);
+        if constexpr (NP == 2) {
+            if constexpr (C > 0)
 #pragma unroll
-        for (int k = 0; k < 2; ++k) residual(St, rdt, p0[k], b0[k], r[k]);
-        store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
-        if constexpr (C > 0)   // restrictor input: mean of the residual components (splitting.F90:146-151)
-            *reinterpret_cast<double2 *>(M0 + 2 * t) =
-                make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
+                for (int c = 0; c < 3; ++c)
+                    *reinterpret_cast<double2 *>(F0 + c * T + 2 * t) = make_double2(p0[0][c], p0[1][c]);
+            store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
+            if constexpr (C > 0)   // restrictor input: mean of the residual components (splitting.F90:146-151)
+                *reinterpret_cast<double2 *>(M0 + 2 * t) =
+                    make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
+        } else {
+            if constexpr (C > 0)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) F0[c * T + t] = p0[0][c];
+            store3(V0.RES(), V0.pitch, s0, r[0]);
+            if constexpr (C > 0) M0[t] = (r[0][0] + r[0][1] + r[0][2]) / 3.;
+        }
     }
     stamp<MT>(A, 2);
     // level-1 sub-element t: its final tnew (coarse launch) for the prolongator, its children
@@ -630,18 +655,24 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? (W8 ? 8 : 4) : 2) void k_vc_
     }
     // ---- prolongation leg (:367-376) from the restriction-leg tnew; with one level,
     //      the 15 coarse smoother calls (:344-359)
-    copy3(x0[0], p0[0]);
-    copy3(x0[1], p0[1]);
-    sweeps2(St, rdt, C > 0 ? ns : ns * A.n_coarse, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) copy3(x0[k], p0[k]);
+    if constexpr (NP == 2) sweeps2(St, rdt, C > 0 ? ns : ns * A.n_coarse, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
+    else sweepsN<1>(St, rdt, C > 0 ? ns : ns * A.n_coarse, b0, x0, p0);
     stamp<MT>(A, 3);
     if (v0) {
         // the cycle's halo words (update_overlaps, :555), all written here (see the header);
         // halo records by vector loads: the boundary lanes are few, and scalar copies of the
         // records would push the kernel past 80 SGPRs (7 instead of 8 waves per SIMD)
 #pragma unroll
-        for (int k = 0; k < 2; ++k) hs_write(false, V0.H, w0, h0[k], p0[k]);
-        store3p(V0.T(), V0.pitch, s0, p0[0], p0[1]);
-        store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
+        for (int k = 0; k < NP; ++k) hs_write(false, V0.H, w0, h0[k], p0[k]);
+        if constexpr (NP == 2) {
+            store3p(V0.T(), V0.pitch, s0, p0[0], p0[1]);
+            store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
+        } else {
+            store3(V0.T(), V0.pitch, s0, p0[0]);
+            store3(V0.TNN(), V0.pitch, s0, x0[0]);
+        }
     }
     stamp<MT>(A, 4);
     // ---- prolongator (:370) on the LDS image (its result is dead, :550), and the restrictor
@@ -657,7 +688,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? (W8 ? 8 : 4) : 2) void k_vc_
                 const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
                 prolong_cascade(F0, T, fi, y1);
             }
-            if (PIPE ? casc : !casc) {
+            if (PIPE ? casc : (!casc && t < 2 * G::nt(1))) {
                 rn[0] = M0[base + c4.z];
                 rn[1] = M0[base + c4.w];
                 rn[2] = M0[base + c4.x];
@@ -763,7 +794,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     if (grid == 0) return hipSuccess;
     // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_VCYCLE_STAMPS") : nullptr;
-    const int waves = coarse ? kMTc / 64 : (1 << fine_tl(n_split)) / 128;
+    const int waves = coarse ? kMTc / 64 : fine_mt(n_split) / 64;
     const size_t nst = (size_t)grid * waves * kStampSlots;
     if (stamp_path) {
         hipError_t e = hipMalloc(&A.stamps, nst * sizeof(long long));
