@@ -168,6 +168,12 @@ int pamg_synchronize(pamg_handle *h);
 /* enable HIP-event timing of the kernel classes in `mask` (bit PAMG_K_*) */
 int pamg_timing_enable(pamg_handle *h, unsigned mask);
 int pamg_timing_reset(pamg_handle *h);
+/* record events around one launch in `every` of each enabled class (the first after a reset,
+ * then every `every`-th); timing_read then reports the sampled launches. A HIP event pair
+ * between back-to-back launches costs ~10 us; bench.py samples 1 in 10. */
+int pamg_timing_stride(pamg_handle *h, int every);
+/* launches of class `kid` issued since the reset while its timing was enabled (sampled or not) */
+int pamg_timing_issued(pamg_handle *h, int kid, long *issued);
 /* total ms, launches and algorithmic HBM bytes of kernel class `kid` since reset */
 int pamg_timing_read(pamg_handle *h, int kid, double *ms_total, long *launches, double *bytes_total);
 /* the unfused level-1 roofline kernel: `sweeps` launches of one smoother sweep

@@ -86,7 +86,10 @@ struct Span {
     pamg_handle *h; int kid; double bytes; hipStream_t s; hipEvent_t a = nullptr;
     Span(pamg_handle *h_, int kid_, double bytes_, hipStream_t s_ = nullptr)
         : h(h_), kid(kid_), bytes(bytes_), s(s_ ? s_ : h_->stream) {
-        if (h->timing.mask & (1u << kid)) { a = take_event(h); (void)hipEventRecord(a, s); }
+        if ((h->timing.mask & (1u << kid)) && h->timing.seq[kid]++ % h->timing.stride == 0) {
+            a = take_event(h);
+            (void)hipEventRecord(a, s);
+        }
     }
     ~Span() {
         if (!a) return;
@@ -870,7 +873,15 @@ int pamg_timing_enable(pamg_handle *h, unsigned mask) {
 int pamg_timing_reset(pamg_handle *h) {
     if (!h) return PAMG_ERR_ARG;
     CHK(drain_timing(h));
-    for (int k = 0; k < PAMG_K_COUNT; ++k) { h->timing.ms[k] = 0; h->timing.count[k] = 0; h->timing.bytes[k] = 0; }
+    for (int k = 0; k < PAMG_K_COUNT; ++k) {
+        h->timing.ms[k] = 0; h->timing.count[k] = 0; h->timing.bytes[k] = 0; h->timing.seq[k] = 0;
+    }
+    return PAMG_OK;
+}
+
+int pamg_timing_stride(pamg_handle *h, int every) {
+    if (!h || every < 1) return PAMG_ERR_ARG;
+    h->timing.stride = every;
     return PAMG_OK;
 }
 
@@ -880,6 +891,12 @@ int pamg_timing_read(pamg_handle *h, int kid, double *ms_total, long *launches, 
     if (ms_total) *ms_total = h->timing.ms[kid];
     if (launches) *launches = h->timing.count[kid];
     if (bytes_total) *bytes_total = h->timing.bytes[kid];
+    return PAMG_OK;
+}
+
+int pamg_timing_issued(pamg_handle *h, int kid, long *issued) {
+    if (!h || !issued || kid < 0 || kid >= PAMG_K_COUNT) return PAMG_ERR_ARG;
+    *issued = h->timing.seq[kid];
     return PAMG_OK;
 }
 

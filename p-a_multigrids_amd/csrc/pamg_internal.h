@@ -91,6 +91,10 @@ struct Level {
 
 struct Timing {
     unsigned mask = 0;
+    // events around one launch in `stride` of each kernel class (the first, then every
+    // stride-th): a HIP event pair costs ~10 us between back-to-back launches
+    int stride = 1;
+    long seq[PAMG_K_COUNT] = {0};
     struct Rec { int kid; hipEvent_t a, b; double bytes; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;

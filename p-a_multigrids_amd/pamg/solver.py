@@ -183,13 +183,16 @@ class SemiImplicitIterative:
     # ---- measurement ------------------------------------------------------
     def timing_enable(self, mask): self._call("pamg_timing_enable", mask)
     def timing_reset(self): self._call("pamg_timing_reset")
+    def timing_stride(self, every): self._call("pamg_timing_stride", every)
 
     def timing(self):
         out = {}
         for kid, name in enumerate(K_NAMES):
             ms, n, by = C.c_double(), C.c_long(), C.c_double()
             self._call("pamg_timing_read", kid, C.byref(ms), C.byref(n), C.byref(by))
-            out[name] = dict(ms=ms.value, launches=n.value, bytes=by.value)
+            iss = C.c_long()
+            self._call("pamg_timing_issued", kid, C.byref(iss))
+            out[name] = dict(ms=ms.value, launches=n.value, bytes=by.value, issued=iss.value)
         return out
 
     def sweep_bench(self, sweeps, assembled):
