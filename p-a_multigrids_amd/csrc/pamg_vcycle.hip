@@ -736,7 +736,10 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
             n = 256;
         return (long)n;
     }();
-    static const long w8_max = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : 4 * n_cu;
+    // (the reference's operation order, Stc, issues 3x the fp64 work and gains from the extra
+    // wave at any size: 0.2678 -> 0.2560 ms per full-mesh cycle)
+    static const long w8_env = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : -1;
+    const long w8_max = w8_env >= 0 ? w8_env : (std::is_same<ST, Stc>::value ? (1l << 40) : 4 * n_cu);
     if constexpr (S >= 3)
         if (part != 1 && fine_mt(S) == 512 && (long)grid > 3 * n_cu && (long)grid <= w8_max)
             return launch_sltw<S, L, ST, true>(s, A, grid, part);
