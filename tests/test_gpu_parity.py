@@ -365,3 +365,24 @@ def test_contracted_fused_equals_kernel_sequence_bitwise(mesh, S, L, ns, fused):
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
     for x, y in zip(a.overlap(), b.overlap()):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("mesh,S,L", [("untitled8192.msh", 5, 3), ("irregular.msh", 4, 4), ("900_ele.msh", 3, 2)])
+@pytest.mark.parametrize("arith", [0, 1])
+def test_pipelined_call_boundaries_are_invisible(mesh, S, L, arith):
+    """fused = 3 pipelines the cycles of one pamg_vcycle call (coarse levels one cycle ahead
+    inside the call): one call of 5 cycles, five calls of one, and calls of 2 + 3 leave the
+    same state, bit for bit."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    runs = []
+    for split in ([5], [1] * 5, [2, 3]):
+        s = pamg.SemiImplicitIterative(m, S, L, arith=arith, fused=3)
+        s.begin_timestep()
+        for n in split:
+            s.vcycle(n)
+        st = s.state()
+        st["t_overlap"], st["t_overlap_old"] = s.overlap()
+        runs.append(st)
+    for st in runs[1:]:
+        for k in runs[0]:
+            np.testing.assert_array_equal(st[k], runs[0][k], err_msg=k)
