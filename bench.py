@@ -52,8 +52,11 @@ EVENT_STRIDE = 10   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 200 warm-up cycles (~30 ms): after 5 (~1 ms) the GPU's clocks have not settled and the
+    # timed region reads 6,550 instead of 7,460 V-cycles/s on the same box
+    # (scripts/event_probe.py, profiles/r01_v15_warmup.txt)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--nsplit", type=int, default=5)
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--nsmooth", type=int, default=4)

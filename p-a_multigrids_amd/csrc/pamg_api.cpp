@@ -301,9 +301,21 @@ double vcycle_coarse_bytes(pamg_handle *h) {
     return b + 104.0 * h->U * (L - 1);
 }
 //   pipelined launch: both, less level 2's RHSN (written and read: 48 B) and its tnew read
-//                     by the coarse part (the level-1 part's read serves both: 24 B)
-double vcycle_pipe_bytes(pamg_handle *h) {
-    return vcycle_fine_bytes(h) + vcycle_coarse_bytes(h) - 72.0 * h->lv[2].N;
+//                     by the coarse part (the level-1 part's read serves both: 24 B), less
+//                     the dead-until-final stores it skips (keep, PAMG_KEEP_*): level 1's
+//                     residual and tnew_nonlin (48 B), the coarse levels' RHS and residual
+//                     (48 B); the halo words are not counted anywhere
+double vcycle_pipe_bytes(pamg_handle *h, int keep) {
+    double b = vcycle_fine_bytes(h) + vcycle_coarse_bytes(h) - 72.0 * h->lv[2].N;
+    if (!(keep & PAMG_KEEP_L1)) b -= 48.0 * h->lv[1].N;
+    if (!(keep & PAMG_KEEP_COARSE))
+        for (int l = 2; l <= h->p.multi_levels; ++l) b -= 48.0 * h->lv[l].N;
+    return b;
+}
+// PAMG_PIPE_KEEP=<mask> forces stores into every pipelined launch (A/B runs; 7 = all)
+int pipe_keep_env() {
+    static const int k = getenv("PAMG_PIPE_KEEP") ? atoi(getenv("PAMG_PIPE_KEEP")) & PAMG_KEEP_ALL : 0;
+    return k;
 }
 
 // the exact local solve of level l (coarse_solver = 1): tnew = tnew_nonlin = A_e^-1 RHS, with
@@ -453,9 +465,15 @@ int vcycle_fused(pamg_handle *h, int n) {
         }
         {
             const bool pc = pipe && c + 1 < n;   // also the coarse levels of cycle c + 1
-            Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE, pc ? vcycle_pipe_bytes(h) : vcycle_fine_bytes(h));
+            // its stores that the rest of the call overwrites unread are skipped: level 1's
+            // residual and tnew_nonlin always (the call's last launch is k_vc_fine, which stores
+            // them), the coarse levels' RHS and residual unless they reach their final cycle
+            // here, the halo words unless every cycle's are exchanged
+            const int keep = pipe_keep_env() | (c + 2 == n ? PAMG_KEEP_COARSE : 0) |
+                             (h->p.halo_exchange == 1 ? PAMG_KEEP_HALO : 0);
+            Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE, pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h));
             HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr, pc));
+                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr, pc, keep));
             if (conc) HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));
         }
         if (L > 1) L2.RHSN = rhsn_w;   // the next cycle's level-2 RHS

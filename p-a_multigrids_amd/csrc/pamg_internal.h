@@ -180,10 +180,12 @@ hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, in
 // level 1; its remote halo words packed into send1 (one of level 1's two send buffers), the
 // restriction of its residual into rhsn2
 // pipe: the same launch also runs the coarse levels of the next cycle (L >= 2; level 2's RHS
-// from LDS, rhsn2 unused)
+// from LDS, rhsn2 unused); keep: which of its dead-until-final stores it makes
+// (PAMG_KEEP_*, pamg_vcycle.hip)
+constexpr int PAMG_KEEP_L1 = 1, PAMG_KEEP_COARSE = 2, PAMG_KEEP_HALO = 4, PAMG_KEEP_ALL = 7;
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                              bool pipe = false);
+                              bool pipe = false, int keep = PAMG_KEEP_ALL);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 // FINDInv (matrix_inversion.F90:50-148) batched, n <= 8, column-major (n, n, nb)

@@ -93,7 +93,19 @@ struct VArgs {
     double rdt;
     double *rhsn2;          // level 2's RHSN buffer: read by the coarse launch, written by the level-1 launch
     long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
+    int keep;               // pipelined launch: the dead-until-final stores it makes (kKeep*)
 };
+
+// Stores of a pipelined launch whose values the rest of the call overwrites before any read
+// ("final-cycle stores"): level 1's residual and tnew_nonlin (the next launch
+// rewrites both; the residual's one reader, the restrictor, takes it from LDS here), the
+// coarse levels' RHS and residual (rewritten by the next launch's coarse part; read from
+// registers and LDS in this one) and the halo words (rewritten every cycle; exchanged after
+// the call's last cycle with halo_exchange = 0). The call's final level-1 launch (k_vc_fine,
+// PIPE = false) stores all of level 1's fields and halo words; its last pipelined launch, the
+// one that leaves the coarse levels at their final cycle, keeps kKeepCoarse.
+constexpr int kKeepL1 = PAMG_KEEP_L1, kKeepCoarse = PAMG_KEEP_COARSE, kKeepHalo = PAMG_KEEP_HALO,
+              kKeepAll = PAMG_KEEP_ALL;
 
 // phase stamps: 100 MHz wall clock per wave at the phase boundaries, plus the wave's HW_ID
 // (diagnostics build only: make PAMG_STAMPS=1; the pointer costs SGPRs the kernels need)
@@ -518,7 +530,8 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
             load3(V.T(), V.pitch, gx, x);
             load3(V.RHSN(), V.pitch, gx, b);
         }
-        if (v) store3(V.RHS(), V.pitch, gx, b);
+        const bool keep = A.keep & kKeepCoarse;
+        if (v && keep) store3(V.RHS(), V.pitch, gx, b);
         stencil(G::uni(l), SP[l], gx >> G::lg(l), St);
         if constexpr (l >= 2) c4 = V.children[gx & ((1 << G::lg(l)) - 1)];
         for (int it = 0; it < ns; ++it) {
@@ -527,7 +540,7 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
         }
         double r[3];
         residual(St, rdt, p, b, r);
-        if (v) store3(V.RES(), V.pitch, gx, r);
+        if (v && keep) store3(V.RES(), V.pitch, gx, r);
         if constexpr (l < C) {
             if (v) {
 #pragma unroll
@@ -594,6 +607,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     stamp<MT>(A, 0);
     stamp_hwid<MT>(A);
     const VLevel &V0 = A.lv[0];
+    const bool keep1 = !PIPE || (A.keep & kKeepL1), keeph = !PIPE || (A.keep & kKeepHalo);
     const bool v0 = NP * t < (nue << G::lg(0));
     const uint32_t s0 = ((uint32_t)u0 << G::lg(0)) + (v0 ? NP * t : 0);   // clamped: loads stay in bounds
     const uint32_t w0 = s0 >> G::lg(0);                                   // un_ele of the thread's sub-elements
@@ -624,7 +638,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 #pragma unroll
                 for (int c = 0; c < 3; ++c)
                     *reinterpret_cast<double2 *>(F0 + c * T + 2 * t) = make_double2(p0[0][c], p0[1][c]);
-            store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
+            if (keep1) store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
             if constexpr (C > 0)   // restrictor input: mean of the residual components (splitting.F90:146-151)
                 *reinterpret_cast<double2 *>(M0 + 2 * t) =
                     make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
@@ -632,7 +646,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
             if constexpr (C > 0)
 #pragma unroll
                 for (int c = 0; c < 3; ++c) F0[c * T + t] = p0[0][c];
-            store3(V0.RES(), V0.pitch, s0, r[0]);
+            if (keep1) store3(V0.RES(), V0.pitch, s0, r[0]);
             if constexpr (C > 0) M0[t] = (r[0][0] + r[0][1] + r[0][2]) / 3.;
         }
     }
@@ -665,13 +679,14 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
         // halo records by vector loads: the boundary lanes are few, and scalar copies of the
         // records would push the kernel past 80 SGPRs (7 instead of 8 waves per SIMD)
 #pragma unroll
-        for (int k = 0; k < NP; ++k) hs_write(false, V0.H, w0, h0[k], p0[k]);
+        for (int k = 0; k < NP; ++k)
+            if (keeph) hs_write(false, V0.H, w0, h0[k], p0[k]);
         if constexpr (NP == 2) {
             store3p(V0.T(), V0.pitch, s0, p0[0], p0[1]);
-            store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
+            if (keep1) store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
         } else {
             store3(V0.T(), V0.pitch, s0, p0[0]);
-            store3(V0.TNN(), V0.pitch, s0, x0[0]);
+            if (keep1) store3(V0.TNN(), V0.pitch, s0, x0[0]);
         }
     }
     stamp<MT>(A, 4);
@@ -738,8 +753,11 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     }();
     // (the reference's operation order, Stc, issues 3x the fp64 work and gains from the extra
     // wave at any size: 0.2678 -> 0.2560 ms per full-mesh cycle)
+    // (the pipelined launch without its dead-until-final stores, kKeep*, moves 72 instead of
+    // 120 B per level-1 sub-element and gains from it too: 0.1377 -> 0.1328 ms per full-mesh
+    // cycle, scripts/ab_probe.py with PAMG_W8_MAX_GRID)
     static const long w8_env = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : -1;
-    const long w8_max = w8_env >= 0 ? w8_env : (std::is_same<ST, Stc>::value ? (1l << 40) : 4 * n_cu);
+    const long w8_max = w8_env >= 0 ? w8_env : ((std::is_same<ST, Stc>::value || part == 2) ? (1l << 40) : 4 * n_cu);
     if constexpr (S >= 3)
         if (part != 1 && fine_mt(S) == 512 && (long)grid > 3 * n_cu && (long)grid <= w8_max)
             return launch_sltw<S, L, ST, true>(s, A, grid, part);
@@ -765,7 +783,7 @@ hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, int par
 }
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
-                       double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part) {
+                       double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part, int keep) {
     const bool coarse = part == 1;
     if (part == 2 && L < 2) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
@@ -791,6 +809,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.n_coarse = n_coarse;
     A.rdt = rdt;
     A.rhsn2 = rhsn2;
+    A.keep = part == 2 ? keep : kKeepAll;
     // tile: 2**fine_tl level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
     const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : fine_tl(n_split) - 2 * n_split;
     const unsigned grid = (unsigned)(((int64_t)U + (1 << GL) - 1) >> GL);
@@ -840,14 +859,14 @@ hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, in
                                 int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2) {
     if (L < 2) return hipSuccess;
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, nullptr, const_cast<double *>(rhsn2),
-                       1);
+                       1, kKeepAll);
 }
 
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                              bool pipe) {
+                              bool pipe, int keep) {
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, L > 1 ? rhsn2 : nullptr,
-                       pipe ? 2 : 0);
+                       pipe ? 2 : 0, keep);
 }
 
 }  // namespace pamg

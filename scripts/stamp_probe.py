@@ -22,11 +22,12 @@ if os.environ.get("PAMG_VCYCLE_STAMPS") is None:
         n = g * w * s
         recs.setdefault("coarse" if L < 0 else "fine", []).append(raw[i + 4:i + 4 + n].reshape(g, w, s))
         i += 4 + n
-    names = {"fine": ["prologue+sweeps", "halo+residual", "final sweeps", "stores+halo", "", "", "cascade"],
+    names = {"fine": ["prologue+sweeps", "halo+residual", "final sweeps", "stores+halo", "cascade+coarse(pipe)", "", ""],
              "coarse": ["prologue+restrict", "L2..C-1 restr-leg", "coarse chain", "prolong legs", "", "",
                         "cascade"]}
     for kind, lst in recs.items():
-        st = lst[-1]
+        # fine: the call's pipelined launches come before its last (plain) level-1 launch
+        st = lst[-2] if kind == "fine" and len(lst) > 1 else lst[-1]
         t = st[:, :, :8].astype(np.float64) * 10.0 / 1000.0  # 100 MHz ticks -> us
         ok = st[:, :, 0] > 0
         t0 = t[:, :, 0][ok].min()
