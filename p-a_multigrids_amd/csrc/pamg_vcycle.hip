@@ -498,9 +498,79 @@ struct PGeo {
     static constexpr int F(int l) { int o = 0; for (int i = 1; i < l; ++i) o += 3 * nt(i); return o; }
     static constexpr int M(int l) { int o = F(C); for (int i = 1; i < l; ++i) o += nt(i); return o; }
     static_assert(M(C) <= 4 * G::T, "coarse images exceed the level-1 image region");
+    // the coarsest level's work runs at the start of the launch (coarsest_chain) when it does
+    // not depend on the launch's level-1 residual (C >= 2); its final tnew waits for the
+    // prolongator cascade in a stash behind the level-1 images. Measured (scripts/ab2.sh,
+    // profiles/r01_v16_hoist_ab.txt): n_split = 5 full mesh 0.1324 -> 0.1300 ms per cycle,
+    // N = 8 partition 0.0218 -> 0.0208, reference order 0.214 -> 0.202; n_split = 3 (16
+    // un_eles per tile) 0.0127 -> 0.0131, so it stays off below n_split = 5
+    static constexpr bool HOIST = C >= 2 && S >= 5;
+    static constexpr int PC() { return 4 * G::T; }
+    static constexpr int LDS() { return 4 * G::T + (HOIST ? 3 * nt(C) : 0); }
 };
 
+// The coarsest level of the next cycle, hoisted to the start of the pipelined launch (C >= 2):
+// its restriction-leg call (:331 via :351), get_residual (:338) and the 1 + n_coarse calls
+// (:351-353) read only its own tnew and its RHSN, both written by the previous launch -- its
+// RHS is the restriction of level C-1's residual of the PREVIOUS cycle (:336) -- so the
+// chain of 4 (1 + n_coarse) dependent sweeps runs on the coarsest level's threads while every
+// thread's level-1 loads are in flight, instead of after the tile's level-1 work, as the
+// launch's last phase. Phase B keeps what needs this launch: the restrictor into RHSN and
+// the prolongator cascade. Loads first (coarsest_load), so that the level-1 loads issued
+// behind them do not delay the chain.
+template <int S, int L>
+__device__ __forceinline__ bool coarsest_thread(int t) {
+    using P = PGeo<S, L>;
+    return t >= P::T0(L - 1) && t < P::T0(L - 1) + P::NTH(L - 1);
+}
+template <int S, int L>
+__device__ __forceinline__ void coarsest_load(const VArgs &A, int t, int64_t u0, int nue, double x[3], double b[3]) {
+    using G = Geo<S, L>;
+    using P = PGeo<S, L>;
+    constexpr int C = G::C;
+    const VLevel &V = A.lv[C];
+    const int i = t - P::T0(C);
+    const bool v = i < P::nt(C) && i < (nue << G::lg(C));
+    const uint32_t gx = ((uint32_t)u0 << G::lg(C)) + (uint32_t)(v ? i : 0);
+    load3(V.T(), V.pitch, gx, x);
+    load3(V.RHSN(), V.pitch, gx, b);
+}
 template <int S, int L, class ST>
+__device__ __forceinline__ void coarsest_chain(const VArgs &A, const double *__restrict__ sp, int t, int64_t u0, int nue,
+                                               double x[3], const double b[3], double *lds) {
+    using G = Geo<S, L>;
+    using P = PGeo<S, L>;
+    constexpr int C = G::C;
+    const VLevel &V = A.lv[C];
+    const double rdt = A.rdt;
+    const int ns = A.n_smooth;
+    const int i = t - P::T0(C);
+    const bool v = i < P::nt(C) && i < (nue << G::lg(C));
+    const uint32_t gx = ((uint32_t)u0 << G::lg(C)) + (uint32_t)(v ? i : 0);
+    const bool keep = A.keep & kKeepCoarse;
+    if (v && keep) store3(V.RHS(), V.pitch, gx, b);
+    ST St;
+    stencil(G::uni(C), sp, gx >> G::lg(C), St);
+    double p[3];
+    for (int it = 0; it < ns; ++it) {
+        copy3(p, x);
+        sweep(St, rdt, b, x);
+    }
+    double r[3];
+    residual(St, rdt, p, b, r);
+    if (v && keep) store3(V.RES(), V.pitch, gx, r);
+    copy3(x, p);   // tnew_nonlin := tnew (:348)
+    const int nB = ns * A.n_coarse;
+    for (int it = 0; it < nB; ++it) {
+        copy3(p, x);
+        sweep(St, rdt, b, x);
+    }
+    if (v) store3(V.T(), V.pitch, gx, p);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) lds[P::PC() + c * P::nt(C) + i] = p[c];
+}
+
+template <int S, int L, class ST, bool HOIST>
 __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__restrict__ const *SP, int t, int64_t u0, int nue,
                                             const double y1[3], const double rn1[3], double *lds) {
     using G = Geo<S, L>;
@@ -523,6 +593,10 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
         i = t - P::T0(l);
         v = i < P::nt(l) && i < (nue << G::lg(l));
         gx = ((uint32_t)u0 << G::lg(l)) + (uint32_t)(v ? i : 0);
+        if constexpr (HOIST && l == C) {   // phase A ran at the start of the launch (coarsest_chain)
+            c4 = V.children[gx & ((1 << G::lg(l)) - 1)];
+            return;
+        }
         if constexpr (l == 1) {
             copy3(x, y1);   // final tnew of the previous cycle (:348 tnew_nonlin := tnew)
             copy3(b, rn1);  // the restriction of level 1's residual (:336)
@@ -564,13 +638,18 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
                 store3(V.RHSN(), V.pitch, gx, rn);
             }
         }
-        const int nB = l == C ? ns * A.n_coarse : ns;
-        for (int it = 0; it < nB; ++it) {
-            copy3(p, x);
-            sweep(St, rdt, b, x);
+        if constexpr (HOIST && l == C) {   // its 1 + n_coarse calls ran in coarsest_chain
+#pragma unroll
+            for (int c = 0; c < 3; ++c) p[c] = lds[P::PC() + c * P::nt(C) + i];
+        } else {
+            const int nB = l == C ? ns * A.n_coarse : ns;
+            for (int it = 0; it < nB; ++it) {
+                copy3(p, x);
+                sweep(St, rdt, b, x);
+            }
         }
         if (v) {
-            store3(V.T(), V.pitch, gx, p);
+            if constexpr (!(HOIST && l == C)) store3(V.T(), V.pitch, gx, p);
             // ---- prolongator into level l - 1 (:370; result dead, :550) by the owner of the
             //      coarse sub-element, from its final tnew, on the restriction-leg image of
             //      level l - 1 (complete since the phase-A barrier; each child has one parent)
@@ -597,7 +676,8 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     // F0 | M0: restriction-leg tnew image and residual means (restrictor input) of level 1;
     // the pipelined tail reuses the region for the coarse levels' images
     constexpr int T = G::T, MT = G::MT, NP = G::NP;
-    __shared__ __attribute__((aligned(16))) double F0[C > 0 ? 4 * T : 1];
+    constexpr bool HOIST = PIPE && PGeo<S, L>::HOIST;
+    __shared__ __attribute__((aligned(16))) double F0[C > 0 ? (PIPE ? PGeo<S, L>::LDS() : 4 * T) : 1];
     double *const M0 = F0 + 3 * T;
     const int t = threadIdx.x;
     const double rdt = A.rdt;
@@ -616,6 +696,9 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 #pragma unroll
     for (int k = 0; k < NP; ++k) h0[k] = v0 ? hs_pack(V0.H.hsub[(s0 + k) & ((1 << G::lg(0)) - 1)]) : 0;
     double x0[NP][3], b0[NP][3], p0[NP][3];
+    double xc[3], bc[3];   // HOIST: the coarsest level's tnew and RHSN (coarsest_chain)
+    if constexpr (HOIST)
+        if (coarsest_thread<S, L>(t)) coarsest_load<S, L>(A, t, u0, nue, xc, bc);
     if constexpr (NP == 2) {
         load3p(V0.T(), V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
         load3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
@@ -623,6 +706,9 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
         load3(V0.T(), V0.pitch, s0, x0[0]);
         load3(V0.RHS(), V0.pitch, s0, b0[0]);
     }
+    if constexpr (HOIST)
+        if (coarsest_thread<S, L>(t)) coarsest_chain<S, L, ST>(A, G::C == 1 ? sp1 : G::C == 2 ? sp2 : G::C == 3 ? sp3 : sp4,
+                                                               t, u0, nue, xc, bc, F0);
     ST St;
     stencil(G::uni(0), sp0, w0, St);
     // ---- restriction leg: smoother (:331), get_residual (:338)
@@ -713,7 +799,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     }
     if constexpr (PIPE) {
         const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
-        coarse_next<S, L, ST>(A, SP, t, u0, nue, y1, rn, F0);
+        coarse_next<S, L, ST, HOIST>(A, SP, t, u0, nue, y1, rn, F0);
     }
     stamp<MT>(A, 7);
 }
@@ -740,6 +826,11 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     return hipGetLastError();
 }
 
+bool no_scratch(const void *kernel) {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, kernel) == hipSuccess && a.localSizeBytes == 0;
+}
+
 // the 64-VGPR instance only where it saves a round: more workgroups than 3 per CU, at most 4
 // (at n_split = 3 the launch fits one round either way and the bounded instance is 50 %
 // slower; PAMG_W8_MAX_GRID=<n> overrides the upper bound for A/B runs)
@@ -758,9 +849,14 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     // cycle, scripts/ab_probe.py with PAMG_W8_MAX_GRID)
     static const long w8_env = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : -1;
     const long w8_max = w8_env >= 0 ? w8_env : ((std::is_same<ST, Stc>::value || part == 2) ? (1l << 40) : 4 * n_cu);
-    if constexpr (S >= 3)
-        if (part != 1 && fine_mt(S) == 512 && (long)grid > 3 * n_cu && (long)grid <= w8_max)
+    // (and only instances that fit 64 VGPRs without scratch: several L >= 4 and n_split = 3
+    // instances spill there and stay at their natural register count)
+    if constexpr (S >= 3) {
+        static const bool fits[2] = {no_scratch((const void *)k_vc_fine<S, L, ST, false, true>),
+                                     L >= 2 && no_scratch((const void *)k_vc_fine<S, L, ST, (L >= 2), true>)};
+        if (part != 1 && fine_mt(S) == 512 && (long)grid > 3 * n_cu && (long)grid <= w8_max && fits[part == 2])
             return launch_sltw<S, L, ST, true>(s, A, grid, part);
+    }
     return launch_sltw<S, L, ST, false>(s, A, grid, part);
 }
 
