@@ -437,6 +437,52 @@ int vcycle_fused(pamg_handle *h, int n) {
     // one cycle ahead, and the last launch brings level 1 (and level 2's RHSN) level with them
     const bool pipe = h->p.fused == 3 && L > 1;
     Level &L2 = h->lv[2];
+    // pipelined, halo exchanged once per call: the tiles are independent for the whole call
+    // (every operation is local to an un_ele, the halo words have no reader inside it), so two
+    // halves of them can run their launch sequences on two streams, each launch's drain
+    // overlapped by the other half's stream (pamg_set_tile_streams; PAMG_TILE_STREAMS=<n>
+    // overrides for A/B runs). Measured (scripts/ab_probe.py, profiles/r01_v16_tile_streams.txt):
+    // N = 4 partition 0.0404 -> 0.0339 ms per cycle, N = 8 0.0208 -> 0.0202, n_split = 3
+    // 0.0128 -> 0.0114, full mesh 0.1319 -> 0.1290. Automatic on partitions only: on one GPU
+    // the bench's per-launch events would time two overlapped half-launches.
+    static const int ts_env = getenv("PAMG_TILE_STREAMS") ? atoi(getenv("PAMG_TILE_STREAMS")) : -1;
+    const int tile_streams = ts_env >= 0 ? ts_env : h->tile_streams ? h->tile_streams : (h->nranks > 1 ? 2 : 1);
+    const int tile = vcycle_tile_un_eles(h->p.n_split);
+    const int ntiles = (h->U + tile - 1) / tile;
+    if (pipe && n > 1 && tile_streams == 2 && h->p.halo_exchange == 0 && ntiles >= 2) {
+        const int buf = two ? 1 - P1.send_cur : 0;
+        if (h->sent_pending[buf]) {
+            HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[buf], 0));
+            h->sent_pending[buf] = false;
+        }
+        const int mid = (ntiles / 2) * tile;
+        HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));
+        HIPCHK(h, hipStreamWaitEvent(h->stream_c, h->ev_fine, 0));
+        // launches alternate between the halves so that each stream always has the next one queued
+        const hipStream_t st[2] = {h->stream, h->stream_c};
+        const int ua[2] = {0, mid}, ub[2] = {mid, h->U};
+        for (int q = 0; q < 2; ++q) {
+            Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h) * (ub[q] - ua[q]) / h->U, st[q]);
+            HIPCHK(h, launch_vcycle_coarse(st[q], h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
+                                           h->tovo, L2.RHSN, ua[q], ub[q]));
+        }
+        for (int c = 0; c < n; ++c) {
+            const bool pc = c + 1 < n;
+            const int keep = pipe_keep_env() | (c + 2 == n ? PAMG_KEEP_COARSE : 0);
+            for (int q = 0; q < 2; ++q) {
+                const double f = (double)(ub[q] - ua[q]) / h->U;
+                Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE,
+                        f * (pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h)), st[q]);
+                HIPCHK(h, launch_vcycle_fine(st[q], h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
+                                             h->tovo, P1.send_buf(buf), L2.RHSN, pc, keep, ua[q], ub[q]));
+            }
+        }
+        HIPCHK(h, hipEventRecord(h->ev_coarse, h->stream_c));
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));
+        h->tnn_level = 1;
+        CHK(halo_async(h, buf));
+        return join_comm(h);
+    }
     if (conc) {
         HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));   // everything issued before this call
     }
@@ -894,6 +940,12 @@ int pamg_timing_reset(pamg_handle *h) {
     for (int k = 0; k < PAMG_K_COUNT; ++k) {
         h->timing.ms[k] = 0; h->timing.count[k] = 0; h->timing.bytes[k] = 0; h->timing.seq[k] = 0;
     }
+    return PAMG_OK;
+}
+
+int pamg_set_tile_streams(pamg_handle *h, int n) {
+    if (!h || n < 0 || n > 2) return PAMG_ERR_ARG;
+    h->tile_streams = n;
     return PAMG_OK;
 }
 

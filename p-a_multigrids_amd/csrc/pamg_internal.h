@@ -132,6 +132,7 @@ struct pamg_handle {
     // fused = 2: the coarse-level launch of each cycle runs on stream_c beside the level-1
     // launch on `stream`; ev_fine / ev_coarse order them across cycles (RHSN of level 2)
     hipStream_t stream_c = nullptr;
+    int tile_streams = 0;   // pamg_set_tile_streams (0: automatic)
     hipEvent_t ev_fine = nullptr, ev_coarse = nullptr;
     // RHSN of every level holds the restriction of the finer level's current residual
     bool rhsn_valid = true;
@@ -175,8 +176,12 @@ hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *t
 // fused V-cycle (pamg_vcycle.hip); lv is the handle's 1-based level array
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth);
 // levels 2..L; the level-2 RHS is taken from rhsn2 (level 2's RHSN or RHSN_alt)
+// [ua, ub): the un_eles a launch covers (ub < 0: all of them); bounds multiples of
+// vcycle_tile_un_eles (ub may be U)
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                                int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2);
+                                int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2, int ua = 0,
+                                int ub = -1);
+int vcycle_tile_un_eles(int n_split);
 // level 1; its remote halo words packed into send1 (one of level 1's two send buffers), the
 // restriction of its residual into rhsn2
 // pipe: the same launch also runs the coarse levels of the next cycle (L >= 2; level 2's RHS
@@ -185,7 +190,7 @@ hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, in
 constexpr int PAMG_KEEP_L1 = 1, PAMG_KEEP_COARSE = 2, PAMG_KEEP_HALO = 4, PAMG_KEEP_ALL = 7;
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                              bool pipe = false, int keep = PAMG_KEEP_ALL);
+                              bool pipe = false, int keep = PAMG_KEEP_ALL, int ua = 0, int ub = -1);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 // FINDInv (matrix_inversion.F90:50-148) batched, n <= 8, column-major (n, n, nb)

@@ -94,6 +94,7 @@ struct VArgs {
     double *rhsn2;          // level 2's RHSN buffer: read by the coarse launch, written by the level-1 launch
     long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
     int keep;               // pipelined launch: the dead-until-final stores it makes (kKeep*)
+    int64_t tile0;          // first tile of the launch (a launch may cover a range of tiles)
 };
 
 // Stores of a pipelined launch whose values the rest of the call overwrites before any read
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
-    const int64_t u0 = (int64_t)blockIdx.x << Q::GL;
+    const int64_t u0 = ((int64_t)blockIdx.x + A.tile0) << Q::GL;
     const int nue = Q::GL == 0 ? 1 : (int)min((int64_t)1 << Q::GL, A.U - u0);   // un_eles in this tile
     stamp<kMTc>(A, 0);
     stamp_hwid<kMTc>(A);
@@ -682,7 +683,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
-    const int64_t u0 = (int64_t)blockIdx.x << G::GL;
+    const int64_t u0 = ((int64_t)blockIdx.x + A.tile0) << G::GL;
     const int nue = G::GL == 0 ? 1 : (int)min((int64_t)1 << G::GL, A.U - u0);   // un_eles in this tile
     stamp<MT>(A, 0);
     stamp_hwid<MT>(A);
@@ -879,7 +880,8 @@ hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, int par
 }
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
-                       double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part, int keep) {
+                       double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part, int keep,
+                       int ua, int ub) {
     const bool coarse = part == 1;
     if (part == 2 && L < 2) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
@@ -908,7 +910,11 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.keep = part == 2 ? keep : kKeepAll;
     // tile: 2**fine_tl level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
     const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : fine_tl(n_split) - 2 * n_split;
-    const unsigned grid = (unsigned)(((int64_t)U + (1 << GL) - 1) >> GL);
+    // un_eles [ua, ub) (ub < 0: all); ua a multiple of the tile, ub too unless it is U
+    if (ub < 0 || ub > U) ub = U;
+    if (ua < 0 || (ua & ((1 << GL) - 1)) || (ub != U && (ub & ((1 << GL) - 1)))) return hipErrorInvalidValue;
+    A.tile0 = ua >> GL;
+    const unsigned grid = ub > ua ? (unsigned)(((int64_t)ub - ua + (1 << GL) - 1) >> GL) : 0u;
     if (grid == 0) return hipSuccess;
     // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_VCYCLE_STAMPS") : nullptr;
@@ -952,17 +958,21 @@ bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mo
 }
 
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
-                                int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2) {
+                                int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2, int ua,
+                                int ub) {
     if (L < 2) return hipSuccess;
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, nullptr, const_cast<double *>(rhsn2),
-                       1, kKeepAll);
+                       1, kKeepAll, ua, ub);
 }
 
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                              bool pipe, int keep) {
+                              bool pipe, int keep, int ua, int ub) {
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, L > 1 ? rhsn2 : nullptr,
-                       pipe ? 2 : 0, keep);
+                       pipe ? 2 : 0, keep, ua, ub);
+}
+
+int vcycle_tile_un_eles(int n_split) { return 1 << (fine_tl(n_split) - 2 * n_split);
 }
 
 }  // namespace pamg

@@ -185,6 +185,10 @@ class SemiImplicitIterative:
     def timing_reset(self): self._call("pamg_timing_reset")
     def timing_stride(self, every): self._call("pamg_timing_stride", every)
 
+    def set_tile_streams(self, n):
+        """Pipelined calls: tiles in n halves on their own streams (0 automatic, 1, 2)."""
+        self._call("pamg_set_tile_streams", n)
+
     def timing(self):
         out = {}
         for kid, name in enumerate(K_NAMES):

@@ -1,5 +1,5 @@
 """Phase timeline of the fused V-cycle kernel from its in-kernel stamps
-(PAMG_VCYCLE_STAMPS), GPU box only. usage: stamp_probe.py S L [ns nc]"""
+(PAMG_VCYCLE_STAMPS), GPU box only. usage: stamp_probe.py S L [ns nc [N]]"""
 import os
 import subprocess
 import sys
@@ -8,7 +8,7 @@ import numpy as np
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 if os.environ.get("PAMG_VCYCLE_STAMPS") is None:
-    out = os.path.join(ROOT, "gpurun_out", "stamps.bin")
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), "pamg_stamps.bin")
     if os.path.exists(out):
         os.remove(out)
     r = subprocess.run([sys.executable, __file__] + sys.argv[1:], env=dict(os.environ, PAMG_VCYCLE_STAMPS=out))
@@ -22,7 +22,7 @@ if os.environ.get("PAMG_VCYCLE_STAMPS") is None:
         n = g * w * s
         recs.setdefault("coarse" if L < 0 else "fine", []).append(raw[i + 4:i + 4 + n].reshape(g, w, s))
         i += 4 + n
-    names = {"fine": ["prologue+sweeps", "halo+residual", "final sweeps", "stores+halo", "cascade+coarse(pipe)", "", ""],
+    names = {"fine": ["prologue(+chain)+sweeps", "halo+residual", "final sweeps", "stores+halo", "cascade+coarse(pipe)", "", ""],
              "coarse": ["prologue+restrict", "L2..C-1 restr-leg", "coarse chain", "prolong legs", "", "",
                         "cascade"]}
     for kind, lst in recs.items():
@@ -62,8 +62,10 @@ S, L = int(sys.argv[1]), int(sys.argv[2])
 ns = int(sys.argv[3]) if len(sys.argv) > 3 else 4
 nc = int(sys.argv[4]) if len(sys.argv) > 4 else 15
 mesh = pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "untitled8192.msh"))
-s = pamg.SemiImplicitIterative(mesh, S, L, n_smooth=ns, n_coarse=nc, solver=3)
+N = int(sys.argv[5]) if len(sys.argv) > 5 else 1   # rank 0's x-strip partition of N (detached)
+comm = None if N == 1 else (N, 0, None, mesh.x_strip_owner(N))
+s = pamg.SemiImplicitIterative(mesh, S, L, n_smooth=ns, n_coarse=nc, solver=3, arith=1, fused=3, comm=comm)
 s.begin_timestep()
-s.vcycle(4)
+s.vcycle(100 if N > 1 else 4)   # a partition's launches are small: settle the clocks first
 s.synchronize()
 s.close()
