@@ -228,9 +228,9 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
     return halo(h, l);
 }
 
-int rhs_level1(pamg_handle *h, bool start_of_step) {
+int rhs_level1(pamg_handle *h, int start_of_step) {
     Level &L = h->lv[1];
-    Span sp(h, PAMG_K_RHS, 96.0 * (double)L.N);
+    Span sp(h, PAMG_K_RHS, (start_of_step == 1 ? 96.0 : start_of_step == 2 ? 72.0 : 48.0) * (double)L.N);
     HIPCHK(h, launch_rhs(h->stream, L, h->geo1, 1 / h->p.dt, h->p.k, start_of_step));
     return PAMG_OK;
 }
@@ -253,7 +253,7 @@ int restrict_residual(pamg_handle *h, int l) {
         CHK(restrict_(h, l));
         return residual(h, l);
     }
-    if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, false));   // get_RHS inside get_residual (:865-867)
+    if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, 0));   // get_RHS inside get_residual (:865-867)
     Span sp(h, PAMG_K_RESIDUAL, 102.0 * (double)L.N + 168.0 * h->U);
     HIPCHK(h, launch_restrict_residual(h->stream, L, h->lv[l + 1], 1 / h->p.dt));
     return PAMG_OK;
@@ -262,7 +262,7 @@ int restrict_residual(pamg_handle *h, int l) {
 int residual(pamg_handle *h, int l) {
     Level &L = h->lv[l];
     h->rhsn_valid = false;
-    if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, false));   // get_RHS inside get_residual (:865-867)
+    if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, 0));   // get_RHS inside get_residual (:865-867)
     Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)L.N + 168.0 * h->U);
     HIPCHK(h, launch_residual(h->stream, L, 1 / h->p.dt));
     return PAMG_OK;
@@ -294,10 +294,10 @@ double vcycle_fine_bytes(pamg_handle *h) {
     const int L = h->p.multi_levels;
     return 120.0 * h->lv[1].N + (L > 1 ? 48.0 * h->lv[2].N : 0.0) + 104.0 * h->U;
 }
-double vcycle_coarse_bytes(pamg_handle *h) {
+double vcycle_coarse_bytes(pamg_handle *h, int keep = PAMG_KEEP_ALL) {
     const int L = h->p.multi_levels;
     double b = 0.0;
-    for (int l = 2; l <= L; ++l) b += (120.0 + (l >= 3 ? 24.0 : 0.0)) * h->lv[l].N;
+    for (int l = 2; l <= L; ++l) b += (120.0 - (keep & PAMG_KEEP_COARSE ? 0.0 : 48.0) + (l >= 3 ? 24.0 : 0.0)) * h->lv[l].N;
     return b + 104.0 * h->U * (L - 1);
 }
 //   pipelined launch: both, less level 2's RHSN (written and read: 48 B) and its tnew read
@@ -460,11 +460,13 @@ int vcycle_fused(pamg_handle *h, int n) {
         HIPCHK(h, hipStreamWaitEvent(h->stream_c, h->ev_fine, 0));
         // launches alternate between the halves so that each stream always has the next one queued
         const hipStream_t st[2] = {h->stream, h->stream_c};
+        // the first coarse launch's RHS and residual are rewritten by the first pipelined one
+        const int ck = pipe_keep_env() & PAMG_KEEP_COARSE;
         const int ua[2] = {0, mid}, ub[2] = {mid, h->U};
         for (int q = 0; q < 2; ++q) {
-            Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h) * (ub[q] - ua[q]) / h->U, st[q]);
+            Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h, ck) * (ub[q] - ua[q]) / h->U, st[q]);
             HIPCHK(h, launch_vcycle_coarse(st[q], h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                           h->tovo, L2.RHSN, ua[q], ub[q]));
+                                           h->tovo, L2.RHSN, ua[q], ub[q], ck));
         }
         for (int c = 0; c < n; ++c) {
             const bool pc = c + 1 < n;
@@ -486,10 +488,11 @@ int vcycle_fused(pamg_handle *h, int n) {
     if (conc) {
         HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));   // everything issued before this call
     }
-    if (pipe && n > 0) {
-        Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h));
+    if (pipe && n > 0) {   // its RHS and residual stores are rewritten by the first pipelined launch if n > 1
+        const int ck = n > 1 ? pipe_keep_env() & PAMG_KEEP_COARSE : PAMG_KEEP_ALL;
+        Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h, ck));
         HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                       h->tovo, L2.RHSN));
+                                       h->tovo, L2.RHSN, 0, -1, ck));
     }
     for (int c = 0; c < n; ++c) {
         const int buf = two ? 1 - P1.send_cur : 0;
@@ -806,8 +809,9 @@ int pamg_get_overlap(pamg_handle *h, double *tov, double *tovo) {
     return PAMG_OK;
 }
 
-int pamg_begin_timestep(pamg_handle *h) {
-    if (!h) return PAMG_ERR_ARG;
+// tnn_dead: the caller runs a V-cycle next, whose first smoother call rewrites tnew_nonlin
+// (:327) before any read, so the :317 copy is not stored (pamg_run)
+int begin_timestep(pamg_handle *h, bool tnn_dead) {
     CHK(check_level(h, 1));
     h->tnn_level = 1;
     if (h->p.solver == 2) {   // solve_Richardson never calls get_RHS inside the smoother
@@ -816,8 +820,13 @@ int pamg_begin_timestep(pamg_handle *h) {
         HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
         return refresh_told_halo(h, 1);
     }
-    CHK(rhs_level1(h, true));
+    CHK(rhs_level1(h, tnn_dead ? 2 : 1));
     return refresh_told_halo(h, 1);
+}
+
+int pamg_begin_timestep(pamg_handle *h) {
+    if (!h) return PAMG_ERR_ARG;
+    return begin_timestep(h, false);
 }
 
 int pamg_copy_to_nonlin(pamg_handle *h, int level) {
@@ -916,7 +925,7 @@ int pamg_block_inverse(pamg_handle *h, int n, long nb, const double *A, double *
 int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
     if (!h || ntime < 0 || n_multigrid < 0) return PAMG_ERR_ARG;
     for (int t = 0; t < ntime; ++t) {
-        CHK(pamg_begin_timestep(h));
+        CHK(begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0));
         CHK(pamg_vcycle(h, n_multigrid));
     }
     return PAMG_OK;

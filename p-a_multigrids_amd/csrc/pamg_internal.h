@@ -167,7 +167,8 @@ hipError_t launch_residual(hipStream_t s, const Level &L, double rdt, bool neg =
 hipError_t launch_interp_add(hipStream_t s, const Level &fine, const Level &coarse);
 hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U, double *out = nullptr);
 hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn);
-hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, bool start_of_step);
+// start_of_step: 0 RHS from told; 1 told := tnew_nonlin := tnew first; 2 told := tnew first
+hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, int start_of_step);
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
 hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
 hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);
@@ -176,18 +177,19 @@ hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *t
 // fused V-cycle (pamg_vcycle.hip); lv is the handle's 1-based level array
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth);
 // levels 2..L; the level-2 RHS is taken from rhsn2 (level 2's RHSN or RHSN_alt)
+// stores a pipelined V-cycle launch may skip (pamg_vcycle.hip, kKeep*)
+constexpr int PAMG_KEEP_L1 = 1, PAMG_KEEP_COARSE = 2, PAMG_KEEP_HALO = 4, PAMG_KEEP_ALL = 7;
 // [ua, ub): the un_eles a launch covers (ub < 0: all of them); bounds multiples of
 // vcycle_tile_un_eles (ub may be U)
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                 int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2, int ua = 0,
-                                int ub = -1);
+                                int ub = -1, int keep = PAMG_KEEP_ALL);
 int vcycle_tile_un_eles(int n_split);
 // level 1; its remote halo words packed into send1 (one of level 1's two send buffers), the
 // restriction of its residual into rhsn2
 // pipe: the same launch also runs the coarse levels of the next cycle (L >= 2; level 2's RHS
 // from LDS, rhsn2 unused); keep: which of its dead-until-final stores it makes
 // (PAMG_KEEP_*, pamg_vcycle.hip)
-constexpr int PAMG_KEEP_L1 = 1, PAMG_KEEP_COARSE = 2, PAMG_KEEP_HALO = 4, PAMG_KEEP_ALL = 7;
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
                               bool pipe = false, int keep = PAMG_KEEP_ALL, int ua = 0, int ub = -1);

@@ -181,7 +181,8 @@ __global__ __launch_bounds__(kBlock) void k_interp_add(double *T, const double *
 // Level-1 right-hand side + time-step start (:316-317, :593, get_RHS :452-464):
 // told := tnew, tnew_nonlin := tnew, source s_j = -2k sin(x_j + y_j) at the
 // sub-element nodes (get_splitting coordinates), cascaded in place through M,
-// RHS_i = rdt (M told)_i + s'_i.
+// RHS_i = rdt (M told)_i + s'_i. start_of_step 2: the same without the tnew_nonlin store
+// (pamg_run: the V-cycle that follows rewrites it before any read, :327).
 __global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, double *TOLD,
                                                 double *__restrict__ TNN, double *__restrict__ RHS,
                                                 const double *__restrict__ stc, const double *__restrict__ geo,
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, do
         for (int c = 0; c < 3; ++c) {
             t[c] = T[c * pitch + s];
             TOLD[c * pitch + s] = t[c];
-            TNN[c * pitch + s] = t[c];
+            if (start_of_step == 1) TNN[c * pitch + s] = t[c];
         }
     } else {
 #pragma unroll
@@ -752,10 +753,10 @@ hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse,
     return hipGetLastError();
 }
 
-hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, bool start_of_step) {
+hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, int start_of_step) {
     if (L.N == 0) return hipSuccess;
     hipLaunchKernelGGL(k_rhs, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.T, L.TOLD, L.TNN, L.RHS, L.stc, geo1,
-                       L.subinfo, L.pitch, L.N, log2i(L.nsub), rdt, k, start_of_step ? 1 : 0);
+                       L.subinfo, L.pitch, L.N, log2i(L.nsub), rdt, k, start_of_step);
     return hipGetLastError();
 }
 

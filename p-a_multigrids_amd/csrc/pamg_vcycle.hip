@@ -58,6 +58,9 @@ using namespace detail;
 #ifndef PAMG_FINE_TL_MIN
 #define PAMG_FINE_TL_MIN 10
 #endif
+#ifndef PAMG_CHAIN_PRIO
+#define PAMG_CHAIN_PRIO 3
+#endif
 constexpr int fine_tl(int S) { return 2 * S > PAMG_FINE_TL_MIN ? 2 * S : PAMG_FINE_TL_MIN; }
 // level-0 sub-elements per thread: an adjacent pair (16-byte accesses); one at n_split <=
 // PAMG_NP1_MAX_S (A/B builds: twice the waves for the single-round launches of small n_split).
@@ -369,7 +372,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
         load3(Q::lev(j) == 1 ? A.rhsn2 : A.lv[Q::lev(j)].RHSN(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
 #pragma unroll
     for (int j = 0; j < N; ++j)
-        if (ok[j]) store3(A.lv[Q::lev(j)].RHS(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
+        if (ok[j] && (A.keep & kKeepCoarse)) store3(A.lv[Q::lev(j)].RHS(), A.lv[Q::lev(j)].pitch, gx[j], b[j]);
     stamp<kMTc>(A, 1);
     // ---- phase A: restriction-leg smoother call of every level (:331), then get_residual (:338)
     for (int it = 0; it < ns; ++it) {
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
         stc_of(j, St);
         double r[3];
         residual(St, rdt, p[j], b[j], r);
-        if (ok[j]) store3(V.RES(), V.pitch, gx[j], r);
+        if (ok[j] && (A.keep & kKeepCoarse)) store3(V.RES(), V.pitch, gx[j], r);
         if (l < C) {   // restriction-leg tnew: start of the prolongation leg and cascade target
             if (ok[j]) {
                 const int i = t + 64 * Q::kk(j);
@@ -552,6 +555,13 @@ __device__ __forceinline__ void coarsest_chain(const VArgs &A, const double *__r
     if (v && keep) store3(V.RHS(), V.pitch, gx, b);
     ST St;
     stencil(G::uni(C), sp, gx >> G::lg(C), St);
+    // the chain is the tile's critical path and the other waves are mostly waiting on HBM:
+    // issue priority to it. Measured (scripts/ab2.sh, profiles/r01_v16_chain_prio.txt):
+    // contracted arithmetic full mesh 0.1300 -> 0.1290 ms per cycle, N = 8 partition 0.0201 ->
+    // 0.0195; the reference's order 0.1985 -> 0.2023 (its 3x fp64 work is not latency-bound
+    // there), so only the contracted instance raises it
+    constexpr int prio = std::is_same<ST, StcF>::value ? PAMG_CHAIN_PRIO : 0;
+    if (prio) __builtin_amdgcn_s_setprio(prio);
     double p[3];
     for (int it = 0; it < ns; ++it) {
         copy3(p, x);
@@ -566,6 +576,7 @@ __device__ __forceinline__ void coarsest_chain(const VArgs &A, const double *__r
         copy3(p, x);
         sweep(St, rdt, b, x);
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
     if (v) store3(V.T(), V.pitch, gx, p);
 #pragma unroll
     for (int c = 0; c < 3; ++c) lds[P::PC() + c * P::nt(C) + i] = p[c];
@@ -907,7 +918,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.n_coarse = n_coarse;
     A.rdt = rdt;
     A.rhsn2 = rhsn2;
-    A.keep = part == 2 ? keep : kKeepAll;
+    A.keep = part == 0 ? kKeepAll : keep;
     // tile: 2**fine_tl level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
     const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : fine_tl(n_split) - 2 * n_split;
     // un_eles [ua, ub) (ub < 0: all); ua a multiple of the tile, ub too unless it is U
@@ -959,10 +970,10 @@ bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mo
 
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                 int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2, int ua,
-                                int ub) {
+                                int ub, int keep) {
     if (L < 2) return hipSuccess;
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, nullptr, const_cast<double *>(rhsn2),
-                       1, kKeepAll, ua, ub);
+                       1, keep, ua, ub);
 }
 
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
