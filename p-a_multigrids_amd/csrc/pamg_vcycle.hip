@@ -58,6 +58,16 @@ using namespace detail;
 #ifndef PAMG_FINE_TL_MIN
 #define PAMG_FINE_TL_MIN 10
 #endif
+// level-1 tnew loads / stores and RHS loads of the V-cycle launches (A/B builds)
+#ifndef PAMG_NT_TL
+#define PAMG_NT_TL ((PAMG_NT & 1) != 0)
+#endif
+#ifndef PAMG_NT_TS
+#define PAMG_NT_TS ((PAMG_NT & 2) != 0)
+#endif
+#ifndef PAMG_NT_RL
+#define PAMG_NT_RL ((PAMG_NT & 1) != 0)
+#endif
 #ifndef PAMG_CHAIN_PRIO
 #define PAMG_CHAIN_PRIO 3
 #endif
@@ -163,23 +173,25 @@ __device__ __forceinline__ void store3(double *f, int64_t pitch, uint32_t s, con
 // the adjacent pair s, s+1 (s even) with 16-byte accesses
 // streamed with non-temporal 16-byte loads and stores (pamg_device.h PAMG_NT)
 typedef double v2d __attribute__((ext_vector_type(2)));
+template <bool NT = (PAMG_NT & 1) != 0>
 __device__ __forceinline__ void load3p(const double *f, int64_t pitch, uint32_t s, double a[3], double b[3]) {
     const uint32_t o = s << 3;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const v2d *q = reinterpret_cast<const v2d *>(reinterpret_cast<const char *>(f + c * pitch) + o);
-        const v2d v = (PAMG_NT & 1) ? __builtin_nontemporal_load(q) : *q;
+        const v2d v = NT ? __builtin_nontemporal_load(q) : *q;
         a[c] = v.x;
         b[c] = v.y;
     }
 }
+template <bool NT = (PAMG_NT & 2) != 0>
 __device__ __forceinline__ void store3p(double *f, int64_t pitch, uint32_t s, const double a[3], const double b[3]) {
     const uint32_t o = s << 3;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         v2d *q = reinterpret_cast<v2d *>(reinterpret_cast<char *>(f + c * pitch) + o);
         const v2d v = {a[c], b[c]};
-        if (PAMG_NT & 2) __builtin_nontemporal_store(v, q);
+        if (NT) __builtin_nontemporal_store(v, q);
         else *q = v;
     }
 }
@@ -712,8 +724,8 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     if constexpr (HOIST)
         if (coarsest_thread<S, L>(t)) coarsest_load<S, L>(A, t, u0, nue, xc, bc);
     if constexpr (NP == 2) {
-        load3p(V0.T(), V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
-        load3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
+        load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
+        load3p<PAMG_NT_RL>(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
     } else {
         load3(V0.T(), V0.pitch, s0, x0[0]);
         load3(V0.RHS(), V0.pitch, s0, b0[0]);
@@ -780,7 +792,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
         for (int k = 0; k < NP; ++k)
             if (keeph) hs_write(false, V0.H, w0, h0[k], p0[k]);
         if constexpr (NP == 2) {
-            store3p(V0.T(), V0.pitch, s0, p0[0], p0[1]);
+            store3p<PAMG_NT_TS>(V0.T(), V0.pitch, s0, p0[0], p0[1]);
             if (keep1) store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
         } else {
             store3(V0.T(), V0.pitch, s0, p0[0]);
