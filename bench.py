@@ -194,8 +194,9 @@ def main():
         elapsed = float(t.item())
     if not live_events:
         # per-launch events time each launch on its own: the post-pass runs the pipelined
-        # calls as one launch sequence (the timed region ran two tile halves on two streams)
-        s.set_tile_streams(1)
+        # calls as one launch per cycle (the timed region ran the partition's automatic
+        # schedule, two tile streams)
+        s.set_call_schedule(1)
         s.timing_enable(0x77F)
         s.timing_reset()
         s.vcycle(max(1, min(a.steps, 20)))
@@ -304,10 +305,10 @@ def main():
                        "arith": "contracted (fma, 1e-15 of the reference)" if a.arith else "reference order (bitwise)",
                        "fused": a.fused, "halo_exchange": "per call" if a.halo_exchange == 0 else "per cycle",
                        "comm": a.comm if world > 1 else None,
-                       "tile_streams": 2 if world > 1 else 1},
+                       "call_schedule": "two tile streams" if world > 1 else "one launch per cycle"},
             "roofline": {"bound": "hbm", "kernel": RK_DESC[rk],
                          "events": (f"timed region, the first and then 1 in {EVENT_STRIDE} launches" if live_events
-                                    else "post-pass of min(steps, 20) cycles, one launch sequence"),
+                                    else "post-pass of min(steps, 20) cycles, one launch per cycle"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "alg_bytes_per_launch": bytes_per_launch, "ms_per_launch": round(ms_per_launch, 4)},

@@ -162,11 +162,12 @@ int pamg_prolongator(pamg_handle *h, int level);
 int pamg_vcycle(pamg_handle *h, int n);
 /* the time loop :299-381 */
 int pamg_run(pamg_handle *h, int ntime, int n_multigrid);
-/* pipelined V-cycle calls (fused = 3, halo exchanged once per call): run the tiles as `n`
- * halves on their own HIP streams (1 or 2; 0 = automatic: 2 on a partition of a
- * multi-rank run, 1 otherwise). Every operation of a call is local to an un_ele, so the
- * halves need no ordering until the call's end; the state is bitwise the same either way. */
-int pamg_set_tile_streams(pamg_handle *h, int n);
+/* launch schedule of pipelined V-cycle calls (fused = 3, halo exchanged once per call).
+ * Every operation of a call is local to an un_ele, so tiles need no ordering until the
+ * call's end: 1 one launch per cycle; 2 the tiles as two halves on two HIP streams;
+ * 0 automatic (one GPU: 1; a partition of a multi-rank run: 2). The state after the call
+ * is bitwise the same in all. */
+int pamg_set_call_schedule(pamg_handle *h, int schedule);
 int pamg_synchronize(pamg_handle *h);
 
 /* ---- measurement ---- */

@@ -440,16 +440,22 @@ int vcycle_fused(pamg_handle *h, int n) {
     // pipelined, halo exchanged once per call: the tiles are independent for the whole call
     // (every operation is local to an un_ele, the halo words have no reader inside it), so two
     // halves of them can run their launch sequences on two streams, each launch's drain
-    // overlapped by the other half's stream (pamg_set_tile_streams; PAMG_TILE_STREAMS=<n>
-    // overrides for A/B runs). Measured (scripts/ab_probe.py, profiles/r01_v16_tile_streams.txt):
+    // overlapped by the other half's stream (schedule 2). Measured (scripts/ab_probe.py, profiles/r01_v16_tile_streams.txt):
     // N = 4 partition 0.0404 -> 0.0339 ms per cycle, N = 8 0.0208 -> 0.0202, n_split = 3
     // 0.0128 -> 0.0114, full mesh 0.1319 -> 0.1290. Automatic on partitions only: on one GPU
-    // the bench's per-launch events would time two overlapped half-launches.
-    static const int ts_env = getenv("PAMG_TILE_STREAMS") ? atoi(getenv("PAMG_TILE_STREAMS")) : -1;
-    const int tile_streams = ts_env >= 0 ? ts_env : h->tile_streams ? h->tile_streams : (h->nranks > 1 ? 2 : 1);
+    // the bench's per-launch events time launches, which schedule 2 overlaps.
+    //
+    // pamg_set_call_schedule(h, s): 0 automatic (2 on a partition of a multi-rank run, 1 on
+    // one GPU), 1 one launch per cycle, 2 two tile streams; PAMG_CALL_SCHEDULE=<s> overrides
+    // for A/B runs. (A persistent form -- one launch whose workgroups loop over their tile's
+    // cycles -- was tried: the loop pushed the launch from 62 to 128 VGPRs with spills, and
+    // it is not kept.)
+    static const int cs_env = getenv("PAMG_CALL_SCHEDULE") ? atoi(getenv("PAMG_CALL_SCHEDULE")) : -1;
     const int tile = vcycle_tile_un_eles(h->p.n_split);
     const int ntiles = (h->U + tile - 1) / tile;
-    if (pipe && n > 1 && tile_streams == 2 && h->p.halo_exchange == 0 && ntiles >= 2) {
+    int sched = cs_env >= 0 ? cs_env : h->call_schedule;
+    if (sched == 0) sched = h->nranks > 1 ? 2 : 1;
+    if (pipe && n > 1 && sched == 2 && h->p.halo_exchange == 0 && ntiles >= 2) {
         const int buf = two ? 1 - P1.send_cur : 0;
         if (h->sent_pending[buf]) {
             HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[buf], 0));
@@ -952,9 +958,9 @@ int pamg_timing_reset(pamg_handle *h) {
     return PAMG_OK;
 }
 
-int pamg_set_tile_streams(pamg_handle *h, int n) {
-    if (!h || n < 0 || n > 2) return PAMG_ERR_ARG;
-    h->tile_streams = n;
+int pamg_set_call_schedule(pamg_handle *h, int schedule) {
+    if (!h || schedule < 0 || schedule > 2) return PAMG_ERR_ARG;
+    h->call_schedule = schedule;
     return PAMG_OK;
 }
 

@@ -132,7 +132,7 @@ struct pamg_handle {
     // fused = 2: the coarse-level launch of each cycle runs on stream_c beside the level-1
     // launch on `stream`; ev_fine / ev_coarse order them across cycles (RHSN of level 2)
     hipStream_t stream_c = nullptr;
-    int tile_streams = 0;   // pamg_set_tile_streams (0: automatic)
+    int call_schedule = 0;   // pamg_set_call_schedule (0: automatic)
     hipEvent_t ev_fine = nullptr, ev_coarse = nullptr;
     // RHSN of every level holds the restriction of the finer level's current residual
     bool rhsn_valid = true;

@@ -79,7 +79,7 @@ def lib():
         "pamg_timing_enable": (I, [P, C.c_uint]),
         "pamg_timing_reset": (I, [P]),
         "pamg_timing_stride": (I, [P, I]),
-        "pamg_set_tile_streams": (I, [P, I]),
+        "pamg_set_call_schedule": (I, [P, I]),
         "pamg_timing_issued": (I, [P, I, C.POINTER(C.c_long)]),
         "pamg_timing_read": (I, [P, I, C.POINTER(D), C.POINTER(C.c_long), C.POINTER(D)]),
         "pamg_sweep_bench": (I, [P, I, I, C.POINTER(D), C.POINTER(D)]),

@@ -185,9 +185,10 @@ class SemiImplicitIterative:
     def timing_reset(self): self._call("pamg_timing_reset")
     def timing_stride(self, every): self._call("pamg_timing_stride", every)
 
-    def set_tile_streams(self, n):
-        """Pipelined calls: tiles in n halves on their own streams (0 automatic, 1, 2)."""
-        self._call("pamg_set_tile_streams", n)
+    def set_call_schedule(self, schedule):
+        """Pipelined calls: 0 automatic, 1 one launch per cycle, 2 two tile streams
+        (pamg_set_call_schedule)."""
+        self._call("pamg_set_call_schedule", schedule)
 
     def timing(self):
         out = {}

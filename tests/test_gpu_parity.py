@@ -389,15 +389,17 @@ def test_pipelined_call_boundaries_are_invisible(mesh, S, L, arith):
 
 
 @pytest.mark.parametrize("mesh,S,L,n", [("untitled8192.msh", 5, 3, 5), ("untitled8192.msh", 3, 3, 2),
-                                        ("irregular.msh", 4, 4, 3), ("900_ele.msh", 3, 2, 4)])
-def test_tile_streams_equal_one_sequence(mesh, S, L, n):
-    """Pipelined calls with the tiles in two halves on two streams (pamg_set_tile_streams(2))
-    leave the state of one launch sequence, bit for bit, including t_overlap."""
+                                        ("irregular.msh", 4, 4, 3), ("900_ele.msh", 3, 2, 4),
+                                        ("untitled8192.msh", 5, 4, 4), ("untitled2048.msh", 5, 5, 3)])
+@pytest.mark.parametrize("arith", [0, 1])
+def test_call_schedules_equal_one_sequence(mesh, S, L, n, arith):
+    """Pipelined calls as two tile halves on two streams (schedule 2) leave the state of one
+    launch per cycle, bit for bit, t_overlap included."""
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
     runs = []
     for ts in (1, 2):
-        s = pamg.SemiImplicitIterative(m, S, L, arith=1, fused=3)
-        s.set_tile_streams(ts)
+        s = pamg.SemiImplicitIterative(m, S, L, arith=arith, fused=3)
+        s.set_call_schedule(ts)
         s.begin_timestep()
         s.vcycle(n)
         s.vcycle(1)
@@ -405,5 +407,6 @@ def test_tile_streams_equal_one_sequence(mesh, S, L, n):
         st["t_overlap"], st["t_overlap_old"] = s.overlap()
         runs.append(st)
         s.close()
-    for k in runs[0]:
-        np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+    for r in runs[1:]:
+        for k in runs[0]:
+            np.testing.assert_array_equal(r[k], runs[0][k], err_msg=k)
