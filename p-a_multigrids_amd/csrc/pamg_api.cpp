@@ -228,10 +228,16 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
     return halo(h, l);
 }
 
+// PAMG_RHS_TOLD_HALO (A/B builds): k_rhs writes the compact told copy of the halo at the start of a
+// step (1) or k_told_halo gathers it afterwards (0, default: the folded form measured 1.4 % slower
+// on the time loop, scripts/ab_tl.sh, profiles/r01_v17_time_loop.txt)
+#ifndef PAMG_RHS_TOLD_HALO
+#define PAMG_RHS_TOLD_HALO 0
+#endif
 int rhs_level1(pamg_handle *h, int start_of_step) {
     Level &L = h->lv[1];
     Span sp(h, PAMG_K_RHS, (start_of_step == 1 ? 96.0 : start_of_step == 2 ? 72.0 : 48.0) * (double)L.N);
-    HIPCHK(h, launch_rhs(h->stream, L, h->geo1, 1 / h->p.dt, h->p.k, start_of_step));
+    HIPCHK(h, launch_rhs(h->stream, L, h->geo1, 1 / h->p.dt, h->p.k, start_of_step, PAMG_RHS_TOLD_HALO && start_of_step != 0));
     return PAMG_OK;
 }
 
@@ -826,8 +832,10 @@ int begin_timestep(pamg_handle *h, bool tnn_dead) {
         HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
         return refresh_told_halo(h, 1);
     }
-    CHK(rhs_level1(h, tnn_dead ? 2 : 1));
-    return refresh_told_halo(h, 1);
+    CHK(rhs_level1(h, tnn_dead ? 2 : 1));   // also the compact told copy of the halo (refresh_told_halo)
+    if (!PAMG_RHS_TOLD_HALO) return refresh_told_halo(h, 1);
+    h->overlap_static_l1 = false;
+    return PAMG_OK;
 }
 
 int pamg_begin_timestep(pamg_handle *h) {

@@ -168,7 +168,9 @@ hipError_t launch_interp_add(hipStream_t s, const Level &fine, const Level &coar
 hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U, double *out = nullptr);
 hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn);
 // start_of_step: 0 RHS from told; 1 told := tnew_nonlin := tnew first; 2 told := tnew first
-hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, int start_of_step);
+// told_halo: with start_of_step, also write the compact told copy of the halo (launch_told_halo)
+hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, int start_of_step,
+                      bool told_halo = false);
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
 hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
 hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);

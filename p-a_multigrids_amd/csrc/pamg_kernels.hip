@@ -178,34 +178,9 @@ __global__ __launch_bounds__(kBlock) void k_interp_add(double *T, const double *
         for (int i = 0; i < 3; ++i) T[i * pitch_f + f[q]] = T[i * pitch_f + f[q]] + add[q][i];
 }
 
-// Level-1 right-hand side + time-step start (:316-317, :593, get_RHS :452-464):
-// told := tnew, tnew_nonlin := tnew, source s_j = -2k sin(x_j + y_j) at the
-// sub-element nodes (get_splitting coordinates), cascaded in place through M,
-// RHS_i = rdt (M told)_i + s'_i. start_of_step 2: the same without the tnew_nonlin store
-// (pamg_run: the V-cycle that follows rewrites it before any read, :327).
-__global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, double *TOLD,
-                                                double *__restrict__ TNN, double *__restrict__ RHS,
-                                                const double *__restrict__ stc, const double *__restrict__ geo,
-                                                const int2 *__restrict__ subinfo, int64_t pitch, int64_t N,
-                                                int nsub_log2, double rdt, double k, int start_of_step) {
-    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (s >= N) return;
-    const int64_t u = s >> nsub_log2;
-    const int sub = (int)(s & ((1ll << nsub_log2) - 1));
-    double t[3];
-    if (start_of_step) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            t[c] = T[c * pitch + s];
-            TOLD[c * pitch + s] = t[c];
-            if (start_of_step == 1) TNN[c * pitch + s] = t[c];
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) t[c] = TOLD[c * pitch + s];
-    }
-    const double *g = geo + u * kGeoStride;
-    const int2 ri = subinfo[sub];
+// one sub-element s of un_ele u: RHS from its told t (the reference's operation order)
+__device__ __forceinline__ void rhs_one(const double *__restrict__ g, const double *__restrict__ M, int2 ri, double rdt,
+                                        double k, const double t[3], double rhs[3]) {
     const int irow = ri.x, ipos = ri.y;
     double xl[3][2];
 #pragma unroll
@@ -221,7 +196,6 @@ __global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, do
             xl[2][d] = x3 + (double)irow * v2 + v1 * (double)(ipos / 2);
         }
     }
-    const double *M = stc + u * kStcStride + kStcM;
     double src[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) src[i] = -(2 * k * sin(xl[i][0] + xl[i][1]));
@@ -229,8 +203,63 @@ __global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, do
     for (int i = 0; i < 3; ++i) {
         src[i] = M[3 * i] * src[0] + M[3 * i + 1] * src[1] + M[3 * i + 2] * src[2];
         const double mo = rdt * (M[3 * i] * t[0] + M[3 * i + 1] * t[1] + M[3 * i + 2] * t[2]);
-        RHS[i * pitch + s] = mo + src[i];
+        rhs[i] = mo + src[i];
     }
+}
+
+// Level-1 right-hand side + time-step start (:316-317, :593, get_RHS :452-464):
+// told := tnew, tnew_nonlin := tnew, source s_j = -2k sin(x_j + y_j) at the
+// sub-element nodes (get_splitting coordinates), cascaded in place through M,
+// RHS_i = rdt (M told)_i + s'_i. start_of_step 2: the same without the tnew_nonlin store
+// (pamg_run: the V-cycle that follows rewrites it before any read, :327).
+// One adjacent pair of sub-elements per thread (same un_ele: nsub is a power of 4), the
+// state planes streamed with 16-byte non-temporal accesses (ld2 / st2). told_halo (start of a
+// step): also the compact told copy of k_told_halo, from the told values in registers.
+__global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, double *TOLD,
+                                                double *__restrict__ TNN, double *__restrict__ RHS,
+                                                const double *__restrict__ stc, const double *__restrict__ geo,
+                                                const int2 *__restrict__ subinfo, int64_t pitch, int64_t N,
+                                                int nsub_log2, double rdt, double k, int start_of_step,
+                                                const int4 *__restrict__ hsub, const int4 *__restrict__ hface,
+                                                double *__restrict__ told_halo) {
+    const int64_t s = 2 * ((int64_t)blockIdx.x * kBlock + threadIdx.x);
+    if (s >= N) return;
+    const int64_t u = s >> nsub_log2;
+    const int sub = (int)(s & ((1ll << nsub_log2) - 1));
+    double t0[3], t1[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double2 v = ld2((start_of_step ? T : TOLD) + c * pitch + s);
+        t0[c] = v.x;
+        t1[c] = v.y;
+        if (start_of_step) {
+            st2(TOLD + c * pitch + s, v);
+            if (start_of_step == 1) st2(TNN + c * pitch + s, v);
+        }
+    }
+    if (told_halo) {   // the compact told copy of the halo's sub-elements (k_told_halo's words)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int4 hs = hsub[sub + q];
+            const int pos[3] = {hs.x, hs.y, hs.z};
+#pragma unroll
+            for (int f = 0; f < 3; ++f) {
+                if (!pos[f]) continue;
+                const int4 rec = hface[3 * u + f];
+                if ((rec.x & 3) == 0) continue;
+                double *o = told_halo + 3 * (int64_t)(rec.w + pos[f] - 1);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) o[c] = q ? t1[c] : t0[c];
+            }
+        }
+    }
+    const double *g = geo + u * kGeoStride;
+    const double *M = stc + u * kStcStride + kStcM;
+    double r0[3], r1[3];
+    rhs_one(g, M, subinfo[sub], rdt, k, t0, r0);
+    rhs_one(g, M, subinfo[sub + 1], rdt, k, t1, r1);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) st2(RHS + c * pitch + s, make_double2(r0[c], r1[c]));
 }
 
 // restrictor (splitting.F90:10-32): RHS_{l+1}(:, c) = averages of the fine
@@ -753,10 +782,13 @@ hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse,
     return hipGetLastError();
 }
 
-hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, int start_of_step) {
+hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, int start_of_step,
+                      bool told_halo) {
     if (L.N == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rhs, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.T, L.TOLD, L.TNN, L.RHS, L.stc, geo1,
-                       L.subinfo, L.pitch, L.N, log2i(L.nsub), rdt, k, start_of_step);
+    if ((L.N & 1) || (L.pitch & 1)) return hipErrorInvalidValue;   // pairs of one un_ele, 16-byte aligned
+    hipLaunchKernelGGL(k_rhs, dim3(grid_for(L.N / 2)), dim3(kBlock), 0, s, L.T, L.TOLD, L.TNN, L.RHS, L.stc, geo1,
+                       L.subinfo, L.pitch, L.N, log2i(L.nsub), rdt, k, start_of_step, L.halo.d_hsub, L.halo.d_hface,
+                       (told_halo && start_of_step && L.halo.d_hface && L.halo.d_hsub) ? L.halo.d_told_halo : nullptr);
     return hipGetLastError();
 }
 
