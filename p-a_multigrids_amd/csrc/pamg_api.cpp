@@ -296,9 +296,9 @@ int prolong(pamg_handle *h, int l, bool fused_copy) {
 //                   level 2 reads the final tnew (prolongator) and writes RHSN (48 B)
 //   coarse launch:  level l >= 2 reads tnew, RHSN and writes RHS, residual, tnew (120 B);
 //                   RHSN of the levels l >= 3 is written here too (24 B)
-double vcycle_fine_bytes(pamg_handle *h) {
+double vcycle_fine_bytes(pamg_handle *h, int keep = PAMG_KEEP_ALL) {
     const int L = h->p.multi_levels;
-    return 120.0 * h->lv[1].N + (L > 1 ? 48.0 * h->lv[2].N : 0.0) + 104.0 * h->U;
+    return (keep & PAMG_KEEP_L1 ? 120.0 : 72.0) * h->lv[1].N + (L > 1 ? 48.0 * h->lv[2].N : 0.0) + 104.0 * h->U;
 }
 double vcycle_coarse_bytes(pamg_handle *h, int keep = PAMG_KEEP_ALL) {
     const int L = h->p.multi_levels;
@@ -414,7 +414,12 @@ int vcycle_corrected(pamg_handle *h) {
 }
 
 // n V-cycles as two fused launches each (pamg_vcycle.hip)
-int vcycle_fused(pamg_handle *h, int n) {
+// dead_after (pamg_run, every step but the last): the next call rewrites the fields this one
+// leaves for an observer -- level 1's residual and tnew_nonlin, the coarse levels' RHS and
+// residual, the halo words -- before any read (nothing reads t_overlap, the next step's first
+// restrictor reads level 2's RHSN, which is stored), so the pipelined schedule skips them
+// and the exchange of the halo words too
+int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     const double rdt = 1 / h->p.dt;
     HaloPlan &P1 = h->lv[1].halo;
@@ -475,6 +480,7 @@ int vcycle_fused(pamg_handle *h, int n) {
         // the first coarse launch's RHS and residual are rewritten by the first pipelined one
         const int ck = pipe_keep_env() & PAMG_KEEP_COARSE;
         const int ua[2] = {0, mid}, ub[2] = {mid, h->U};
+        const int kf = dead_after ? pipe_keep_env() : PAMG_KEEP_ALL;   // the call's last level-1 launch
         for (int q = 0; q < 2; ++q) {
             Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h, ck) * (ub[q] - ua[q]) / h->U, st[q]);
             HIPCHK(h, launch_vcycle_coarse(st[q], h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
@@ -482,11 +488,11 @@ int vcycle_fused(pamg_handle *h, int n) {
         }
         for (int c = 0; c < n; ++c) {
             const bool pc = c + 1 < n;
-            const int keep = pipe_keep_env() | (c + 2 == n ? PAMG_KEEP_COARSE : 0);
+            const int keep = pc ? pipe_keep_env() | (c + 2 == n && !dead_after ? PAMG_KEEP_COARSE : 0) : kf;
             for (int q = 0; q < 2; ++q) {
                 const double f = (double)(ub[q] - ua[q]) / h->U;
                 Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE,
-                        f * (pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h)), st[q]);
+                        f * (pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h, keep)), st[q]);
                 HIPCHK(h, launch_vcycle_fine(st[q], h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
                                              h->tovo, P1.send_buf(buf), L2.RHSN, pc, keep, ua[q], ub[q]));
             }
@@ -494,6 +500,10 @@ int vcycle_fused(pamg_handle *h, int n) {
         HIPCHK(h, hipEventRecord(h->ev_coarse, h->stream_c));
         HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));
         h->tnn_level = 1;
+        if (dead_after) {
+            P1.send_cur = buf;
+            return join_comm(h);
+        }
         CHK(halo_async(h, buf));
         return join_comm(h);
     }
@@ -501,7 +511,7 @@ int vcycle_fused(pamg_handle *h, int n) {
         HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));   // everything issued before this call
     }
     if (pipe && n > 0) {   // its RHS and residual stores are rewritten by the first pipelined launch if n > 1
-        const int ck = n > 1 ? pipe_keep_env() & PAMG_KEEP_COARSE : PAMG_KEEP_ALL;
+        const int ck = (n > 1 || dead_after) ? pipe_keep_env() & PAMG_KEEP_COARSE : PAMG_KEEP_ALL;
         Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h, ck));
         HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
                                        h->tovo, L2.RHSN, 0, -1, ck));
@@ -530,9 +540,12 @@ int vcycle_fused(pamg_handle *h, int n) {
             // residual and tnew_nonlin always (the call's last launch is k_vc_fine, which stores
             // them), the coarse levels' RHS and residual unless they reach their final cycle
             // here, the halo words unless every cycle's are exchanged
-            const int keep = pipe_keep_env() | (c + 2 == n ? PAMG_KEEP_COARSE : 0) |
-                             (h->p.halo_exchange == 1 ? PAMG_KEEP_HALO : 0);
-            Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE, pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h));
+            const bool dead = pipe && dead_after && h->p.halo_exchange == 0;
+            const int keep = pc ? pipe_keep_env() | (c + 2 == n && !dead ? PAMG_KEEP_COARSE : 0) |
+                                      (h->p.halo_exchange == 1 ? PAMG_KEEP_HALO : 0)
+                                : (dead && c + 1 == n ? pipe_keep_env() : PAMG_KEEP_ALL);
+            Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE,
+                    pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h, keep));
             HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
                                          h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr, pc, keep));
             if (conc) HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));
@@ -543,7 +556,8 @@ int vcycle_fused(pamg_handle *h, int n) {
         // packed into `buf`); the next cycle rewrites every one of them and nothing reads
         // t_overlap in between: halo_exchange = 0 exchanges the last cycle's words only,
         // 1 every cycle's, in flight during the next one
-        if (h->p.halo_exchange == 1 || c + 1 == n) CHK(halo_async(h, buf));
+        if (h->p.halo_exchange == 1 || (c + 1 == n && !(pipe && dead_after))) CHK(halo_async(h, buf));
+        else if (c + 1 == n) P1.send_cur = buf;
     }
     if (conc && n > 0) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));   // join
     return join_comm(h);
@@ -890,8 +904,7 @@ int pamg_prolongator(pamg_handle *h, int level) {
     return prolong(h, level, false);
 }
 
-int pamg_vcycle(pamg_handle *h, int n) {
-    if (!h || n < 0) return PAMG_ERR_ARG;
+int vcycle(pamg_handle *h, int n, bool dead_after) {
     CHK(check_level(h, 1));
     const int L = h->p.multi_levels;
     if (h->p.cycle == 1) {
@@ -900,9 +913,14 @@ int pamg_vcycle(pamg_handle *h, int n) {
     }
     if (h->p.fused && h->p.coarse_solver == 0 &&
         vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth))
-        return vcycle_fused(h, n);
+        return vcycle_fused(h, n, dead_after);
     for (int c = 0; c < n; ++c) CHK(vcycle_steps(h));
     return PAMG_OK;
+}
+
+int pamg_vcycle(pamg_handle *h, int n) {
+    if (!h || n < 0) return PAMG_ERR_ARG;
+    return vcycle(h, n, false);
 }
 
 int pamg_direct_solve(pamg_handle *h, int level) {
@@ -940,7 +958,7 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
     if (!h || ntime < 0 || n_multigrid < 0) return PAMG_ERR_ARG;
     for (int t = 0; t < ntime; ++t) {
         CHK(begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0));
-        CHK(pamg_vcycle(h, n_multigrid));
+        CHK(vcycle(h, n_multigrid, t + 1 < ntime));   // a step's leftovers die in the next one
     }
     return PAMG_OK;
 }

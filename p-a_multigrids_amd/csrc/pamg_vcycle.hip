@@ -118,8 +118,7 @@ struct VArgs {
 // the call's last cycle with halo_exchange = 0). The call's final level-1 launch (k_vc_fine,
 // PIPE = false) stores all of level 1's fields and halo words; its last pipelined launch, the
 // one that leaves the coarse levels at their final cycle, keeps kKeepCoarse.
-constexpr int kKeepL1 = PAMG_KEEP_L1, kKeepCoarse = PAMG_KEEP_COARSE, kKeepHalo = PAMG_KEEP_HALO,
-              kKeepAll = PAMG_KEEP_ALL;
+constexpr int kKeepL1 = PAMG_KEEP_L1, kKeepCoarse = PAMG_KEEP_COARSE, kKeepHalo = PAMG_KEEP_HALO;
 
 // phase stamps: 100 MHz wall clock per wave at the phase boundaries, plus the wave's HW_ID
 // (diagnostics build only: make PAMG_STAMPS=1; the pointer costs SGPRs the kernels need)
@@ -711,7 +710,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     stamp<MT>(A, 0);
     stamp_hwid<MT>(A);
     const VLevel &V0 = A.lv[0];
-    const bool keep1 = !PIPE || (A.keep & kKeepL1), keeph = !PIPE || (A.keep & kKeepHalo);
+    const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo;
     const bool v0 = NP * t < (nue << G::lg(0));
     const uint32_t s0 = ((uint32_t)u0 << G::lg(0)) + (v0 ? NP * t : 0);   // clamped: loads stay in bounds
     const uint32_t w0 = s0 >> G::lg(0);                                   // un_ele of the thread's sub-elements
@@ -930,7 +929,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.n_coarse = n_coarse;
     A.rdt = rdt;
     A.rhsn2 = rhsn2;
-    A.keep = part == 0 ? kKeepAll : keep;
+    A.keep = keep;
     // tile: 2**fine_tl level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
     const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : fine_tl(n_split) - 2 * n_split;
     // un_eles [ua, ub) (ub < 0: all); ua a multiple of the tile, ub too unless it is U

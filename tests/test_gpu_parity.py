@@ -410,3 +410,52 @@ def test_call_schedules_equal_one_sequence(mesh, S, L, n, arith):
     for r in runs[1:]:
         for k in runs[0]:
             np.testing.assert_array_equal(r[k], runs[0][k], err_msg=k)
+
+
+@pytest.mark.parametrize("mesh,S,L,n", [("untitled8192.msh", 5, 3, 2), ("irregular.msh", 4, 4, 3),
+                                        ("900_ele.msh", 3, 2, 1), ("untitled2048.msh", 5, 5, 2)])
+@pytest.mark.parametrize("schedule", [1, 2])
+def test_time_loop_equals_public_steps(mesh, S, L, n, schedule):
+    """pamg_run skips what a step leaves that the next step overwrites unread (the step-start
+    tnew_nonlin copy, the last cycle's residual / tnew_nonlin / coarse RHS and residual / halo
+    words and their exchange): its state after 3 steps equals 3 x (begin_timestep; vcycle),
+    bit for bit, t_overlap included."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    a = pamg.SemiImplicitIterative(m, S, L, arith=1, fused=3)
+    b = pamg.SemiImplicitIterative(m, S, L, arith=1, fused=3)
+    for s in (a, b):
+        s.set_call_schedule(schedule)
+    a.run(3, n)
+    for _ in range(3):
+        b.begin_timestep()
+        b.vcycle(n)
+    sa, sb = a.state(), b.state()
+    for k in sb:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    for x, y in zip(a.overlap(), b.overlap()):
+        np.testing.assert_array_equal(x, y)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("S,nparts", [(3, 2), (5, 8)])
+def test_partitioned_time_loop_matches_single_gpu(S, nparts):
+    """Several time steps on partitions (pamg_run skips the exchanges of all but the last
+    step) leave the single-domain state after the loopback exchange, bit for bit."""
+    mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
+    full = pamg.SemiImplicitIterative(mesh, S, 3)
+    full.run(3, 2)
+    owner = mesh.x_strip_owner(nparts)
+    parts = [pamg.SemiImplicitIterative(mesh, S, 3, comm=(nparts, r, None, owner), fused=3)
+             for r in range(nparts)]
+    for p in parts:
+        p.run(3, 2)
+    halo_loopback(parts, 1)
+    ref_state = full.state()
+    ref_ov = full.overlap()
+    for r, p in enumerate(parts):
+        own = np.flatnonzero(owner == r)
+        for k, v in p.state().items():
+            np.testing.assert_array_equal(v, ref_state[k][:, :, own], err_msg=k)
+        for x, y in zip(p.overlap(), ref_ov):
+            np.testing.assert_array_equal(x, y[:, :, own])
