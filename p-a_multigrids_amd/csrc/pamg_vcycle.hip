@@ -68,6 +68,11 @@ using namespace detail;
 #ifndef PAMG_NT_RL
 #define PAMG_NT_RL ((PAMG_NT & 1) != 0)
 #endif
+// issue priority of the pipelined launch's coarse tail (A/B builds; 1 and 2 measured within noise
+// of 0, profiles/r01_v18_tail_prio_ab.txt)
+#ifndef PAMG_TAIL_PRIO
+#define PAMG_TAIL_PRIO 0
+#endif
 #ifndef PAMG_CHAIN_PRIO
 #define PAMG_CHAIN_PRIO 3
 #endif
@@ -822,6 +827,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     }
     if constexpr (PIPE) {
         const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
+        if (PAMG_TAIL_PRIO) __builtin_amdgcn_s_setprio(PAMG_TAIL_PRIO);
         coarse_next<S, L, ST, HOIST>(A, SP, t, u0, nue, y1, rn, F0);
     }
     stamp<MT>(A, 7);
