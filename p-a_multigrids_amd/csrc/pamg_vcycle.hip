@@ -111,7 +111,7 @@ struct VArgs {
     double rdt;
     double *rhsn2;          // level 2's RHSN buffer: read by the coarse launch, written by the level-1 launch
     long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
-    int keep;               // pipelined launch: the dead-until-final stores it makes (kKeep*)
+    int keep;               // the dead-until-final stores the launch makes (kKeep*)
     int64_t tile0;          // first tile of the launch (a launch may cover a range of tiles)
 };
 
@@ -122,7 +122,8 @@ struct VArgs {
 // registers and LDS in this one) and the halo words (rewritten every cycle; exchanged after
 // the call's last cycle with halo_exchange = 0). The call's final level-1 launch (k_vc_fine,
 // PIPE = false) stores all of level 1's fields and halo words; its last pipelined launch, the
-// one that leaves the coarse levels at their final cycle, keeps kKeepCoarse.
+// one that leaves the coarse levels at their final cycle, keeps kKeepCoarse. Inside pamg_run
+// every step but the last skips those too (the next step overwrites them unread).
 constexpr int kKeepL1 = PAMG_KEEP_L1, kKeepCoarse = PAMG_KEEP_COARSE, kKeepHalo = PAMG_KEEP_HALO;
 
 // phase stamps: 100 MHz wall clock per wave at the phase boundaries, plus the wave's HW_ID
