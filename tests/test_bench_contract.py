@@ -1,0 +1,32 @@
+"""bench.py's one-line JSON contract on one GPU (a small, fast configuration)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+
+
+@pytest.mark.gpu
+def test_bench_prints_the_contract_line():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+                        "--nsplit", "3", "--no-extra", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2
+    assert d["unit"] == "V-cycles/s" and d["higher_is_better"] is True and d["dtype"] == "f64"
+    assert d["value"] > 0 and abs(d["ms_per_step"] - 1e3 / d["value"]) < 1e-3 * max(1.0, 1e3 / d["value"])
+    assert "workload" in d["config"]
+    rf = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rf, k
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert 0 < rf["frac"] < 2.0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
