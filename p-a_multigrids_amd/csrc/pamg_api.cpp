@@ -247,6 +247,7 @@ int restrict_(pamg_handle *h, int l);
 // told changed on level l: refresh the compact told copy the halo reads
 int refresh_told_halo(pamg_handle *h, int l) {
     h->overlap_static_l1 = false;
+    if (l == 1) h->told_halo_stale_l1 = false;
     HIPCHK(h, launch_told_halo(h->stream, h->lv[l], h->U));
     return PAMG_OK;
 }
@@ -431,7 +432,8 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
     }
     if (!h->overlap_static_l1) {   // once per time step: the halo words the cycle's last smoother
         CHK(join_comm(h));         // leaves constant (into both send buffers)
-        HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo));
+        HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, nullptr, h->told_halo_stale_l1));
+        h->told_halo_stale_l1 = false;
         if (two) HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, P1.d_send_b));
         h->overlap_static_l1 = true;
     }
@@ -836,8 +838,10 @@ int pamg_get_overlap(pamg_handle *h, double *tov, double *tovo) {
 }
 
 // tnn_dead: the caller runs a V-cycle next, whose first smoother call rewrites tnew_nonlin
-// (:327) before any read, so the :317 copy is not stored (pamg_run)
-int begin_timestep(pamg_handle *h, bool tnn_dead) {
+// (:327) before any read, so the :317 copy is not stored (pamg_run); told_lazy: that V-cycle
+// is the fused one, whose k_overlap_static refreshes the compact told copy of the halo from
+// TOLD itself (one launch instead of k_told_halo + k_overlap_static)
+int begin_timestep(pamg_handle *h, bool tnn_dead, bool told_lazy = false) {
     CHK(check_level(h, 1));
     h->tnn_level = 1;
     if (h->p.solver == 2) {   // solve_Richardson never calls get_RHS inside the smoother
@@ -847,9 +851,12 @@ int begin_timestep(pamg_handle *h, bool tnn_dead) {
         return refresh_told_halo(h, 1);
     }
     CHK(rhs_level1(h, tnn_dead ? 2 : 1));   // also the compact told copy of the halo (refresh_told_halo)
-    if (!PAMG_RHS_TOLD_HALO) return refresh_told_halo(h, 1);
-    h->overlap_static_l1 = false;
-    return PAMG_OK;
+    if (PAMG_RHS_TOLD_HALO || told_lazy) {
+        h->overlap_static_l1 = false;
+        h->told_halo_stale_l1 = !PAMG_RHS_TOLD_HALO;
+        return PAMG_OK;
+    }
+    return refresh_told_halo(h, 1);
 }
 
 int pamg_begin_timestep(pamg_handle *h) {
@@ -957,7 +964,10 @@ int pamg_block_inverse(pamg_handle *h, int n, long nb, const double *A, double *
 int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
     if (!h || ntime < 0 || n_multigrid < 0) return PAMG_ERR_ARG;
     for (int t = 0; t < ntime; ++t) {
-        CHK(begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0));
+        const int L = h->p.multi_levels;
+        const bool fused_next = n_multigrid > 0 && h->p.cycle == 0 && h->p.fused && h->p.coarse_solver == 0 &&
+                                vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth);
+        CHK(begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0, fused_next));
         CHK(vcycle(h, n_multigrid, t + 1 < ntime));   // a step's leftovers die in the next one
     }
     return PAMG_OK;

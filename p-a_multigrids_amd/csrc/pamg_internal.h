@@ -124,6 +124,9 @@ struct pamg_handle {
     // time step (the fused V-cycle then writes only the tnew words); cleared by every
     // operation that writes or changes them otherwise
     bool overlap_static_l1 = false;
+    // level 1's compact told copy of the halo is behind TOLD (pamg_run started a step without
+    // refreshing it); the fused V-cycle's k_overlap_static writes it from TOLD
+    bool told_halo_stale_l1 = false;
     // the fused V-cycle's halo exchange (RCCL) runs on stream_comm, overlapped with the next
     // cycle; joined back into `stream` before pamg_vcycle returns
     hipStream_t stream_comm = nullptr;
@@ -174,8 +177,10 @@ hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double 
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
 hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
 hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);
+// from_told: read told from the TOLD planes and also write the compact told copy
+// (launch_told_halo's words) instead of reading that copy
 hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo,
-                                 double *send = nullptr);
+                                 double *send = nullptr, bool from_told = false);
 // fused V-cycle (pamg_vcycle.hip); lv is the handle's 1-based level array
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth);
 // levels 2..L; the level-2 RHS is taken from rhsn2 (level 2's RHSN or RHSN_alt)

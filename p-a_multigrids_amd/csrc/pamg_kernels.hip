@@ -50,7 +50,11 @@ __global__ __launch_bounds__(kBlock) void k_told_halo(const double *__restrict__
 // the level's smoother writes them (update_overlaps, splitting.F90:1210-1397); one
 // thread per (un_ele, face, position), the order of k_told_halo. The fused V-cycle
 // writes only the tnew words; this kernel runs before its first launch in a time step.
-__global__ __launch_bounds__(kBlock) void k_overlap_static(HaloArgs H, const int *__restrict__ surf, int U) {
+// TOLD != null (pamg_run's steps): told straight from the TOLD planes, and the compact told copy
+// of k_told_halo written on the way (same threads, same words: one launch instead of two).
+__global__ __launch_bounds__(kBlock) void k_overlap_static(HaloArgs H, const int *__restrict__ surf, int U,
+                                                           const double *__restrict__ TOLD, int64_t pitch,
+                                                           int nsub_log2) {
     const int m = H.m;
     const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (idx >= (int64_t)U * 3 * m) return;
@@ -59,7 +63,17 @@ __global__ __launch_bounds__(kBlock) void k_overlap_static(HaloArgs H, const int
     const int64_t q = idx / (3 * m);
     const int4 rec = H.hface[3 * q + f - 1];
     double to[3] = {0.0, 0.0, 0.0};
-    if (rec.x & 3) {
+    if (TOLD) {
+        if (rec.x & 3) {
+            const int64_t s = (q << nsub_log2) + surf[(i - 1) + (f - 1) * m] - 1;
+            double *o = const_cast<double *>(H.told) + 3 * (int64_t)(rec.w + i - 1);   // d_told_halo
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                to[c] = TOLD[c * pitch + s];
+                o[c] = to[c];
+            }
+        }
+    } else if (rec.x & 3) {
         // the sub-element's told sits in the compact told halo at its first copied face
         const int sub = surf[(i - 1) + (f - 1) * m] - 1;
         const int4 hs = H.hsub[sub];
@@ -817,12 +831,14 @@ hipError_t launch_told_halo(hipStream_t s, const Level &L, int U) {
     return hipGetLastError();
 }
 
-hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo, double *send) {
+hipError_t launch_overlap_static(hipStream_t s, const Level &L, int U, double *tov, double *tovo, double *send,
+                                 bool from_told) {
     const HaloPlan &P = L.halo;
     if (U == 0 || P.d_hface == nullptr) return hipSuccess;
     const int m = 1 << L.isplit;
     HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, send ? send : P.d_send, m};
-    hipLaunchKernelGGL(k_overlap_static, dim3(grid_for((int64_t)U * 3 * m)), dim3(kBlock), 0, s, H, P.d_surf, U);
+    hipLaunchKernelGGL(k_overlap_static, dim3(grid_for((int64_t)U * 3 * m)), dim3(kBlock), 0, s, H, P.d_surf, U,
+                       from_told ? L.TOLD : nullptr, L.pitch, log2i(L.nsub));
     return hipGetLastError();
 }
 
