@@ -468,7 +468,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
     const int ntiles = (h->U + tile - 1) / tile;
     int sched = cs_env >= 0 ? cs_env : h->call_schedule;
     if (sched == 0) sched = h->nranks > 1 ? 2 : 1;
-    if (pipe && n > 1 && sched == 2 && h->p.halo_exchange == 0 && ntiles >= 2) {
+    if (pipe && n > 1 && sched == 2 && h->p.halo_exchange == 0 && ntiles >= 2 && !h->coarse_ahead) {
         const int buf = two ? 1 - P1.send_cur : 0;
         if (h->sent_pending[buf]) {
             HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[buf], 0));
@@ -512,12 +512,21 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
     if (conc) {
         HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));   // everything issued before this call
     }
-    if (pipe && n > 0) {   // its RHS and residual stores are rewritten by the first pipelined launch if n > 1
+    // pamg_run: a step's last launch may have run this call's first coarse cycle already
+    // (into_next below); else its RHS and residual stores are rewritten by the first
+    // pipelined launch if n > 1
+    if (pipe && n > 0 && !h->coarse_ahead) {
         const int ck = (n > 1 || dead_after) ? pipe_keep_env() & PAMG_KEEP_COARSE : PAMG_KEEP_ALL;
         Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h, ck));
         HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
                                        h->tovo, L2.RHSN, 0, -1, ck));
     }
+    h->coarse_ahead = false;
+    // pamg_run, every step but the last: the call's last level-1 launch is a pipelined one too,
+    // carrying the next step's first coarse cycle -- it depends on this call's last residual
+    // (:336) and on the coarse levels' own state only, not on begin_timestep (level 1) -- so
+    // each step saves its separate coarse launch
+    const bool into_next = pipe && dead_after && h->p.halo_exchange == 0;
     for (int c = 0; c < n; ++c) {
         const int buf = two ? 1 - P1.send_cur : 0;
         if (h->sent_pending[buf]) {   // the exchange that read this buffer two cycles ago
@@ -537,15 +546,16 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
             if (conc) HIPCHK(h, hipEventRecord(h->ev_coarse, h->stream_c));
         }
         {
-            const bool pc = pipe && c + 1 < n;   // also the coarse levels of cycle c + 1
+            const bool pc = pipe && (c + 1 < n || into_next);   // also the coarse levels of cycle c + 1
             // its stores that the rest of the call overwrites unread are skipped: level 1's
             // residual and tnew_nonlin always (the call's last launch is k_vc_fine, which stores
             // them), the coarse levels' RHS and residual unless they reach their final cycle
             // here, the halo words unless every cycle's are exchanged
             const bool dead = pipe && dead_after && h->p.halo_exchange == 0;
-            const int keep = pc ? pipe_keep_env() | (c + 2 == n && !dead ? PAMG_KEEP_COARSE : 0) |
-                                      (h->p.halo_exchange == 1 ? PAMG_KEEP_HALO : 0)
-                                : (dead && c + 1 == n ? pipe_keep_env() : PAMG_KEEP_ALL);
+            const int keep = c + 1 == n && into_next ? pipe_keep_env() | (n == 1 ? PAMG_KEEP_COARSE : 0)
+                             : pc ? pipe_keep_env() | (c + 2 == n && !dead ? PAMG_KEEP_COARSE : 0) |
+                                        (h->p.halo_exchange == 1 ? PAMG_KEEP_HALO : 0)
+                                  : (dead && c + 1 == n ? pipe_keep_env() : PAMG_KEEP_ALL);
             Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE,
                     pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h, keep));
             HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
@@ -561,6 +571,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
         if (h->p.halo_exchange == 1 || (c + 1 == n && !(pipe && dead_after))) CHK(halo_async(h, buf));
         else if (c + 1 == n) P1.send_cur = buf;
     }
+    h->coarse_ahead = into_next && n > 0;
     if (conc && n > 0) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));   // join
     return join_comm(h);
 }
@@ -967,8 +978,12 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
         const int L = h->p.multi_levels;
         const bool fused_next = n_multigrid > 0 && h->p.cycle == 0 && h->p.fused && h->p.coarse_solver == 0 &&
                                 vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth);
-        CHK(begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0, fused_next));
-        CHK(vcycle(h, n_multigrid, t + 1 < ntime));   // a step's leftovers die in the next one
+        int rc = begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0, fused_next);
+        if (rc == PAMG_OK) rc = vcycle(h, n_multigrid, t + 1 < ntime);   // a step's leftovers die in the next one
+        if (rc != PAMG_OK) {
+            h->coarse_ahead = false;
+            return rc;
+        }
     }
     return PAMG_OK;
 }

@@ -127,6 +127,9 @@ struct pamg_handle {
     // level 1's compact told copy of the halo is behind TOLD (pamg_run started a step without
     // refreshing it); the fused V-cycle's k_overlap_static writes it from TOLD
     bool told_halo_stale_l1 = false;
+    // pamg_run: the coarse levels already ran the next call's first cycle (its last launch was
+    // pipelined); that call skips its first coarse launch
+    bool coarse_ahead = false;
     // the fused V-cycle's halo exchange (RCCL) runs on stream_comm, overlapped with the next
     // cycle; joined back into `stream` before pamg_vcycle returns
     hipStream_t stream_comm = nullptr;

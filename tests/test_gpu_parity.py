@@ -212,15 +212,22 @@ def test_fused_vcycle_counts_one_launch_per_cycle():
 
 
 def test_pipelined_vcycle_launches():
-    """fused = 3: a call of n cycles is coarse(1), n - 1 pipelined launches, level 1 (n)."""
+    """fused = 3: a call of n cycles is coarse(1), n - 1 pipelined launches, level 1 (n); inside
+    pamg_run a step's last launch is pipelined too, carrying the next step's first coarse
+    cycle, so 2 steps of 3 cycles are coarse, 5 pipelined, level 1."""
     meta, _ = goldens.load("u8_s3_l3_gs")
     s = gpu_solver(meta, fused=3)
     s.timing_enable(0x7FF)
     s.timing_reset()
+    s.vcycle(3)
+    t = s.timing()
+    assert t["vcycle_coarse"]["launches"] == 1 and t["vcycle_pipe"]["launches"] == 2
+    assert t["vcycle"]["launches"] == 1
+    s.timing_reset()
     s.run(2, 3)
     t = s.timing()
-    assert t["vcycle_coarse"]["launches"] == 2 and t["vcycle_pipe"]["launches"] == 4
-    assert t["vcycle"]["launches"] == 2 and t["smooth_L1"]["launches"] == 0
+    assert t["vcycle_coarse"]["launches"] == 1 and t["vcycle_pipe"]["launches"] == 5
+    assert t["vcycle"]["launches"] == 1 and t["smooth_L1"]["launches"] == 0
 
 
 @pytest.mark.parametrize("mesh,S,L,solver,ns", [
