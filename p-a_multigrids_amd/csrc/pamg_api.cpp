@@ -415,6 +415,13 @@ int vcycle_corrected(pamg_handle *h) {
 }
 
 // n V-cycles as two fused launches each (pamg_vcycle.hip)
+// pipelined-call schedule (pamg_set_call_schedule; PAMG_CALL_SCHEDULE=<s> overrides for A/B runs)
+int call_schedule(pamg_handle *h) {
+    static const int cs_env = getenv("PAMG_CALL_SCHEDULE") ? atoi(getenv("PAMG_CALL_SCHEDULE")) : -1;
+    const int s = cs_env >= 0 ? cs_env : h->call_schedule;
+    return s ? s : (h->nranks > 1 ? 2 : 1);
+}
+
 // dead_after (pamg_run, every step but the last): the next call rewrites the fields this one
 // leaves for an observer -- level 1's residual and tnew_nonlin, the coarse levels' RHS and
 // residual, the halo words -- before any read (nothing reads t_overlap, the next step's first
@@ -430,13 +437,21 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
             HIPCHK(h, launch_restrict(h->stream, h->lv[l], h->lv[l + 1], h->U, h->lv[l + 1].RHSN));
         h->rhsn_valid = true;
     }
-    if (!h->overlap_static_l1) {   // once per time step: the halo words the cycle's last smoother
-        CHK(join_comm(h));         // leaves constant (into both send buffers)
+    // once per time step: the halo words the cycle's last smoother leaves constant (into both
+    // send buffers); when this call starts a pamg_run step whose told and RHS its first level-1
+    // launch computes (rhs_pending), after that launch, as it reads told
+    auto overlap_static = [&]() -> int {
+        if (h->overlap_static_l1) return PAMG_OK;
+        CHK(join_comm(h));
         HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, nullptr, h->told_halo_stale_l1));
         h->told_halo_stale_l1 = false;
         if (two) HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, P1.d_send_b));
         h->overlap_static_l1 = true;
-    }
+        return PAMG_OK;
+    };
+    const bool rhs_first = h->rhs_pending;
+    h->rhs_pending = false;
+    if (!rhs_first) CHK(overlap_static());
     // fused = 2: the coarse launch of cycle c (levels 2..L, fp64-issue-bound) runs on stream_c
     // beside the level-1 launch of cycle c (HBM-bound). Their only shared data is level 2's
     // RHSN, read by the coarse launch and written by the level-1 launch: double-buffered,
@@ -463,11 +478,9 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
     // for A/B runs. (A persistent form -- one launch whose workgroups loop over their tile's
     // cycles -- was tried: the loop pushed the launch from 62 to 128 VGPRs with spills, and
     // it is not kept.)
-    static const int cs_env = getenv("PAMG_CALL_SCHEDULE") ? atoi(getenv("PAMG_CALL_SCHEDULE")) : -1;
     const int tile = vcycle_tile_un_eles(h->p.n_split);
     const int ntiles = (h->U + tile - 1) / tile;
-    int sched = cs_env >= 0 ? cs_env : h->call_schedule;
-    if (sched == 0) sched = h->nranks > 1 ? 2 : 1;
+    const int sched = call_schedule(h);
     if (pipe && n > 1 && sched == 2 && h->p.halo_exchange == 0 && ntiles >= 2 && !h->coarse_ahead) {
         const int buf = two ? 1 - P1.send_cur : 0;
         if (h->sent_pending[buf]) {
@@ -556,10 +569,16 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
                              : pc ? pipe_keep_env() | (c + 2 == n && !dead ? PAMG_KEEP_COARSE : 0) |
                                         (h->p.halo_exchange == 1 ? PAMG_KEEP_HALO : 0)
                                   : (dead && c + 1 == n ? pipe_keep_env() : PAMG_KEEP_ALL);
+            // rhs_first: this launch also starts the time step -- told := tnew and level 1's RHS
+            // (k_rhs's work: +48 B stored, 24 B of RHS not read per level-1 sub-element)
+            const bool rhsf = rhs_first && c == 0;
+            if (rhsf && !pc) { h->err = "internal: time-step start on a non-pipelined launch"; return PAMG_ERR_STATE; }
             Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE,
-                    pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h, keep));
+                    (pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h, keep)) + (rhsf ? 24.0 * h->lv[1].N : 0.0));
             HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr, pc, keep));
+                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr, pc, keep, 0, -1,
+                                         rhsf ? h->geo1 : nullptr, h->p.k));
+            if (rhsf) CHK(overlap_static());
             if (conc) HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));
         }
         if (L > 1) L2.RHSN = rhsn_w;   // the next cycle's level-2 RHS
@@ -852,8 +871,15 @@ int pamg_get_overlap(pamg_handle *h, double *tov, double *tovo) {
 // (:327) before any read, so the :317 copy is not stored (pamg_run); told_lazy: that V-cycle
 // is the fused one, whose k_overlap_static refreshes the compact told copy of the halo from
 // TOLD itself (one launch instead of k_told_halo + k_overlap_static)
-int begin_timestep(pamg_handle *h, bool tnn_dead, bool told_lazy = false) {
+int begin_timestep(pamg_handle *h, bool tnn_dead, bool told_lazy = false, bool defer_rhs = false) {
     CHK(check_level(h, 1));
+    if (defer_rhs && h->p.solver != 2) {   // the first launch of the step's fused V-cycle does k_rhs's work
+        h->tnn_level = 1;
+        h->overlap_static_l1 = false;
+        h->told_halo_stale_l1 = true;
+        h->rhs_pending = true;
+        return PAMG_OK;
+    }
     h->tnn_level = 1;
     if (h->p.solver == 2) {   // solve_Richardson never calls get_RHS inside the smoother
         Level &L = h->lv[1];
@@ -978,10 +1004,16 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
         const int L = h->p.multi_levels;
         const bool fused_next = n_multigrid > 0 && h->p.cycle == 0 && h->p.fused && h->p.coarse_solver == 0 &&
                                 vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth);
-        int rc = begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0, fused_next);
+        // told := tnew and the RHS inside the step's first level-1 launch when that launch is a
+        // pipelined one on the one-stream schedule
+        const bool defer_rhs = fused_next && h->p.fused == 3 && L > 1 && h->p.halo_exchange == 0 &&
+                               call_schedule(h) == 1 && (n_multigrid > 1 || t + 1 < ntime) && !PAMG_RHS_TOLD_HALO &&
+                               getenv("PAMG_NO_RHS_FUSION") == nullptr;
+        int rc = begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0, fused_next, defer_rhs);
         if (rc == PAMG_OK) rc = vcycle(h, n_multigrid, t + 1 < ntime);   // a step's leftovers die in the next one
         if (rc != PAMG_OK) {
             h->coarse_ahead = false;
+            h->rhs_pending = false;
             return rc;
         }
     }

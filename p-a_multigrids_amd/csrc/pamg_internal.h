@@ -130,6 +130,9 @@ struct pamg_handle {
     // pamg_run: the coarse levels already ran the next call's first cycle (its last launch was
     // pipelined); that call skips its first coarse launch
     bool coarse_ahead = false;
+    // pamg_run: this step's told := tnew and level-1 RHS are left to the first level-1 launch
+    // of its fused V-cycle (RHSF)
+    bool rhs_pending = false;
     // the fused V-cycle's halo exchange (RCCL) runs on stream_comm, overlapped with the next
     // cycle; joined back into `stream` before pamg_vcycle returns
     hipStream_t stream_comm = nullptr;
@@ -202,7 +205,8 @@ int vcycle_tile_un_eles(int n_split);
 // (PAMG_KEEP_*, pamg_vcycle.hip)
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                              bool pipe = false, int keep = PAMG_KEEP_ALL, int ua = 0, int ub = -1);
+                              bool pipe = false, int keep = PAMG_KEEP_ALL, int ua = 0, int ub = -1,
+                              const double *geo1 = nullptr, double kdiff = 0.0);   // geo1: RHSF (pipe only)
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 // FINDInv (matrix_inversion.F90:50-148) batched, n <= 8, column-major (n, n, nb)

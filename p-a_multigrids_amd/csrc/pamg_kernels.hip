@@ -192,35 +192,6 @@ __global__ __launch_bounds__(kBlock) void k_interp_add(double *T, const double *
         for (int i = 0; i < 3; ++i) T[i * pitch_f + f[q]] = T[i * pitch_f + f[q]] + add[q][i];
 }
 
-// one sub-element s of un_ele u: RHS from its told t (the reference's operation order)
-__device__ __forceinline__ void rhs_one(const double *__restrict__ g, const double *__restrict__ M, int2 ri, double rdt,
-                                        double k, const double t[3], double rhs[3]) {
-    const int irow = ri.x, ipos = ri.y;
-    double xl[3][2];
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-        const double x3 = g[d], v1 = g[2 + d], v2 = g[4 + d];
-        if (ipos % 2 != 0) {
-            xl[2][d] = x3 + (double)(irow - 1) * v2 + (double)(ipos / 2) * v1;
-            xl[1][d] = x3 + (double)irow * v2 + (double)(ipos / 2) * v1;
-            xl[0][d] = x3 + (double)(irow - 1) * v2 + v1 * (double)(ipos / 2 + 1);
-        } else {
-            xl[0][d] = x3 + (double)irow * v2 + v1 * (double)(ipos / 2 - 1);
-            xl[1][d] = x3 + (double)(irow - 1) * v2 + v1 * (double)(ipos / 2);
-            xl[2][d] = x3 + (double)irow * v2 + v1 * (double)(ipos / 2);
-        }
-    }
-    double src[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) src[i] = -(2 * k * sin(xl[i][0] + xl[i][1]));
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        src[i] = M[3 * i] * src[0] + M[3 * i + 1] * src[1] + M[3 * i + 2] * src[2];
-        const double mo = rdt * (M[3 * i] * t[0] + M[3 * i + 1] * t[1] + M[3 * i + 2] * t[2]);
-        rhs[i] = mo + src[i];
-    }
-}
-
 // Level-1 right-hand side + time-step start (:316-317, :593, get_RHS :452-464):
 // told := tnew, tnew_nonlin := tnew, source s_j = -2k sin(x_j + y_j) at the
 // sub-element nodes (get_splitting coordinates), cascaded in place through M,

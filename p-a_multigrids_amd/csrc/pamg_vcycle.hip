@@ -113,6 +113,10 @@ struct VArgs {
     long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
     int keep;               // the dead-until-final stores the launch makes (kKeep*)
     int64_t tile0;          // first tile of the launch (a launch may cover a range of tiles)
+    // RHSF launches (the first of a pamg_run step): told := tnew and level 1's RHS from it
+    const double *geo1;     // U * kGeoStride: X3, v1, v2 of every un_ele (get_splitting)
+    const int2 *subinfo1;   // nsub: (irow, ipos) of level 1's sub-elements
+    double kdiff;           // diffusion coefficient k of the source term
 };
 
 // Stores of a pipelined launch whose values the rest of the call overwrites before any read
@@ -693,7 +697,7 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
 // ===================================================================== level 0
 // Ownership: the adjacent pair 2t, 2t+1 of the tile (16-byte accesses, one un_ele,
 // one operator record); for the prolongator, level-1 sub-element t.
-template <int S, int L, class ST, bool PIPE, bool W8>
+template <int S, int L, class ST, bool PIPE, bool W8, bool RHSF = false>
 __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8 : 4) : 2) void k_vc_fine(VArgs A, const double *__restrict__ sp0,
                                                                       const double *__restrict__ sp1,
                                                                       const double *__restrict__ sp2,
@@ -728,7 +732,21 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     double xc[3], bc[3];   // HOIST: the coarsest level's tnew and RHSN (coarsest_chain)
     if constexpr (HOIST)
         if (coarsest_thread<S, L>(t)) coarsest_load<S, L>(A, t, u0, nue, xc, bc);
-    if constexpr (NP == 2) {
+    if constexpr (RHSF) {
+        // the start of a time step (:316-317, get_RHS :452-464): told := tnew and RHS from it,
+        // as k_rhs computes them (tnew_nonlin := tnew is rewritten by :327 right here)
+        static_assert(NP == 2, "RHSF launches stream pairs");
+        load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
+        const uint32_t sub = s0 & ((1 << G::lg(0)) - 1);
+        const double *g = A.geo1 + (size_t)w0 * kGeoStride;
+        const double *M = sp0 + (size_t)w0 * kStcStride + kStcM;
+        rhs_one(g, M, A.subinfo1[sub], rdt, A.kdiff, x0[0], b0[0]);
+        rhs_one(g, M, A.subinfo1[sub + 1], rdt, A.kdiff, x0[1], b0[1]);
+        if (v0) {
+            store3p(V0.base + 12 * V0.pitch, V0.pitch, s0, x0[0], x0[1]);   // told
+            store3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
+        }
+    } else if constexpr (NP == 2) {
         load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);      // tnew_nonlin := tnew (:327)
         load3p<PAMG_NT_RL>(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);    // RHS of level 1 (get_RHS, constant in the time step)
     } else {
@@ -849,6 +867,12 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
                                A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         else
             return hipErrorInvalidValue;
+    } else if (part == 3) {   // part 2 starting a time step (RHSF)
+        if constexpr (L >= 2 && fine_np(S) == 2)
+            hipLaunchKernelGGL((k_vc_fine<S, L, ST, true, W8, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A,
+                               A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+        else
+            return hipErrorInvalidValue;
     } else {
         hipLaunchKernelGGL((k_vc_fine<S, L, ST, false, W8>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc, nullptr,
                            nullptr, nullptr, nullptr);
@@ -882,9 +906,11 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     // (and only instances that fit 64 VGPRs without scratch: several L >= 4 and n_split = 3
     // instances spill there and stay at their natural register count)
     if constexpr (S >= 3) {
-        static const bool fits[2] = {no_scratch((const void *)k_vc_fine<S, L, ST, false, true>),
-                                     L >= 2 && no_scratch((const void *)k_vc_fine<S, L, ST, (L >= 2), true>)};
-        if (part != 1 && fine_mt(S) == 512 && (long)grid > 3 * n_cu && (long)grid <= w8_max && fits[part == 2])
+        static const bool fits[3] = {no_scratch((const void *)k_vc_fine<S, L, ST, false, true>),
+                                     L >= 2 && no_scratch((const void *)k_vc_fine<S, L, ST, (L >= 2), true>),
+                                     L >= 2 && no_scratch((const void *)k_vc_fine<S, L, ST, (L >= 2), true, true>)};
+        if (part != 1 && fine_mt(S) == 512 && (long)grid > 3 * n_cu && (long)grid <= w8_max &&
+            fits[part == 3 ? 2 : part == 2 ? 1 : 0])
             return launch_sltw<S, L, ST, true>(s, A, grid, part);
     }
     return launch_sltw<S, L, ST, false>(s, A, grid, part);
@@ -910,9 +936,10 @@ hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, int par
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
                        double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part, int keep,
-                       int ua, int ub) {
+                       int ua, int ub, const double *geo1 = nullptr, const int2 *subinfo1 = nullptr,
+                       double kdiff = 0.0) {
     const bool coarse = part == 1;
-    if (part == 2 && L < 2) return hipErrorInvalidValue;
+    if ((part == 2 || part == 3) && L < 2) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
     VArgs A{};
     for (int l = 0; l < L; ++l) {
@@ -937,6 +964,10 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.rdt = rdt;
     A.rhsn2 = rhsn2;
     A.keep = keep;
+    A.geo1 = geo1;
+    A.subinfo1 = subinfo1;
+    A.kdiff = kdiff;
+    if (part == 3 && (!geo1 || !subinfo1)) return hipErrorInvalidValue;
     // tile: 2**fine_tl level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
     const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : fine_tl(n_split) - 2 * n_split;
     // un_eles [ua, ub) (ub < 0: all); ua a multiple of the tile, ub too unless it is U
@@ -996,9 +1027,9 @@ hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, in
 
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                              bool pipe, int keep, int ua, int ub) {
+                              bool pipe, int keep, int ua, int ub, const double *geo1, double kdiff) {
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, L > 1 ? rhsn2 : nullptr,
-                       pipe ? 2 : 0, keep, ua, ub);
+                       pipe ? (geo1 ? 3 : 2) : 0, keep, ua, ub, geo1, lv[1].subinfo, kdiff);
 }
 
 int vcycle_tile_un_eles(int n_split) { return 1 << (fine_tl(n_split) - 2 * n_split);
