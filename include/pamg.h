@@ -217,13 +217,28 @@ int pamg_csr_bench(pamg_handle *h, pamg_csr *m, long n, int reps, double *ms_avg
 int pamg_comm_unique_id(char out[128]);
 /* owner[U] = rank (0-based) owning each un_ele; call before pamg_upload_mesh.
  * nranks == 1 needs no id. The halo (update_overlaps) towards un_eles owned by
- * other ranks is exchanged with grouped ncclSend/ncclRecv after every halo write. */
+ * other ranks is exchanged with grouped ncclSend/ncclRecv after every halo write.
+ * RCCL's asynchronous error state is polled at the end of pamg_vcycle / pamg_run and
+ * while pamg_synchronize and the getters wait: a failed peer returns PAMG_ERR_COMM (the
+ * communicator is aborted) instead of a hang; PAMG_COMM_TIMEOUT_S (seconds), when set, also
+ * bounds how long pamg_synchronize waits for the stream to drain. */
 int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int U, const int *owner);
 int pamg_owned_count(pamg_handle *h);
 /* single-process exchange of the packed halo of `level` between n partition
  * handles (created with pamg_comm_init(id = NULL)): the same send/recv
  * segments RCCL would carry, copied device to device, then unpacked */
 int pamg_halo_loopback(pamg_handle *const *hs, int n, int level);
+/* single-process device-copy transport: binds the n detached partition handles of one owner
+ * map (ranks 0..n-1, pamg_comm_init(id = NULL), meshes uploaded) into a group whose halo
+ * exchange runs the RCCL path itself -- halo_async on the comm stream, the double-buffered send
+ * words, join_comm -- with ncclSend / ncclRecv replaced by device-to-device copies between the
+ * handles. Each handle must then be driven by its own host thread (ranks meet at every
+ * exchange, as grouped send / recv calls do); a rank waiting longer than PAMG_COMM_TIMEOUT_S
+ * (default 120 s) for a peer returns PAMG_ERR_COMM. */
+int pamg_comm_local_group(pamg_handle *const *hs, int n);
+/* RCCL version (ncclGetVersion) and the path of the librccl this library is bound to;
+ * returns 0 (no communicator), 1 (RCCL) or 2 (local group), < 0 on error */
+int pamg_comm_info(pamg_handle *h, int *version, char *lib_path, int len);
 
 /* ---- host-only halo plan (tooling / CPU tests of the partitioned exchange) ---- */
 typedef struct pamg_plan pamg_plan;

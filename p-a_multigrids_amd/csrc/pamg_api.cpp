@@ -1,15 +1,20 @@
 // C-ABI of libpamg: handle, setup, state transfer, the hot-path entry points
 // (one per reference call site) and the V-cycle driver of
 // transport_tri_semi.F90:299-381.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pamg_internal.h"
@@ -17,8 +22,27 @@
 using namespace pamg;
 
 namespace pamg {
+// Single-process device-copy transport (pamg_comm_local_group): n partition handles of one
+// owner map, each driven by its own host thread like one process per rank. The exchange is
+// the RCCL one with ncclSend / ncclRecv replaced by device-to-device copies between the
+// handles: a rank posts its packed send words (pointer + an event recorded after the
+// packing) to every peer, pulls each peer's words for it into its own receive buffer behind
+// that peer's event, and then waits, before it may repack, until every peer has issued its
+// reads of its words (the send completion of ncclSend). Posts carry a per-pair sequence
+// number, so ranks meet exchange by exchange as grouped send/recv calls do.
+struct LocalGroup {
+    struct Post { long seq = 0; const double *ptr = nullptr; hipEvent_t ev = nullptr; };
+    int n = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Post> ready, done;   // [src * n + dst]
+    int refs = 0;
+};
 struct Comm {
     ncclComm_t nccl = nullptr;
+    LocalGroup *local = nullptr;
+    std::vector<long> seq;           // per peer index (level 1's plan): exchanges completed
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
 };
 }  // namespace pamg
 
@@ -144,11 +168,82 @@ double *field_ptr(pamg_handle *h, int l, int what) {
 // The halo words of a smoother call are written by the smoother kernel itself
 // (local neighbours and boundary values into t_overlap, remote neighbours into
 // the packed send buffer); what remains here is the exchange with other ranks.
+// pamg_comm_local_group transport: the grouped send/recv below as device copies between the
+// partition handles of one process (LocalGroup)
+int local_timeout_s() {
+    const char *e = getenv("PAMG_COMM_TIMEOUT_S");
+    const int t = e ? atoi(e) : 120;
+    return t > 0 ? t : 120;
+}
+
+int exchange_local(pamg_handle *h, int l, const double *send, hipStream_t st) {
+    Comm &C = *h->comm;
+    LocalGroup &G = *C.local;
+    const HaloPlan &P = h->lv[l].halo;
+    const int me = h->rank, np = (int)P.peers.size();
+    std::vector<LocalGroup::Post> got(np);
+    auto wait_posts = [&](std::vector<LocalGroup::Post> &box, const char *what) -> int {
+        std::unique_lock<std::mutex> lk(G.mu);
+        for (int q = 0; q < np; ++q) {
+            const int peer = P.peers[q];
+            const long want = C.seq[peer] + 1;
+            LocalGroup::Post &b = box[(size_t)peer * G.n + me];
+            if (!G.cv.wait_for(lk, std::chrono::seconds(local_timeout_s()), [&] { return b.seq >= want; })) {
+                h->err = "local halo exchange: rank " + std::to_string(me) + " timed out waiting for rank " +
+                         std::to_string(peer) + "'s " + what;
+                return PAMG_ERR_COMM;
+            }
+            if (b.seq != want) { h->err = "local halo exchange: sequence mismatch"; return PAMG_ERR_COMM; }
+            got[q] = b;
+        }
+        return PAMG_OK;
+    };
+    // 1. post the packed words, pull the peers' words for this rank behind their events
+    HIPCHK(h, hipEventRecord(C.ev_ready, st));
+    {
+        std::lock_guard<std::mutex> lk(G.mu);
+        for (int q = 0; q < np; ++q) {
+            const int peer = P.peers[q];
+            G.ready[(size_t)me * G.n + peer] = {C.seq[peer] + 1, send + 6 * (size_t)P.send_peer_off[q], C.ev_ready};
+        }
+    }
+    G.cv.notify_all();
+    CHK(wait_posts(G.ready, "send words"));
+    for (int q = 0; q < np; ++q) {
+        const size_t nr = (size_t)(P.recv_peer_off[q + 1] - P.recv_peer_off[q]);
+        HIPCHK(h, hipStreamWaitEvent(st, got[q].ev, 0));
+        if (nr)
+            HIPCHK(h, hipMemcpyAsync(P.d_recv + 6 * (size_t)P.recv_peer_off[q], got[q].ptr, 6 * nr * sizeof(double),
+                                     hipMemcpyDeviceToDevice, st));
+    }
+    // 2. this rank's reads are issued; its send words may be repacked once every peer's are
+    HIPCHK(h, hipEventRecord(C.ev_done, st));
+    {
+        std::lock_guard<std::mutex> lk(G.mu);
+        for (int q = 0; q < np; ++q) {
+            const int peer = P.peers[q];
+            G.done[(size_t)me * G.n + peer] = {C.seq[peer] + 1, nullptr, C.ev_done};
+        }
+    }
+    G.cv.notify_all();
+    CHK(wait_posts(G.done, "receive completion"));
+    for (int q = 0; q < np; ++q) {
+        HIPCHK(h, hipStreamWaitEvent(st, got[q].ev, 0));
+        C.seq[P.peers[q]] += 1;
+    }
+    return PAMG_OK;
+}
+
 int exchange(pamg_handle *h, int l, int buf, hipStream_t st) {
     Level &L = h->lv[l];
     const HaloPlan &P = L.halo;
     const double *send = P.send_buf(buf);
     Span sp(h, PAMG_K_HALO, 2.0 * 48.0 * (double)(P.remote.size() + P.recv_dst.size()), st);
+    if (h->comm->local) {
+        CHK(exchange_local(h, l, send, st));
+        HIPCHK(h, launch_halo_unpack(st, L, h->tov, h->tovo));
+        return PAMG_OK;
+    }
     NCCLCHK(h, ncclGroupStart());
     for (size_t q = 0; q < P.peers.size(); ++q) {
         const int peer = P.peers[q];
@@ -194,6 +289,47 @@ int join_comm(pamg_handle *h) {
             h->sent_pending[b] = false;
         }
     return PAMG_OK;
+}
+
+// RCCL's asynchronous error state (polled at the ends of the hot-path calls): a
+// failed peer or link is reported as PAMG_ERR_COMM instead of a hang in the next exchange
+int comm_error(pamg_handle *h) {
+    if (!h->comm || !h->comm->nccl) return PAMG_OK;
+    ncclResult_t r = ncclSuccess;
+    NCCLCHK(h, ncclCommGetAsyncError(h->comm->nccl, &r));
+    if (r != ncclSuccess && r != ncclInProgress) {
+        h->err = std::string("RCCL asynchronous error: ") + ncclGetErrorString(r);
+        (void)ncclCommAbort(h->comm->nccl);
+        h->comm->nccl = nullptr;
+        return PAMG_ERR_COMM;
+    }
+    return PAMG_OK;
+}
+
+// stream synchronisation that keeps polling RCCL's error state: a rank whose peer failed
+// returns PAMG_ERR_COMM (communicator aborted) instead of waiting on a receive that never
+// completes; PAMG_COMM_TIMEOUT_S, when set, also bounds the wait
+int sync_stream(pamg_handle *h, hipStream_t s) {
+    if (!h->comm || !h->comm->nccl) {
+        HIPCHK(h, hipStreamSynchronize(s));
+        return PAMG_OK;
+    }
+    const char *env = getenv("PAMG_COMM_TIMEOUT_S");
+    const int limit = env ? atoi(env) : 0;   // unset: no limit, only the error polling
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return PAMG_OK;
+        if (e != hipErrorNotReady) HIPCHK(h, e);
+        CHK(comm_error(h));
+        if (limit > 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(limit)) {
+            h->err = "stream did not drain within PAMG_COMM_TIMEOUT_S; RCCL communicator aborted";
+            (void)ncclCommAbort(h->comm->nccl);
+            h->comm->nccl = nullptr;
+            return PAMG_ERR_COMM;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
 }
 
 // `sweeps` sweeps on level l reading the iterate from T (src_is_T: the leg
@@ -688,6 +824,51 @@ int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int
     return PAMG_OK;
 }
 
+int pamg_comm_local_group(pamg_handle *const *hs, int n) {
+    if (!hs || n < 2) return PAMG_ERR_ARG;
+    std::vector<int> seen(n, 0);
+    for (int a = 0; a < n; ++a) {
+        pamg_handle *h = hs[a];
+        if (!h || !h->mesh_ready || h->nranks != n || h->comm || h->rank < 0 || h->rank >= n || seen[h->rank]++)
+            return PAMG_ERR_ARG;
+        if (h->owner != hs[0]->owner) { h->err = "local group: the partitions' owner maps differ"; return PAMG_ERR_ARG; }
+    }
+    auto *G = new LocalGroup;
+    G->n = n;
+    G->ready.resize((size_t)n * n);
+    G->done.resize((size_t)n * n);
+    G->refs = n;
+    for (int a = 0; a < n; ++a) {
+        pamg_handle *h = hs[a];
+        h->comm = new Comm;
+        h->comm->local = G;
+        h->comm->seq.assign(n, 0);
+        if (hipSetDevice(h->device) != hipSuccess ||
+            hipEventCreateWithFlags(&h->comm->ev_ready, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&h->comm->ev_done, hipEventDisableTiming) != hipSuccess) {
+            h->err = "local group: hipEventCreate failed";
+            return PAMG_ERR_HIP;
+        }
+    }
+    return PAMG_OK;
+}
+
+int pamg_comm_info(pamg_handle *h, int *version, char *lib_path, int len) {
+    if (!h) return PAMG_ERR_ARG;
+    if (version) {
+        int v = 0;
+        if (ncclGetVersion(&v) != ncclSuccess) return PAMG_ERR_COMM;
+        *version = v;
+    }
+    if (lib_path && len > 0) {
+        Dl_info di{};
+        const char *p = dladdr((void *)&ncclGetVersion, &di) && di.dli_fname ? di.dli_fname : "";
+        std::strncpy(lib_path, p, (size_t)len - 1);
+        lib_path[len - 1] = 0;
+    }
+    return !h->comm ? 0 : h->comm->local ? 2 : 1;
+}
+
 int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, const int *neig, const int *fneig,
                      const int *dir) {
     if (!h || U < 1 || !X || !region || !neig || !fneig || !dir) return PAMG_ERR_ARG;
@@ -840,7 +1021,7 @@ int pamg_set_state(pamg_handle *h, int level, int what, const double *host) {
     HIPCHK(h, launch_to_soa(h->stream, h->scratch, dst, L.N, L.pitch));
     if (what == PAMG_TOLD) CHK(refresh_told_halo(h, level));
     if (what == PAMG_RESIDUAL) h->rhsn_valid = false;
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    CHK(sync_stream(h, h->stream));
     return PAMG_OK;
 }
 
@@ -854,7 +1035,7 @@ int pamg_get_state(pamg_handle *h, int level, int what, double *host) {
     CHK(ensure_scratch(h, 3 * (size_t)L.N * sizeof(double)));
     HIPCHK(h, launch_to_aos(h->stream, src, h->scratch, L.N, L.pitch));
     HIPCHK(h, hipMemcpyAsync(host, h->scratch, 3 * (size_t)L.N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    CHK(sync_stream(h, h->stream));
     return PAMG_OK;
 }
 
@@ -863,7 +1044,7 @@ int pamg_get_overlap(pamg_handle *h, double *tov, double *tovo) {
     const size_t n = (size_t)h->slots * 3 * h->U * sizeof(double);
     if (tov) HIPCHK(h, hipMemcpyAsync(tov, h->tov, n, hipMemcpyDeviceToHost, h->stream));
     if (tovo) HIPCHK(h, hipMemcpyAsync(tovo, h->tovo, n, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    CHK(sync_stream(h, h->stream));
     return PAMG_OK;
 }
 
@@ -964,7 +1145,8 @@ int vcycle(pamg_handle *h, int n, bool dead_after) {
 
 int pamg_vcycle(pamg_handle *h, int n) {
     if (!h || n < 0) return PAMG_ERR_ARG;
-    return vcycle(h, n, false);
+    CHK(vcycle(h, n, false));
+    return comm_error(h);
 }
 
 int pamg_direct_solve(pamg_handle *h, int level) {
@@ -1017,12 +1199,12 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
             return rc;
         }
     }
-    return PAMG_OK;
+    return comm_error(h);
 }
 
 int pamg_synchronize(pamg_handle *h) {
     if (!h) return PAMG_ERR_ARG;
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    CHK(sync_stream(h, h->stream));
     return PAMG_OK;
 }
 
@@ -1108,12 +1290,24 @@ int pamg_destroy(pamg_handle *h) {
     if (!h) return PAMG_OK;
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
+    (void)hipStreamSynchronize(h->stream_comm);
+    if (h->stream_c) (void)hipStreamSynchronize(h->stream_c);
     free_levels(h);
     dev_free(h->scratch);
     for (auto e : h->timing.pool) (void)hipEventDestroy(e);
     for (auto &r : h->timing.pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     if (h->comm) {
         if (h->comm->nccl) ncclCommDestroy(h->comm->nccl);
+        if (h->comm->ev_ready) (void)hipEventDestroy(h->comm->ev_ready);
+        if (h->comm->ev_done) (void)hipEventDestroy(h->comm->ev_done);
+        if (LocalGroup *G = h->comm->local) {
+            bool last;
+            {
+                std::lock_guard<std::mutex> lk(G->mu);
+                last = --G->refs == 0;
+            }
+            if (last) delete G;
+        }
         delete h->comm;
     }
     (void)hipStreamSynchronize(h->stream_comm);

@@ -95,6 +95,8 @@ def lib():
         "pamg_comm_init": (I, [P, I, I, C.c_char_p, I, ip]),
         "pamg_owned_count": (I, [P]),
         "pamg_halo_loopback": (I, [C.POINTER(P), I, I]),
+        "pamg_comm_local_group": (I, [C.POINTER(P), I]),
+        "pamg_comm_info": (I, [P, C.POINTER(I), C.c_char_p, I]),
         "pamg_plan_build": (I, [I, dp, ip, ip, ip, I, I, I, I, ip, C.POINTER(P)]),
         "pamg_plan_sizes": (I, [P, ip]),
         "pamg_plan_get": (I, [P] + [C.c_void_p] * 10),

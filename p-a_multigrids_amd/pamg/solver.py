@@ -178,6 +178,16 @@ class SemiImplicitIterative:
         self._call("pamg_block_inverse", n, nb, a, inv, err)
         return inv.reshape((n, n, nb), order="F"), err
     def run(self, ntime=2, n_multigrid=2): self._call("pamg_run", ntime, n_multigrid)
+
+    def comm_info(self):
+        """(transport, RCCL version, path of the librccl libpamg is bound to); transport is
+        "none", "rccl" or "local" (pamg_comm_local_group)"""
+        v = C.c_int()
+        buf = C.create_string_buffer(1024)
+        rc = self.L.pamg_comm_info(self.h, C.byref(v), buf, 1024)
+        if rc < 0:
+            _check("pamg_comm_info", rc, self.h)
+        return {0: "none", 1: "rccl", 2: "local"}[rc], v.value, buf.value.decode(errors="replace")
     def synchronize(self): self._call("pamg_synchronize")
 
     # ---- measurement ------------------------------------------------------
@@ -262,6 +272,38 @@ def halo_loopback(solvers, level=1):
     """Exchange the packed halo between partition handles of one process (no RCCL)."""
     arr = (C.c_void_p * len(solvers))(*[s.h for s in solvers])
     _check("pamg_halo_loopback", lib().pamg_halo_loopback(arr, len(solvers), level))
+
+
+def local_group(solvers):
+    """Bind detached partition handles (ranks 0..n-1 of one owner map) into one process's
+    device-copy transport (pamg_comm_local_group): their exchanges then run the RCCL path
+    with device copies in place of ncclSend/ncclRecv. Drive them with run_ranks."""
+    arr = (C.c_void_p * len(solvers))(*[s.h for s in solvers])
+    rc = lib().pamg_comm_local_group(arr, len(solvers))
+    if rc != PAMG_OK:
+        _check("pamg_comm_local_group", rc, solvers[0].h)
+
+
+def run_ranks(solvers, fn):
+    """fn(solver) on every partition, one host thread per rank (the ranks of a local group meet
+    at every halo exchange); re-raises the first error."""
+    import threading
+    errs = [None] * len(solvers)
+
+    def body(i):
+        try:
+            fn(solvers[i])
+        except BaseException as e:  # noqa: BLE001 -- reported to the caller
+            errs[i] = e
+
+    ts = [threading.Thread(target=body, args=(i,)) for i in range(len(solvers))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
 
 
 class HaloPlan:
