@@ -131,8 +131,59 @@ RK_DESC = {"vcycle_pipe": "k_vc_fine<.., true> (pipelined fused V-cycle: level 1
            "smooth_L1": "k_smooth (level-1 smoother call, n_smooth sweeps fused)"}
 
 
+TIME_LOOP_STEPS = 50
+
+
+def measure_time_loop(s):
+    """The time loop as the reference drives it (transport_tri_semi.F90:299-381): pamg_run of
+    TIME_LOOP_STEPS steps, each begin_timestep (told := tnew, level-1 RHS) + n_multigrid = 2
+    V-cycles. Wall time without events; then the same loop with an event pair around every
+    launch for the per-launch algorithmic bytes, the kernel time and the roofline of the
+    launch that starts each step (told, RHS and the step's constant halo words)."""
+    s.timing_enable(0)
+    s.run(10, 2)   # warm-up
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.run(TIME_LOOP_STEPS, 2)
+    s.synchronize()
+    el = time.perf_counter() - t0
+    s.timing_enable(0xF7F)
+    s.timing_stride(1)
+    s.timing_reset()
+    s.run(TIME_LOOP_STEPS, 2)
+    s.synchronize()
+    tm = s.timing()
+    s.timing_enable(0)
+    by = sum(v["bytes"] / v["launches"] * v["issued"] for v in tm.values() if v["launches"]) / TIME_LOOP_STEPS
+    kms = sum(v["ms"] for v in tm.values() if v["launches"]) / TIME_LOOP_STEPS
+    ms_step = 1e3 * el / TIME_LOOP_STEPS
+    out = {"workload": f"pamg_run(ntime={TIME_LOOP_STEPS}, n_multigrid=2): each step begin_timestep + 2 V-cycles "
+                       "(the reference's n_multigrid loop inside its time loop)",
+           "vcycles_per_s": round(2 * TIME_LOOP_STEPS / el, 1), "ms_per_step": round(ms_step, 4),
+           "alg_bytes_per_step": by, "achieved": round(by / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(by / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "kernel_ms_per_step_evented": round(kms, 4),
+           "launches": {k: dict(per_step=round(v["issued"] / TIME_LOOP_STEPS, 2),
+                                ms=round(v["ms"] / v["launches"], 4),
+                                alg_bytes=v["bytes"] / v["launches"],
+                                frac=round(v["bytes"] / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+                        for k, v in tm.items() if v["launches"]}}
+    return out
+
+
+def comm_report(s, world, dist):
+    kind, ver, path = s.comm_info()
+    mine = {"transport": kind, "rccl_version": ver, "librccl": path}
+    if world == 1:
+        return [mine]
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    return allr
+
+
 def main():
     a = parse()
+    time_loop = None
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -147,13 +198,17 @@ def main():
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     mesh = pamg.Mesh.read(a.mesh)
-    comm = None
-    if world > 1 and a.comm == "detached":   # orchestration check on one GPU: no RCCL, no exchange
-        comm = (world, rank, None, mesh.x_strip_owner(world))
-    elif world > 1:
+
+    def comm_for(_mode=None):
+        if world == 1:
+            return None
+        if a.comm == "detached":   # orchestration check on one GPU: no RCCL, no exchange
+            return (world, rank, None, mesh.x_strip_owner(world))
         obj = [pamg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        comm = (world, rank, obj[0], mesh.x_strip_owner(world))
+        return (world, rank, obj[0], mesh.x_strip_owner(world))
+
+    comm = comm_for()
     ndev = max(1, torch.cuda.device_count())
     device = local % ndev
     if torch.cuda.is_available():
@@ -168,7 +223,7 @@ def main():
     # each rank's share of a cycle is ~1/N as long and the events would be a visible part of
     # it, so there they are recorded in a short pass after the timed region
     live_events = world == 1
-    s.timing_enable(0x77F if live_events else 0)  # every class but sweep_bench
+    s.timing_enable(0xF7F if live_events else 0)  # every class but sweep_bench
     # an event pair between back-to-back launches costs ~10 us (~5 % of a cycle): time the
     # first launch of each class and then one in EVENT_STRIDE
     s.timing_stride(EVENT_STRIDE)
@@ -197,7 +252,7 @@ def main():
         # calls as one launch per cycle (the timed region ran the partition's automatic
         # schedule, two tile streams)
         s.set_call_schedule(1)
-        s.timing_enable(0x77F)
+        s.timing_enable(0xF7F)
         s.timing_reset()
         s.vcycle(max(1, min(a.steps, 20)))
         s.synchronize()
@@ -221,19 +276,14 @@ def main():
     tot_bytes = sum(v["bytes"] / v["launches"] * v["issued"] for v in tm.values() if v["launches"])
     extra["cycle_alg_bytes"] = tot_bytes / a.steps
     extra["cycle_alg_gbs"] = round(tot_bytes / elapsed / 1e9, 1)
+    extra["comm"] = comm_report(s, world, dist)
     if rank == 0 and world == 1 and not a.no_extra:
         for asm in (False, True):
             ms, by = s.sweep_bench(20, asm)
             extra["sweep_assembled" if asm else "sweep_stencil"] = dict(
                 ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
                 frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
-        # the time loop as the reference drives it (:299-381): ntime steps of begin_timestep
-        # (told, tnew_nonlin, level-1 RHS) + n_multigrid = 2 V-cycles each
-        s.synchronize()
-        t0 = time.perf_counter()
-        s.run(10, 2)
-        s.synchronize()
-        extra["time_loop_ntime10_nmg2_vcycles_per_s"] = round(20 / (time.perf_counter() - t0), 1)
+        time_loop = measure_time_loop(s)
         # the matrices.F90 SpMV (csr_mul_array, 3 entries per row) over the level-1 operator's
         # size in the reference's block numbering: 3 N1 rows, 52 B per row (3 x (4 B column +
         # 8 B value), 8 B result, 8 B of the gathered vector)
@@ -279,6 +329,26 @@ def main():
         s3.synchronize()
         extra["nsplit3_vcycles_per_s"] = round(max(a.steps, 200) / (time.perf_counter() - t0), 1)
         s3.close()
+    if world > 1 and not a.no_extra:
+        # the other exchange mode on the same partition (timed region the same shape): halo words
+        # exchanged after every cycle, overlapped with the next one
+        mode = 1 - a.halo_exchange
+        sx = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
+                                        halo_mode=a.halo_mode, comm=comm_for(mode), fused=a.fused, arith=a.arith,
+                                        halo_exchange=mode)
+        sx.begin_timestep()
+        sx.vcycle(a.warmup)
+        sx.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        sx.vcycle(a.steps)
+        sx.synchronize()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        extra[f"halo_exchange{mode}_vcycles_per_s"] = round(a.steps / float(t.item()), 2)
+        extra[f"halo_exchange{a.halo_exchange}_vcycles_per_s"] = round(value, 2)
+        sx.close()
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline()
@@ -299,7 +369,9 @@ def main():
             "dtype": "f64",
             "data": "reference mesh untitled8192.msh, deterministic mode-9 IC/source (no random data)",
             "config": {"workload": f"untitled8192.msh n_split={a.nsplit} multi_levels={a.levels} "
-                                   f"n_smooth={a.nsmooth} GS, 1 V-cycle per step",
+                                   f"n_smooth={a.nsmooth} GS; a step = one V-cycle over the whole mesh, the "
+                                   f"{a.steps} timed steps issued as one pamg_vcycle({a.steps}) call inside one time "
+                                   f"step (the reference-shaped loop, 2 V-cycles per time step: time_loop)",
                        "fine_sub_elements": mesh.U * 4 ** a.nsplit, "levels": a.levels,
                        "parallelism": f"dd{world}", "halo_mode": a.halo_mode,
                        "arith": "contracted (fma, 1e-15 of the reference)" if a.arith else "reference order (bitwise)",
@@ -313,6 +385,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "alg_bytes_per_launch": bytes_per_launch, "ms_per_launch": round(ms_per_launch, 4)},
             "cpu_baseline": ({k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")} if cpu else None),
+            "time_loop": time_loop,
             "extra": extra,
         }
         print(json.dumps(line), flush=True)

@@ -58,7 +58,8 @@ extern "C" {
 #define PAMG_K_VCYCLE 8          /* fused V-cycle, level-1 launch */
 #define PAMG_K_VCYCLE_COARSE 9   /* fused V-cycle, levels 2..L launch */
 #define PAMG_K_VCYCLE_PIPE 10    /* pipelined fused V-cycle: level 1 of cycle c + levels 2..L of cycle c+1 */
-#define PAMG_K_COUNT 11
+#define PAMG_K_VCYCLE_RHSF 11    /* the pipelined launch that starts a pamg_run step (told, RHS) */
+#define PAMG_K_COUNT 12
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;

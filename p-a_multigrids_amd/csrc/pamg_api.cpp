@@ -373,7 +373,7 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
 int rhs_level1(pamg_handle *h, int start_of_step) {
     Level &L = h->lv[1];
     Span sp(h, PAMG_K_RHS, (start_of_step == 1 ? 96.0 : start_of_step == 2 ? 72.0 : 48.0) * (double)L.N);
-    HIPCHK(h, launch_rhs(h->stream, L, h->geo1, 1 / h->p.dt, h->p.k, start_of_step, PAMG_RHS_TOLD_HALO && start_of_step != 0));
+    HIPCHK(h, launch_rhs(h->stream, L, 1 / h->p.dt, start_of_step, PAMG_RHS_TOLD_HALO && start_of_step != 0));
     return PAMG_OK;
 }
 
@@ -707,14 +707,25 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
                                   : (dead && c + 1 == n ? pipe_keep_env() : PAMG_KEEP_ALL);
             // rhs_first: this launch also starts the time step -- told := tnew and level 1's RHS
             // (k_rhs's work: +48 B stored, 24 B of RHS not read per level-1 sub-element)
+            // (+24 B of s' read and 24 B of RHS stored per level-1 sub-element, the RHS read
+            // saved; kKeepTold, the step the next one does not overwrite: told stored and the
+            // step's constant halo words written, k_overlap_static's work)
             const bool rhsf = rhs_first && c == 0;
             if (rhsf && !pc) { h->err = "internal: time-step start on a non-pipelined launch"; return PAMG_ERR_STATE; }
-            Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE,
-                    (pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h, keep)) + (rhsf ? 24.0 * h->lv[1].N : 0.0));
+            const int kt = rhsf && !dead_after ? PAMG_KEEP_TOLD : 0;
+            Span sp(h, rhsf ? PAMG_K_VCYCLE_RHSF : pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE,
+                    (pc ? vcycle_pipe_bytes(h, keep) : vcycle_fine_bytes(h, keep)) +
+                        (rhsf ? (kt ? 48.0 : 24.0) * h->lv[1].N : 0.0));
+            if (kt) CHK(join_comm(h));   // the send buffers' told halves are rewritten
             HIPCHK(h, launch_vcycle_fine(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr, pc, keep, 0, -1,
-                                         rhsf ? h->geo1 : nullptr, h->p.k));
-            if (rhsf) CHK(overlap_static());
+                                         h->tovo, P1.send_buf(buf), L > 1 ? rhsn_w : nullptr, pc, keep | kt, 0, -1,
+                                         rhsf, two ? P1.send_buf(1 - buf) : nullptr));
+            if (rhsf) {
+                // kKeepTold: the launch wrote what k_overlap_static would (from told in registers);
+                // else told and those words are dead until the next step rewrites them
+                h->overlap_static_l1 = kt != 0;
+                h->told_halo_stale_l1 = kt == 0;
+            }
             if (conc) HIPCHK(h, hipEventRecord(h->ev_fine, h->stream));
         }
         if (L > 1) L2.RHSN = rhsn_w;   // the next cycle's level-2 RHS
@@ -927,13 +938,15 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         L.N = (int64_t)L.nsub * Ul;
         L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64);
         double *base = nullptr;
-        const size_t planes = (l == 2) ? 21 : 18;   // level 2: RHSN_alt for the concurrent fused cycle
+        // level 1: the source term s' (SRC); level 2: RHSN_alt for the concurrent fused cycle
+        const size_t planes = (l <= 2) ? 21 : 18;
         CHK(dev_alloc(h, &base, planes * (size_t)L.pitch));
         HIPCHK(h, hipMemsetAsync(base, 0, planes * (size_t)L.pitch * sizeof(double), h->stream));
         L.T = base; L.TNN = base + 3 * L.pitch; L.RHS = base + 6 * L.pitch; L.RES = base + 9 * L.pitch;
         L.TOLD = base + 12 * L.pitch;
         L.RHSN = base + 15 * L.pitch;   // restriction of the zero residual: valid
         L.RHSN_alt = (l == 2) ? base + 18 * L.pitch : nullptr;
+        L.SRC = (l == 1) ? base + 18 * L.pitch : nullptr;
         std::vector<double> stc((size_t)std::max(Ul, 1) * kStcStride, 0.0);
         for (int q = 0; q < Ul; ++q) {
             level_stencil(X + 6 * (size_t)h->owned[q], L.isplit, h->p.k, h->p.dt, h->p.omega,
@@ -951,6 +964,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
             sub[e - 1] = make_int2(irow, ipos);
         }
         CHK(dev_upload(h, &L.subinfo, sub));
+        if (l == 1) HIPCHK(h, launch_source(h->stream, L, h->geo1, h->p.k));   // s' of get_RHS, once
         if (l < Lc) {
             std::vector<int4> ch(L.nsub / 4);
             for (int c = 1; c <= L.nsub / 4; ++c) {
@@ -1189,6 +1203,7 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
         // told := tnew and the RHS inside the step's first level-1 launch when that launch is a
         // pipelined one on the one-stream schedule
         const bool defer_rhs = fused_next && h->p.fused == 3 && L > 1 && h->p.halo_exchange == 0 &&
+                               vcycle_rhsf_supported(h->p.n_split) &&
                                call_schedule(h) == 1 && (n_multigrid > 1 || t + 1 < ntime) && !PAMG_RHS_TOLD_HALO &&
                                getenv("PAMG_NO_RHS_FUSION") == nullptr;
         int rc = begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0, fused_next, defer_rhs);

@@ -220,12 +220,12 @@ __device__ __forceinline__ void halo_write(const HaloArgs &H, const HaloPre &P, 
 }
 
 
-// Level-1 RHS of one sub-element from its told t (get_RHS :452-464 with the source term :593:
-// s_j = -2k sin(x_j + y_j) at the get_splitting node coordinates, cascaded through M), the
-// reference's operation order; shared by k_rhs and the pipelined V-cycle launch that starts a
-// time step (pamg_vcycle.hip, RHSF)
-__device__ __forceinline__ void rhs_one(const double *__restrict__ g, const double *__restrict__ M, int2 ri, double rdt,
-                                        double k, const double t[3], double rhs[3]) {
+// The cascaded source term s' of one level-1 sub-element (get_RHS :452-464 with the source
+// term :593): s_j = -2k sin(x_j + y_j) at the get_splitting node coordinates, cascaded in place
+// through M (s'_1 = (M s)_1, s'_2 = M_21 s'_1 + M_22 s_2 + M_23 s_3, ...), the reference's
+// operation order. It depends on the geometry only: k_source forms it once at upload.
+__device__ __forceinline__ void source_one(const double *__restrict__ g, const double *__restrict__ M, int2 ri,
+                                           double k, double src[3]) {
     const int irow = ri.x, ipos = ri.y;
     double xl[3][2];
 #pragma unroll
@@ -241,15 +241,23 @@ __device__ __forceinline__ void rhs_one(const double *__restrict__ g, const doub
             xl[2][d] = x3 + (double)irow * v2 + v1 * (double)(ipos / 2);
         }
     }
-    double src[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) src[i] = -(2 * k * sin(xl[i][0] + xl[i][1]));
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        src[i] = M[3 * i] * src[0] + M[3 * i + 1] * src[1] + M[3 * i + 2] * src[2];
-        const double mo = rdt * (M[3 * i] * t[0] + M[3 * i + 1] * t[1] + M[3 * i + 2] * t[2]);
-        rhs[i] = mo + src[i];
-    }
+    for (int i = 0; i < 3; ++i) src[i] = M[3 * i] * src[0] + M[3 * i + 1] * src[1] + M[3 * i + 2] * src[2];
+}
+
+// Level-1 RHS of one sub-element from its told t and its s' (get_RHS :452-464):
+// RHS_i = rdt (M t)_i + s'_i, the reference's operation order; (M t)_i is evaluated from
+// c = M_12 as in apply_A, bit for bit the reference's (M_i1 t_1 + M_i2 t_2) + M_i3 t_3.
+// Shared by k_rhs and the pipelined V-cycle launch that starts a time step (RHSF).
+__device__ __forceinline__ void rhs_from_source(double c, double rdt, const double t[3], const double src[3],
+                                                double rhs[3]) {
+    const double y0 = c * t[0], y1 = c * t[1], y2 = c * t[2];
+    const double mx[3] = {__builtin_fma(2.0, y0, y1) + y2, __builtin_fma(2.0, y1, y0) + y2,
+                          __builtin_fma(2.0, y2, y0 + y1)};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) rhs[i] = rdt * mx[i] + src[i];
 }
 
 }  // namespace detail

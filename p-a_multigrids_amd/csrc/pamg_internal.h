@@ -80,6 +80,10 @@ struct Level {
     // level 2 only: the second RHSN buffer of the concurrent fused cycle (fused = 2), whose
     // level-1 launch writes the one the concurrent coarse launch is not reading
     double *RHSN_alt = nullptr;
+    // level 1 only: the cascaded source term s' of get_RHS (:452-464, :593), M s with
+    // s_j = -2k sin(x_j + y_j) at the sub-element nodes -- geometry only, formed once at upload
+    // (k_source) and added to rdt M told by every RHS evaluation
+    double *SRC = nullptr;
     double *stc = nullptr;            // U_local * kStcStride
     int2 *subinfo = nullptr;          // nsub: (irow, ipos) of get_str_info
     int4 *children = nullptr;         // nsub/4 (children of the next coarser level's sub-elements)
@@ -178,8 +182,10 @@ hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse
 hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn);
 // start_of_step: 0 RHS from told; 1 told := tnew_nonlin := tnew first; 2 told := tnew first
 // told_halo: with start_of_step, also write the compact told copy of the halo (launch_told_halo)
-hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, int start_of_step,
-                      bool told_halo = false);
+// RHS = rdt M told + s' with s' from L.SRC (launch_source)
+hipError_t launch_rhs(hipStream_t s, const Level &L, double rdt, int start_of_step, bool told_halo = false);
+// s' of level 1 into L.SRC (once, at upload): the source term of get_RHS from the geometry
+hipError_t launch_source(hipStream_t s, const Level &L, const double *geo1, double k);
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
 hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
 hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);
@@ -192,21 +198,29 @@ bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mo
 // levels 2..L; the level-2 RHS is taken from rhsn2 (level 2's RHSN or RHSN_alt)
 // stores a pipelined V-cycle launch may skip (pamg_vcycle.hip, kKeep*)
 constexpr int PAMG_KEEP_L1 = 1, PAMG_KEEP_COARSE = 2, PAMG_KEEP_HALO = 4, PAMG_KEEP_ALL = 7;
+// RHSF launches (the first level-1 launch of a pamg_run step, which starts the step): store
+// told and write the halo words that are constant within the step (k_overlap_static's) --
+// skipped when the next step overwrites them unread
+constexpr int PAMG_KEEP_TOLD = 8;
 // [ua, ub): the un_eles a launch covers (ub < 0: all of them); bounds multiples of
 // vcycle_tile_un_eles (ub may be U)
 hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                 int n_coarse, double rdt, double *tov, double *tovo, const double *rhsn2, int ua = 0,
                                 int ub = -1, int keep = PAMG_KEEP_ALL);
 int vcycle_tile_un_eles(int n_split);
+bool vcycle_rhsf_supported(int n_split);
 // level 1; its remote halo words packed into send1 (one of level 1's two send buffers), the
 // restriction of its residual into rhsn2
 // pipe: the same launch also runs the coarse levels of the next cycle (L >= 2; level 2's RHS
 // from LDS, rhsn2 unused); keep: which of its dead-until-final stores it makes
 // (PAMG_KEEP_*, pamg_vcycle.hip)
+// rhsf (pipe only): the launch also starts the time step (told := tnew, RHS = rdt M told + s');
+// with keep & PAMG_KEEP_TOLD it stores told and writes the step's constant halo words, the told
+// halves of the send entries into both send1 and send_b
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
                               bool pipe = false, int keep = PAMG_KEEP_ALL, int ua = 0, int ub = -1,
-                              const double *geo1 = nullptr, double kdiff = 0.0);   // geo1: RHSF (pipe only)
+                              bool rhsf = false, double *send_b = nullptr);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
 // FINDInv (matrix_inversion.F90:50-148) batched, n <= 8, column-major (n, n, nb)

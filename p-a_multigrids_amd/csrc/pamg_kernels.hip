@@ -193,30 +193,32 @@ __global__ __launch_bounds__(kBlock) void k_interp_add(double *T, const double *
 }
 
 // Level-1 right-hand side + time-step start (:316-317, :593, get_RHS :452-464):
-// told := tnew, tnew_nonlin := tnew, source s_j = -2k sin(x_j + y_j) at the
-// sub-element nodes (get_splitting coordinates), cascaded in place through M,
-// RHS_i = rdt (M told)_i + s'_i. start_of_step 2: the same without the tnew_nonlin store
-// (pamg_run: the V-cycle that follows rewrites it before any read, :327).
+// told := tnew, tnew_nonlin := tnew, RHS_i = rdt (M told)_i + s'_i with the cascaded source
+// term s' precomputed by k_source (the reference recomputes it, with three sines per node, at
+// every visit; it depends on the geometry only). start_of_step 2: the same without the
+// tnew_nonlin store (pamg_run: the V-cycle that follows rewrites it before any read, :327).
 // One adjacent pair of sub-elements per thread (same un_ele: nsub is a power of 4), the
 // state planes streamed with 16-byte non-temporal accesses (ld2 / st2). told_halo (start of a
 // step): also the compact told copy of k_told_halo, from the told values in registers.
 __global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, double *TOLD,
                                                 double *__restrict__ TNN, double *__restrict__ RHS,
-                                                const double *__restrict__ stc, const double *__restrict__ geo,
-                                                const int2 *__restrict__ subinfo, int64_t pitch, int64_t N,
-                                                int nsub_log2, double rdt, double k, int start_of_step,
-                                                const int4 *__restrict__ hsub, const int4 *__restrict__ hface,
-                                                double *__restrict__ told_halo) {
+                                                const double *__restrict__ SRC, const double *__restrict__ stc,
+                                                int64_t pitch, int64_t N, int nsub_log2, double rdt,
+                                                int start_of_step, const int4 *__restrict__ hsub,
+                                                const int4 *__restrict__ hface, double *__restrict__ told_halo) {
     const int64_t s = 2 * ((int64_t)blockIdx.x * kBlock + threadIdx.x);
     if (s >= N) return;
     const int64_t u = s >> nsub_log2;
     const int sub = (int)(s & ((1ll << nsub_log2) - 1));
-    double t0[3], t1[3];
+    double t0[3], t1[3], q0[3], q1[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const double2 v = ld2((start_of_step ? T : TOLD) + c * pitch + s);
+        const double2 w = ld2(SRC + c * pitch + s);
         t0[c] = v.x;
         t1[c] = v.y;
+        q0[c] = w.x;
+        q1[c] = w.y;
         if (start_of_step) {
             st2(TOLD + c * pitch + s, v);
             if (start_of_step == 1) st2(TNN + c * pitch + s, v);
@@ -238,13 +240,26 @@ __global__ __launch_bounds__(kBlock) void k_rhs(const double *__restrict__ T, do
             }
         }
     }
-    const double *g = geo + u * kGeoStride;
-    const double *M = stc + u * kStcStride + kStcM;
+    const double c = stc[u * kStcStride + kStcC];
     double r0[3], r1[3];
-    rhs_one(g, M, subinfo[sub], rdt, k, t0, r0);
-    rhs_one(g, M, subinfo[sub + 1], rdt, k, t1, r1);
+    rhs_from_source(c, rdt, t0, q0, r0);
+    rhs_from_source(c, rdt, t1, q1, r1);
 #pragma unroll
     for (int c = 0; c < 3; ++c) st2(RHS + c * pitch + s, make_double2(r0[c], r1[c]));
+}
+
+// The cascaded source term s' of every level-1 sub-element (source_one), once at upload.
+__global__ __launch_bounds__(kBlock) void k_source(double *__restrict__ SRC, const double *__restrict__ stc,
+                                                   const double *__restrict__ geo, const int2 *__restrict__ subinfo,
+                                                   int64_t pitch, int64_t N, int nsub_log2, double k) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= N) return;
+    const int64_t u = s >> nsub_log2;
+    const int sub = (int)(s & ((1ll << nsub_log2) - 1));
+    double q[3];
+    source_one(geo + u * kGeoStride, stc + u * kStcStride + kStcM, subinfo[sub], k, q);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) SRC[c * pitch + s] = q[c];
 }
 
 // restrictor (splitting.F90:10-32): RHS_{l+1}(:, c) = averages of the fine
@@ -767,13 +782,20 @@ hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse,
     return hipGetLastError();
 }
 
-hipError_t launch_rhs(hipStream_t s, const Level &L, const double *geo1, double rdt, double k, int start_of_step,
-                      bool told_halo) {
+hipError_t launch_rhs(hipStream_t s, const Level &L, double rdt, int start_of_step, bool told_halo) {
     if (L.N == 0) return hipSuccess;
-    if ((L.N & 1) || (L.pitch & 1)) return hipErrorInvalidValue;   // pairs of one un_ele, 16-byte aligned
-    hipLaunchKernelGGL(k_rhs, dim3(grid_for(L.N / 2)), dim3(kBlock), 0, s, L.T, L.TOLD, L.TNN, L.RHS, L.stc, geo1,
-                       L.subinfo, L.pitch, L.N, log2i(L.nsub), rdt, k, start_of_step, L.halo.d_hsub, L.halo.d_hface,
+    if ((L.N & 1) || (L.pitch & 1) || !L.SRC) return hipErrorInvalidValue;   // pairs of one un_ele, 16-byte aligned
+    hipLaunchKernelGGL(k_rhs, dim3(grid_for(L.N / 2)), dim3(kBlock), 0, s, L.T, L.TOLD, L.TNN, L.RHS, L.SRC, L.stc,
+                       L.pitch, L.N, log2i(L.nsub), rdt, start_of_step, L.halo.d_hsub, L.halo.d_hface,
                        (told_halo && start_of_step && L.halo.d_hface && L.halo.d_hsub) ? L.halo.d_told_halo : nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_source(hipStream_t s, const Level &L, const double *geo1, double k) {
+    if (L.N == 0) return hipSuccess;
+    if (!L.SRC) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_source, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.SRC, L.stc, geo1, L.subinfo, L.pitch, L.N,
+                       log2i(L.nsub), k);
     return hipGetLastError();
 }
 

@@ -97,7 +97,9 @@ struct VLevel {
     __device__ __forceinline__ double *TNN() const { return base + 3 * pitch; }
     __device__ __forceinline__ double *RHS() const { return base + 6 * pitch; }
     __device__ __forceinline__ double *RES() const { return base + 9 * pitch; }
+    __device__ __forceinline__ double *TOLD() const { return base + 12 * pitch; }
     __device__ __forceinline__ double *RHSN() const { return base + 15 * pitch; }
+    __device__ __forceinline__ double *SRC() const { return base + 18 * pitch; }   // level 0 only
     const double *stc;
     const int4 *children;   // children (in-un_ele indices) of this level's sub-elements in the next finer level
     int64_t pitch;
@@ -113,10 +115,9 @@ struct VArgs {
     long long *stamps;      // phase timeline (PAMG_VCYCLE_STAMPS diagnostics), null otherwise
     int keep;               // the dead-until-final stores the launch makes (kKeep*)
     int64_t tile0;          // first tile of the launch (a launch may cover a range of tiles)
-    // RHSF launches (the first of a pamg_run step): told := tnew and level 1's RHS from it
-    const double *geo1;     // U * kGeoStride: X3, v1, v2 of every un_ele (get_splitting)
-    const int2 *subinfo1;   // nsub: (irow, ipos) of level 1's sub-elements
-    double kdiff;           // diffusion coefficient k of the source term
+    // RHSF launches (the first of a pamg_run step, told := tnew and level 1's RHS from it) with
+    // kKeepTold: the second send buffer, whose told halves it writes too
+    double *send_b;
 };
 
 // Stores of a pipelined launch whose values the rest of the call overwrites before any read
@@ -129,6 +130,7 @@ struct VArgs {
 // one that leaves the coarse levels at their final cycle, keeps kKeepCoarse. Inside pamg_run
 // every step but the last skips those too (the next step overwrites them unread).
 constexpr int kKeepL1 = PAMG_KEEP_L1, kKeepCoarse = PAMG_KEEP_COARSE, kKeepHalo = PAMG_KEEP_HALO;
+constexpr int kKeepTold = PAMG_KEEP_TOLD;
 
 // phase stamps: 100 MHz wall clock per wave at the phase boundaries, plus the wave's HW_ID
 // (diagnostics build only: make PAMG_STAMPS=1; the pointer costs SGPRs the kernels need)
@@ -255,8 +257,8 @@ __device__ __forceinline__ void residual(const ST &S, double rdt, const double p
 }
 
 // ---- halo words of one sub-element (update_overlaps, :555)
-// h: its positions along faces 1..3 packed 6 bits each (0: not on that face)
-__device__ __forceinline__ int hs_pack(int4 q) { return q.x | (q.y << 6) | (q.z << 12); }
+// h: its positions along faces 1..3 packed 8 bits each (0: not on that face; 2**i_split <= 128)
+__device__ __forceinline__ int hs_pack(int4 q) { return q.x | (q.y << 8) | (q.z << 16); }
 
 // tnew words of the halo (update_overlaps); t_overlap_old and the boundary values are
 // constant within a time step and are written by k_overlap_static (pamg_kernels.hip)
@@ -264,10 +266,35 @@ __device__ __forceinline__ void hs_write(bool uni, const HaloArgs &H, uint32_t u
     if (h == 0) return;
     if (uni) u = __builtin_amdgcn_readfirstlane(u);
     const int4 r1 = H.hface[3 * u], r2 = H.hface[3 * u + 1], r3 = H.hface[3 * u + 2];
-    const int a = h & 63, b = (h >> 6) & 63, c = h >> 12;
+    const int a = h & 255, b = (h >> 8) & 255, c = h >> 16;
     if (a) halo_face<true, false>(H, r1, 1, a, t, t);
     if (b) halo_face<true, false>(H, r2, 2, b, t, t);
     if (c) halo_face<true, false>(H, r3, 3, c, t, t);
+}
+
+// the words of one sub-element that are constant within a time step (k_overlap_static's, from
+// its told `to`): t_overlap_old of the neighbour, the boundary values of both arrays, the told
+// half of a send entry -- into both send buffers -- and the compact told copy of the halo
+__device__ __forceinline__ void hs_write_static(const HaloArgs &H, double *send_b, uint32_t u, int h,
+                                                const double to[3]) {
+    if (h == 0) return;
+    const int pos[3] = {h & 255, (h >> 8) & 255, h >> 16};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        if (!pos[f]) continue;
+        const int4 r = H.hface[3 * u + f];
+        halo_face<false, true>(H, r, f + 1, pos[f], to, to);
+        const int mode = r.x & 3;
+        if (mode == 0) continue;
+        double *o = const_cast<double *>(H.told) + 3 * (int64_t)(r.w + pos[f] - 1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[c] = to[c];
+        if (mode == 2 && send_b) {
+            double *q = send_b + 6 * (int64_t)(r.z + pos[f] - 1);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) q[3 + c] = to[c];
+        }
+    }
 }
 
 // prolongator cascade (splitting.F90:59-88) on the LDS image of the fine tile (component stride n)
@@ -733,17 +760,25 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     if constexpr (HOIST)
         if (coarsest_thread<S, L>(t)) coarsest_load<S, L>(A, t, u0, nue, xc, bc);
     if constexpr (RHSF) {
-        // the start of a time step (:316-317, get_RHS :452-464): told := tnew and RHS from it,
-        // as k_rhs computes them (tnew_nonlin := tnew is rewritten by :327 right here)
+        // the start of a time step (:316-317, get_RHS :452-464): told := tnew and RHS from it
+        // and the precomputed source term s', as k_rhs computes them (tnew_nonlin := tnew is
+        // rewritten by :327 right here). kKeepTold: told stored and the step's constant halo
+        // words written (k_overlap_static's); without it (a pamg_run step the next one
+        // overwrites) both are dead
         static_assert(NP == 2, "RHSF launches stream pairs");
+        double q0[3], q1[3];
         load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
-        const uint32_t sub = s0 & ((1 << G::lg(0)) - 1);
-        const double *g = A.geo1 + (size_t)w0 * kGeoStride;
-        const double *M = sp0 + (size_t)w0 * kStcStride + kStcM;
-        rhs_one(g, M, A.subinfo1[sub], rdt, A.kdiff, x0[0], b0[0]);
-        rhs_one(g, M, A.subinfo1[sub + 1], rdt, A.kdiff, x0[1], b0[1]);
+        load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, s0, q0, q1);
+        const uint32_t wu = G::uni(0) ? (uint32_t)__builtin_amdgcn_readfirstlane(w0) : w0;
+        const double c = sp0[(size_t)wu * kStcStride + kStcC];
+        rhs_from_source(c, rdt, x0[0], q0, b0[0]);
+        rhs_from_source(c, rdt, x0[1], q1, b0[1]);
         if (v0) {
-            store3p(V0.base + 12 * V0.pitch, V0.pitch, s0, x0[0], x0[1]);   // told
+            if (A.keep & kKeepTold) {
+                store3p(V0.TOLD(), V0.pitch, s0, x0[0], x0[1]);
+#pragma unroll
+                for (int k = 0; k < NP; ++k) hs_write_static(V0.H, A.send_b, w0, h0[k], x0[k]);
+            }
             store3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
         }
     } else if constexpr (NP == 2) {
@@ -902,7 +937,7 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     // 120 B per level-1 sub-element and gains from it too: 0.1377 -> 0.1328 ms per full-mesh
     // cycle, scripts/ab_probe.py with PAMG_W8_MAX_GRID)
     static const long w8_env = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : -1;
-    const long w8_max = w8_env >= 0 ? w8_env : ((std::is_same<ST, Stc>::value || part == 2) ? (1l << 40) : 4 * n_cu);
+    const long w8_max = w8_env >= 0 ? w8_env : ((std::is_same<ST, Stc>::value || part >= 2) ? (1l << 40) : 4 * n_cu);
     // (and only instances that fit 64 VGPRs without scratch: several L >= 4 and n_split = 3
     // instances spill there and stay at their natural register count)
     if constexpr (S >= 3) {
@@ -936,8 +971,7 @@ hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, int par
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
                        double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part, int keep,
-                       int ua, int ub, const double *geo1 = nullptr, const int2 *subinfo1 = nullptr,
-                       double kdiff = 0.0) {
+                       int ua, int ub, double *send_b = nullptr) {
     const bool coarse = part == 1;
     if ((part == 2 || part == 3) && L < 2) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
@@ -948,7 +982,8 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
         if ((uint64_t)V.pitch * 3 >= (1ull << 29)) return hipErrorInvalidValue;   // 32-bit byte offsets
         VLevel &o = A.lv[l];
         if (V.TNN != V.T + 3 * V.pitch || V.RHS != V.T + 6 * V.pitch || V.RES != V.T + 9 * V.pitch ||
-            (l != 1 && V.RHSN != V.T + 15 * V.pitch))
+            V.TOLD != V.T + 12 * V.pitch || (l != 1 && V.RHSN != V.T + 15 * V.pitch) ||
+            (l == 0 && part == 3 && V.SRC != V.T + 18 * V.pitch))
             return hipErrorInvalidValue;
         if (l == 1 && rhsn2 != V.T + 15 * V.pitch && (!V.RHSN_alt || rhsn2 != V.RHSN_alt)) return hipErrorInvalidValue;
         o.base = V.T; o.stc = V.stc;
@@ -964,10 +999,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.rdt = rdt;
     A.rhsn2 = rhsn2;
     A.keep = keep;
-    A.geo1 = geo1;
-    A.subinfo1 = subinfo1;
-    A.kdiff = kdiff;
-    if (part == 3 && (!geo1 || !subinfo1)) return hipErrorInvalidValue;
+    A.send_b = send_b;
     // tile: 2**fine_tl level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
     const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : fine_tl(n_split) - 2 * n_split;
     // un_eles [ua, ub) (ub < 0: all); ua a multiple of the tile, ub too unless it is U
@@ -1027,10 +1059,14 @@ hipError_t launch_vcycle_coarse(hipStream_t s, const Level *lv, int L, int U, in
 
 hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                               int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                              bool pipe, int keep, int ua, int ub, const double *geo1, double kdiff) {
+                              bool pipe, int keep, int ua, int ub, bool rhsf, double *send_b) {
+    if (rhsf && !pipe) return hipErrorInvalidValue;
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, L > 1 ? rhsn2 : nullptr,
-                       pipe ? (geo1 ? 3 : 2) : 0, keep, ua, ub, geo1, lv[1].subinfo, kdiff);
+                       pipe ? (rhsf ? 3 : 2) : 0, keep, ua, ub, send_b);
 }
+
+// the RHSF instance streams adjacent pairs (fine_np == 2; A/B builds with PAMG_NP1_MAX_S may not)
+bool vcycle_rhsf_supported(int n_split) { return fine_np(n_split) == 2; }
 
 int vcycle_tile_un_eles(int n_split) { return 1 << (fine_tl(n_split) - 2 * n_split);
 }

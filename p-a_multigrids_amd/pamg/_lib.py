@@ -21,7 +21,7 @@ TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN = 0, 1, 2, 3, 4
 (K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH, K_VCYCLE,
  K_VCYCLE_COARSE) = range(10)
 K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle",
-           "vcycle_coarse", "vcycle_pipe"]
+           "vcycle_coarse", "vcycle_pipe", "vcycle_rhsf"]
 
 
 class PamgParams(C.Structure):

@@ -25,7 +25,7 @@ for S, L, ns in cases:
             s.vcycle(n)
             s.synchronize()
             wall = (time.perf_counter() - t0) / n * 1e3
-            s.timing_enable(0x77F)
+            s.timing_enable(0xF7F)
             s.timing_reset()
             t0 = time.perf_counter()
             s.vcycle(n)

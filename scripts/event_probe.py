@@ -16,7 +16,7 @@ s.begin_timestep()
 s.vcycle(5)
 s.synchronize()
 for rep in range(3):
-    for mask, stride in ((0, 10), (0x77F, 10), (0x77F, 1000000)):
+    for mask, stride in ((0, 10), (0xF7F, 10), (0xF7F, 1000000)):
         s.timing_enable(mask)
         s.timing_stride(stride)
         s.timing_reset()

@@ -23,7 +23,7 @@ for n in (1, 2, 4, 8):
     s.synchronize()
     res = []
     for timed in (0, 1):
-        s.timing_enable(0x77F if timed else 0)
+        s.timing_enable(0xF7F if timed else 0)
         s.timing_reset()
         k = 200
         t0 = time.perf_counter()

@@ -22,7 +22,7 @@ for S, L, ns, nc in cases:
         s.begin_timestep()
         s.vcycle(3)
         s.synchronize()
-        s.timing_enable(0x77F)
+        s.timing_enable(0xF7F)
         s.timing_reset()
         n = 20
         t0 = time.perf_counter()

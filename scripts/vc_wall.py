@@ -16,7 +16,7 @@ s.begin_timestep()
 s.vcycle(5)
 s.synchronize()
 for timed in (0, 1, 0, 1):
-    s.timing_enable(0x77F if timed else 0)
+    s.timing_enable(0xF7F if timed else 0)
     s.timing_reset()
     n = 50
     t0 = time.perf_counter()

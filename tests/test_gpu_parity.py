@@ -202,7 +202,7 @@ def test_timing_counts_launches():
 def test_fused_vcycle_counts_one_launch_per_cycle():
     meta, _ = goldens.load("u8_s3_l3_gs")
     s = gpu_solver(meta, fused=1)
-    s.timing_enable(0x7FF)
+    s.timing_enable(0xF7F)
     s.timing_reset()
     s.run(2, 3)
     t = s.timing()
@@ -217,7 +217,7 @@ def test_pipelined_vcycle_launches():
     cycle, so 2 steps of 3 cycles are coarse, 5 pipelined, level 1."""
     meta, _ = goldens.load("u8_s3_l3_gs")
     s = gpu_solver(meta, fused=3)
-    s.timing_enable(0x7FF)
+    s.timing_enable(0xF7F)
     s.timing_reset()
     s.vcycle(3)
     t = s.timing()
@@ -226,7 +226,9 @@ def test_pipelined_vcycle_launches():
     s.timing_reset()
     s.run(2, 3)
     t = s.timing()
-    assert t["vcycle_coarse"]["launches"] == 1 and t["vcycle_pipe"]["launches"] == 5
+    # each step's first pipelined launch also starts the step (told, RHS: vcycle_rhsf)
+    assert t["vcycle_coarse"]["launches"] == 1 and t["vcycle_rhsf"]["launches"] == 2
+    assert t["vcycle_pipe"]["launches"] == 3 and t["rhs"]["launches"] == 0
     assert t["vcycle"]["launches"] == 1 and t["smooth_L1"]["launches"] == 0
 
 
