@@ -392,7 +392,7 @@ int refresh_told_halo(pamg_handle *h, int l) {
 int restrict_residual(pamg_handle *h, int l) {
     Level &L = h->lv[l];
     h->rhsn_valid = false;
-    if (l >= h->p.multi_levels || L.nsub > 1024) {
+    if (l >= h->p.multi_levels) {
         CHK(restrict_(h, l));
         return residual(h, l);
     }
@@ -745,7 +745,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
 void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
         Level &L = h->lv[l];
-        dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.children); dev_free(L.blocks);
+        dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.d_pos); dev_free(L.blocks);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
         dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
@@ -930,8 +930,16 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         }
         CHK(dev_upload(h, &h->geo1, geo));
     }
+    std::vector<int> pos[kMaxLevels + 1];   // hierarchical storage order of every level (Level::pos)
+    hier_positions(S, Lc, pos);
+    for (int l = 1; l <= Lc; ++l) {
+        std::vector<char> seen(pos[l].size(), 0);
+        for (int v : pos[l])
+            if (v < 0 || v >= (int)pos[l].size() || seen[v]++) { h->err = "storage order is not a permutation"; return PAMG_ERR_STATE; }
+    }
     for (int l = 1; l <= Lc; ++l) {
         Level &L = h->lv[l];
+        L.pos = pos[l];
         L.isplit = S - l + 1;
         L.arith = h->p.arith;
         L.nsub = 1 << (2 * L.isplit);
@@ -961,21 +969,11 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         for (int e = 1; e <= L.nsub; ++e) {
             int irow, ipos, o;
             get_str_info(L.isplit, e, &irow, &ipos, &o);
-            sub[e - 1] = make_int2(irow, ipos);
+            sub[L.pos[e - 1]] = make_int2(irow, ipos);
         }
         CHK(dev_upload(h, &L.subinfo, sub));
+        CHK(dev_upload(h, &L.d_pos, L.pos));
         if (l == 1) HIPCHK(h, launch_source(h->stream, L, h->geo1, h->p.k));   // s' of get_RHS, once
-        if (l < Lc) {
-            std::vector<int4> ch(L.nsub / 4);
-            for (int c = 1; c <= L.nsub / 4; ++c) {
-                int fin[4];
-                element_conversion(fin, c, L.isplit - 1);
-                for (int q = 0; q < 4; ++q)
-                    if (fin[q] < 1 || fin[q] > L.nsub) { h->err = "element_conversion out of range"; return PAMG_ERR_STATE; }
-                ch[c - 1] = make_int4(fin[0] - 1, fin[1] - 1, fin[2] - 1, fin[3] - 1);
-            }
-            CHK(dev_upload(h, &L.children, ch));
-        }
         CHK(build_halo(h, l, X, neig, fneig, dir));
         HaloPlan &P = L.halo;
         CHK(dev_upload(h, &P.d_local, P.local));
@@ -1032,7 +1030,7 @@ int pamg_set_state(pamg_handle *h, int level, int what, const double *host) {
     if (!dst) return PAMG_ERR_ARG;
     CHK(ensure_scratch(h, 3 * (size_t)L.N * sizeof(double)));
     HIPCHK(h, hipMemcpyAsync(h->scratch, host, 3 * (size_t)L.N * sizeof(double), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, launch_to_soa(h->stream, h->scratch, dst, L.N, L.pitch));
+    HIPCHK(h, launch_to_soa(h->stream, L, h->scratch, dst));
     if (what == PAMG_TOLD) CHK(refresh_told_halo(h, level));
     if (what == PAMG_RESIDUAL) h->rhsn_valid = false;
     CHK(sync_stream(h, h->stream));
@@ -1047,7 +1045,7 @@ int pamg_get_state(pamg_handle *h, int level, int what, double *host) {
     double *src = field_ptr(h, level, what);
     if (!src) return PAMG_ERR_ARG;
     CHK(ensure_scratch(h, 3 * (size_t)L.N * sizeof(double)));
-    HIPCHK(h, launch_to_aos(h->stream, src, h->scratch, L.N, L.pitch));
+    HIPCHK(h, launch_to_aos(h->stream, L, src, h->scratch));
     HIPCHK(h, hipMemcpyAsync(host, h->scratch, 3 * (size_t)L.N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     CHK(sync_stream(h, h->stream));
     return PAMG_OK;

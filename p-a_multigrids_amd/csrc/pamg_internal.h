@@ -13,6 +13,7 @@ namespace pamg {
 
 constexpr int kMaxLevels = 12;
 constexpr int kMaxFusedLevels = 5;
+constexpr int kMaxFusedSplit = 7;   // fused V-cycle instances: n_split <= 7 (a tile is a part of an un_ele at >= 6)
 
 // Per (un_ele, level) operator record, fp64, 32 doubles = 256 B (two 128-B lines):
 // M (3x3 row-major) | Kd (3x3 row-major) | w = omega / D (3) | c = M_12 |
@@ -85,8 +86,17 @@ struct Level {
     // (k_source) and added to rdt M told by every RHS evaluation
     double *SRC = nullptr;
     double *stc = nullptr;            // U_local * kStcStride
-    int2 *subinfo = nullptr;          // nsub: (irow, ipos) of get_str_info
-    int4 *children = nullptr;         // nsub/4 (children of the next coarser level's sub-elements)
+    int2 *subinfo = nullptr;          // nsub: (irow, ipos) of get_str_info, by storage position
+    // Storage order of the sub-elements of an un_ele: hierarchical, not the
+    // reference's row-wise numbering -- the four children of the coarser level's sub-element at
+    // position p (element_conversion, splitting.F90:97-140, in its order) sit at positions
+    // 4p .. 4p+3, so over a whole level the children of global coarse index g are the global
+    // fine indices 4g .. 4g+3, and every aligned block of 4**k sub-elements carries its own
+    // coarser sub-elements. The coarsest level keeps the reference's order.
+    // pos[e - 1] = storage position of the reference's str_ele e (host); d_pos on the device
+    // for the (3, nsub, U) boundary layout converters.
+    std::vector<int> pos;
+    int *d_pos = nullptr;
     double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
     int arith = 0;                    // operator arithmetic of this level's kernels (pamg_params.arith)
@@ -165,6 +175,8 @@ void get_str_info(int n_split, int ele, int *irow, int *ipos, int *orientation);
 void element_conversion(int fin[4], int coarse_ele, int i_split);
 void loc_surf_ele(int n, std::vector<int> &surf);
 void get_splitting(const double *un_x, int n_split, int str_ele, double str_x[3][2]);
+// storage positions of every level (see Level::pos): levels 1..L of a split n_split
+void hier_positions(int n_split, int L, std::vector<int> pos[]);
 void level_stencil(const double *X, int i_split, double k, double dt, double omega, double *rec);
 // M == c [[2,1,1],[1,2,1],[1,1,2]] bit for bit (the form the smoother kernels evaluate)
 bool mass_is_p1_midpoint(const double *rec);
@@ -222,14 +234,14 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
                               bool pipe = false, int keep = PAMG_KEEP_ALL, int ua = 0, int ub = -1,
                               bool rhsf = false, double *send_b = nullptr);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
-hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch);
+hipError_t launch_to_soa(hipStream_t s, const Level &L, const double *aos, double *soa);
 // FINDInv (matrix_inversion.F90:50-148) batched, n <= 8, column-major (n, n, nb)
 hipError_t launch_block_inverse(hipStream_t s, int n, int64_t nb, const double *A, double *inv, int *err);
 // A_e = (1/dt) M + Kd per un_ele of level L and its FINDInv inverse (9 fp64 per un_ele)
 hipError_t launch_block_ops(hipStream_t s, const Level &L, int U, double rdt, double *Ainv, int *err);
 // direct local solve of level L: tnew = tnew_nonlin = A_e^-1 RHS
 hipError_t launch_block_solve(hipStream_t s, const Level &L, const double *Ainv);
-hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch);
+hipError_t launch_to_aos(hipStream_t s, const Level &L, const double *soa, double *aos);
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);

@@ -174,18 +174,15 @@ __global__ __launch_bounds__(kBlock) void k_residual(const double *__restrict__ 
 
 // corrected cycle: tnew_l += P tnew_{l+1}, the P1 interpolation the prolongator's cascade
 // (splitting.F90:59-88) encodes, applied to the coarse correction alone; one thread per
-// coarse sub-element (its four children are its own)
-__global__ __launch_bounds__(kBlock) void k_interp_add(double *T, const double *__restrict__ Tc,
-                                                       const int4 *__restrict__ children, int64_t pitch_f,
-                                                       int64_t pitch_c, int64_t Nc, int nsubc_log2) {
+// coarse sub-element (its four children are its own: fine 4c .. 4c+3 in the storage order)
+__global__ __launch_bounds__(kBlock) void k_interp_add(double *T, const double *__restrict__ Tc, int64_t pitch_f,
+                                                       int64_t pitch_c, int64_t Nc) {
     const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (c >= Nc) return;
     const double y0 = Tc[c], y1 = Tc[pitch_c + c], y2 = Tc[2 * pitch_c + c];
     const double m20 = 0.5 * y2 + 0.5 * y0, m12 = 0.5 * y1 + 0.5 * y2, m01 = 0.5 * y0 + 0.5 * y1;
     const double add[4][3] = {{m20, m12, y2}, {m12, m20, m01}, {y0, m01, m20}, {m01, y1, m12}};
-    const int4 ch = children[c & ((1ll << nsubc_log2) - 1)];
-    const int64_t fb = (c >> nsubc_log2) << (nsubc_log2 + 2);
-    const int64_t f[4] = {fb + ch.x, fb + ch.y, fb + ch.z, fb + ch.w};
+    const int64_t f[4] = {4 * c, 4 * c + 1, 4 * c + 2, 4 * c + 3};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -262,74 +259,14 @@ __global__ __launch_bounds__(kBlock) void k_source(double *__restrict__ SRC, con
     for (int c = 0; c < 3; ++c) SRC[c * pitch + s] = q[c];
 }
 
-// restrictor (splitting.F90:10-32): RHS_{l+1}(:, c) = averages of the fine
-// residuals of children 3, 4, 1 (element_conversion, :97-140).
-__global__ __launch_bounds__(kBlock) void k_restrict(const double *__restrict__ RES, double *__restrict__ RHSc,
-                                                     const int4 *__restrict__ children, int64_t pitch_f,
-                                                     int64_t pitch_c, int64_t Nc, int nsubc_log2) {
-    const int64_t cg = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (cg >= Nc) return;
-    const int64_t u = cg >> nsubc_log2;
-    const int c = (int)(cg & ((1ll << nsubc_log2) - 1));
-    const int4 ch = children[c];
-    const int64_t base = u << (nsubc_log2 + 2);
-    const int64_t pick[3] = {base + ch.z, base + ch.w, base + ch.x};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int64_t f = pick[i];
-        RHSc[i * pitch_c + cg] = (RES[f] + RES[pitch_f + f] + RES[2 * pitch_f + f]) / 3.;
-    }
-}
-
-// prolongator (splitting.F90:38-91), fused with the preceding
-// tnew_nonlin := tnew copy of the prolongation leg (:365-367).
-__global__ __launch_bounds__(kBlock) void k_prolong(double *__restrict__ T, double *__restrict__ TNN,
-                                                    const double *__restrict__ Tc, const int4 *__restrict__ children,
-                                                    int64_t pitch_f, int64_t pitch_c, int64_t Nc, int nsubc_log2,
-                                                    int write_tnn) {
-    const int64_t cg = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (cg >= Nc) return;
-    const int64_t u = cg >> nsubc_log2;
-    const int c = (int)(cg & ((1ll << nsubc_log2) - 1));
-    const int4 ch = children[c];
-    const int64_t base = u << (nsubc_log2 + 2);
-    const int64_t fi[4] = {base + ch.x, base + ch.y, base + ch.z, base + ch.w};
-    const double y[3] = {Tc[cg], Tc[pitch_c + cg], Tc[2 * pitch_c + cg]};
-    double f[4][3];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            f[q][i] = T[i * pitch_f + fi[q]];
-            if (write_tnn) TNN[i * pitch_f + fi[q]] = f[q][i];
-        }
-    f[0][0] = f[0][0] + 0.5 * y[2] + 0.5 * y[0];
-    f[0][1] = f[0][1] + 0.5 * y[1] + 0.5 * y[2];
-    f[0][2] = f[0][2] + y[2];
-    f[1][0] = f[1][0] + f[0][1];
-    f[1][1] = f[1][1] + f[0][0];
-    f[1][2] = f[1][2] + 0.5 * y[0] + 0.5 * y[1];
-    f[2][0] = f[2][0] + y[0];
-    f[2][1] = f[2][1] + f[1][2];
-    f[2][2] = f[2][2] + f[1][1];
-    f[3][0] = f[3][0] + f[1][2];
-    f[3][1] = f[3][1] + y[1];
-    f[3][2] = f[3][2] + f[1][0];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < 3; ++i) T[i * pitch_f + fi[q]] = f[q][i];
-}
-
-// LDS-tiled inter-level transfers. A workgroup owns a tile of whole un_eles
-// (TF fine sub-elements, TF >= nsub_f): the fine fields of the tile are
-// streamed into LDS with coalesced double2 loads, the children of each coarse
-// sub-element (element_conversion, splitting.F90:97-140) are then addressed in
-// LDS, and the tile is streamed back. This replaces per-thread gathers of four
-// children spread over two rows of the un_ele.
+// LDS-tiled inter-level transfers. A workgroup owns an aligned tile of TF fine
+// sub-elements, which carries its own TF / 4 coarse sub-elements (the storage order puts the
+// children of coarse g at fine 4g .. 4g+3, pamg_internal.h Level::pos): the fine fields of
+// the tile are streamed into LDS with coalesced double2 loads, the children of each coarse
+// sub-element (element_conversion, splitting.F90:97-140) are addressed in LDS at tile-local
+// 4cc .. 4cc+3, and the tile is streamed back.
 __global__ __launch_bounds__(kBlock) void k_prolong_tile(double *T, double *TNN, const double *__restrict__ Tc,
-                                                         const int4 *__restrict__ children, int64_t pitch_f,
-                                                         int64_t pitch_c, int64_t Nf, int nsubf_log2, int tile_log2,
+                                                         int64_t pitch_f, int64_t pitch_c, int64_t Nf, int tile_log2,
                                                          int write_tnn) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int TF = 1 << tile_log2;
@@ -344,13 +281,9 @@ __global__ __launch_bounds__(kBlock) void k_prolong_tile(double *T, double *TNN,
         }
     }
     __syncthreads();
-    const int nsubc_log2 = nsubf_log2 - 2;
     const int64_t c0 = f0 >> 2;
     for (int cc = threadIdx.x; cc < (nf >> 2); cc += kBlock) {
-        const int c = (int)((c0 + cc) & ((1ll << nsubc_log2) - 1));
-        const int base = (cc >> nsubc_log2) << nsubf_log2;
-        const int4 ch = children[c];
-        const int fi[4] = {base + ch.x, base + ch.y, base + ch.z, base + ch.w};
+        const int fi[4] = {4 * cc, 4 * cc + 1, 4 * cc + 2, 4 * cc + 3};
         const double y[3] = {Tc[c0 + cc], Tc[pitch_c + c0 + cc], Tc[2 * pitch_c + c0 + cc]};
         double f[4][3];
 #pragma unroll
@@ -381,8 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_prolong_tile(double *T, double *TNN,
 }
 
 __global__ __launch_bounds__(kBlock) void k_restrict_tile(const double *__restrict__ RES, double *__restrict__ RHSc,
-                                                          const int4 *__restrict__ children, int64_t pitch_f,
-                                                          int64_t pitch_c, int64_t Nf, int nsubf_log2, int tile_log2) {
+                                                          int64_t pitch_f, int64_t pitch_c, int64_t Nf, int tile_log2) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int TF = 1 << tile_log2;
     const int64_t f0 = (int64_t)blockIdx.x << tile_log2;
@@ -392,21 +324,17 @@ __global__ __launch_bounds__(kBlock) void k_restrict_tile(const double *__restri
         for (int c = 0; c < 3; ++c)
             *reinterpret_cast<double2 *>(&lds[c * TF + j]) = ld2(RES + c * pitch_f + f0 + j);
     __syncthreads();
-    const int nsubc_log2 = nsubf_log2 - 2;
     const int64_t c0 = f0 >> 2;
     for (int cc = threadIdx.x; cc < (nf >> 2); cc += kBlock) {
-        const int c = (int)((c0 + cc) & ((1ll << nsubc_log2) - 1));
-        const int base = (cc >> nsubc_log2) << nsubf_log2;
-        const int4 ch = children[c];
-        const int pick[3] = {base + ch.z, base + ch.w, base + ch.x};   // children 3, 4, 1 (splitting.F90:26-28)
+        const int pick[3] = {4 * cc + 2, 4 * cc + 3, 4 * cc};   // children 3, 4, 1 (splitting.F90:26-28)
 #pragma unroll
         for (int i = 0; i < 3; ++i)
             RHSc[i * pitch_c + c0 + cc] = (lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]) / 3.;
     }
 }
 
-// restrictor(l) followed by get_residual(l) (:336, :338) in one pass over a
-// tile of whole un_eles: the previous cycle's residual is staged in LDS and
+// restrictor(l) followed by get_residual(l) (:336, :338) in one pass over an
+// aligned tile of fine sub-elements: the previous cycle's residual is staged in LDS and
 // restricted into RHS_{l+1}; then the new residual A tnew - RHS overwrites it.
 // ITER = tile / 512: every thread issues all its loads (old residual, tnew,
 // RHS) before the tile barrier, so the three streams are in flight together.
@@ -414,8 +342,7 @@ template <bool UNIFORM, int ITER, class ST = Stc>
 __global__ __launch_bounds__(kBlock) void k_restrict_residual(const double *__restrict__ T,
                                                               const double *__restrict__ RHS, double *RES,
                                                               double *__restrict__ RHSc,
-                                                              const double *__restrict__ stc,
-                                                              const int4 *__restrict__ children, int64_t pitch_f,
+                                                              const double *__restrict__ stc, int64_t pitch_f,
                                                               int64_t pitch_c, int64_t Nf, int nsubf_log2, double rdt) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int TF = ITER * 2 * kBlock;
@@ -443,13 +370,9 @@ __global__ __launch_bounds__(kBlock) void k_restrict_residual(const double *__re
         }
     }
     __syncthreads();
-    const int nsubc_log2 = nsubf_log2 - 2;
     const int64_t c0 = f0 >> 2;
     for (int cc = threadIdx.x; cc < (nf >> 2); cc += kBlock) {
-        const int c = (int)((c0 + cc) & ((1ll << nsubc_log2) - 1));
-        const int base = (cc >> nsubc_log2) << nsubf_log2;
-        const int4 ch = children[c];
-        const int pick[3] = {base + ch.z, base + ch.w, base + ch.x};
+        const int pick[3] = {4 * cc + 2, 4 * cc + 3, 4 * cc};
 #pragma unroll
         for (int i = 0; i < 3; ++i)
             RHSc[i * pitch_c + c0 + cc] = (lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]) / 3.;
@@ -492,20 +415,25 @@ __global__ __launch_bounds__(kBlock) void k_copy(const double *__restrict__ a, d
         st2(b + 2 * i, ld2(a + 2 * i));
 }
 
-// layout converters between the reference's (3, nsub, U) and the planes
+// layout converters between the reference's (3, nsub, U) -- str_ele in its row-wise
+// numbering -- and the planes in the storage order (pos[e]: position of str_ele e + 1)
 __global__ __launch_bounds__(kBlock) void k_to_soa(const double *__restrict__ aos, double *__restrict__ soa,
-                                                   int64_t N, int64_t pitch) {
+                                                   const int *__restrict__ pos, int64_t N, int64_t pitch,
+                                                   int nsub_log2) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= N) return;
+    const int64_t d = ((s >> nsub_log2) << nsub_log2) + pos[s & ((1ll << nsub_log2) - 1)];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) soa[c * pitch + s] = aos[3 * s + c];
+    for (int c = 0; c < 3; ++c) soa[c * pitch + d] = aos[3 * s + c];
 }
 __global__ __launch_bounds__(kBlock) void k_to_aos(const double *__restrict__ soa, double *__restrict__ aos,
-                                                   int64_t N, int64_t pitch) {
+                                                   const int *__restrict__ pos, int64_t N, int64_t pitch,
+                                                   int nsub_log2) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= N) return;
+    const int64_t d = ((s >> nsub_log2) << nsub_log2) + pos[s & ((1ll << nsub_log2) - 1)];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) aos[3 * s + c] = soa[c * pitch + s];
+    for (int c = 0; c < 3; ++c) aos[3 * s + c] = soa[c * pitch + d];
 }
 
 // ---- roofline kernels: one unfused level-1 sweep -------------------------
@@ -726,40 +654,36 @@ hipError_t launch_residual(hipStream_t s, const Level &L, double rdt, bool neg) 
 
 hipError_t launch_interp_add(hipStream_t s, const Level &fine, const Level &coarse) {
     if (coarse.N == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_interp_add, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.T, coarse.T, fine.children,
-                       fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub));
+    hipLaunchKernelGGL(k_interp_add, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.T, coarse.T, fine.pitch,
+                       coarse.pitch, coarse.N);
     return hipGetLastError();
 }
 
-// tile of whole un_eles with at least 1024 fine sub-elements; LDS = 3 * TF * 8 B (<= 96 KiB)
-inline int tile_log2_for(int nsub_f) { const int lg = log2i(nsub_f); return lg > 10 ? lg : 10; }
+// aligned tiles of 1024 fine sub-elements (each carries its own 256 coarse ones, Level::pos);
+// LDS = 3 * 1024 * 8 B = 24 KiB
+constexpr int kTileLog2 = 10;
 
 hipError_t launch_restrict(hipStream_t s, const Level &fine, const Level &coarse, int U, double *out) {
     double *dst = out ? out : coarse.RHS;
     (void)U;
     if (coarse.N == 0) return hipSuccess;
-    if (fine.nsub <= 4096) {
-        const int tl = tile_log2_for(fine.nsub);
-        const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
-        hipLaunchKernelGGL(k_restrict_tile, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.RES, dst,
-                           fine.children, fine.pitch, coarse.pitch, fine.N, log2i(fine.nsub), tl);
-    } else {
-        hipLaunchKernelGGL(k_restrict, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.RES, dst,
-                           fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub));
-    }
+    const int tl = kTileLog2;
+    const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
+    hipLaunchKernelGGL(k_restrict_tile, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.RES, dst, fine.pitch,
+                       coarse.pitch, fine.N, tl);
     return hipGetLastError();
 }
 
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt) {
     if (fine.N == 0) return hipSuccess;
-    // tiles of 1024 fine sub-elements = whole un_eles (nsub <= 1024; the caller splits larger ones)
-    const int tl = 10;
+    // aligned tiles of 1024 fine sub-elements (each with its own coarse sub-elements, Level::pos)
+    const int tl = kTileLog2;
     const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
     const size_t lds = (size_t)3 * 8 << tl;
     const int lg = log2i(fine.nsub);
 #define PAMG_RR(U, IT, ST)                                                                                      \
     hipLaunchKernelGGL((k_restrict_residual<U, IT, ST>), dim3(grid), dim3(kBlock), lds, s, fine.T, fine.RHS,       \
-                       fine.RES, coarse.RHS, fine.stc, fine.children, fine.pitch, coarse.pitch, fine.N, lg, rdt)
+                       fine.RES, coarse.RHS, fine.stc, fine.pitch, coarse.pitch, fine.N, lg, rdt)
     if (fine.arith == 1) { if (fine.nsub >= 128) PAMG_RR(true, 2, StcF); else PAMG_RR(false, 2, StcF); }
     else if (fine.nsub >= 128) PAMG_RR(true, 2, Stc);
     else PAMG_RR(false, 2, Stc);
@@ -769,16 +693,10 @@ hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Leve
 
 hipError_t launch_prolong(hipStream_t s, const Level &fine, const Level &coarse, bool write_tnn) {
     if (coarse.N == 0) return hipSuccess;
-    if (fine.nsub <= 4096) {
-        const int tl = tile_log2_for(fine.nsub);
-        const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
-        hipLaunchKernelGGL(k_prolong_tile, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.T, fine.TNN,
-                           coarse.T, fine.children, fine.pitch, coarse.pitch, fine.N, log2i(fine.nsub), tl,
-                           write_tnn ? 1 : 0);
-    } else {
-        hipLaunchKernelGGL(k_prolong, dim3(grid_for(coarse.N)), dim3(kBlock), 0, s, fine.T, fine.TNN, coarse.T,
-                           fine.children, fine.pitch, coarse.pitch, coarse.N, log2i(coarse.nsub), write_tnn ? 1 : 0);
-    }
+    const int tl = kTileLog2;
+    const unsigned grid = (unsigned)((fine.N + (1ll << tl) - 1) >> tl);
+    hipLaunchKernelGGL(k_prolong_tile, dim3(grid), dim3(kBlock), (size_t)3 * 8 << tl, s, fine.T, fine.TNN, coarse.T,
+                       fine.pitch, coarse.pitch, fine.N, tl, write_tnn ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -865,15 +783,17 @@ hipError_t launch_block_solve(hipStream_t s, const Level &L, const double *Ainv)
     return hipGetLastError();
 }
 
-hipError_t launch_to_soa(hipStream_t s, const double *aos, double *soa, int64_t N, int64_t pitch) {
-    if (N == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_to_soa, dim3(grid_for(N)), dim3(kBlock), 0, s, aos, soa, N, pitch);
+hipError_t launch_to_soa(hipStream_t s, const Level &L, const double *aos, double *soa) {
+    if (L.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_to_soa, dim3(grid_for(L.N)), dim3(kBlock), 0, s, aos, soa, L.d_pos, L.N, L.pitch,
+                       log2i(L.nsub));
     return hipGetLastError();
 }
 
-hipError_t launch_to_aos(hipStream_t s, const double *soa, double *aos, int64_t N, int64_t pitch) {
-    if (N == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_to_aos, dim3(grid_for(N)), dim3(kBlock), 0, s, soa, aos, N, pitch);
+hipError_t launch_to_aos(hipStream_t s, const Level &L, const double *soa, double *aos) {
+    if (L.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_to_aos, dim3(grid_for(L.N)), dim3(kBlock), 0, s, soa, aos, L.d_pos, L.N, L.pitch,
+                       log2i(L.nsub));
     return hipGetLastError();
 }
 

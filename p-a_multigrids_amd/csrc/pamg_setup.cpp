@@ -86,6 +86,24 @@ void get_splitting(const double *un_x, int n_split, int str_ele, double str_x[3]
     }
 }
 
+// Hierarchical storage positions (Level::pos): the coarsest level (i_split = n_split - L + 1)
+// in the reference's order; on every finer level the children fin[0..3] of the coarse
+// sub-element c (element_conversion) at 4 pos(c) + 0..3. pos[l] for l = 1..L, 0-based values.
+void hier_positions(int n_split, int L, std::vector<int> pos[]) {
+    const int ic = n_split - L + 1;
+    pos[L].resize((size_t)1 << (2 * ic));
+    for (size_t e = 0; e < pos[L].size(); ++e) pos[L][e] = (int)e;
+    for (int l = L - 1; l >= 1; --l) {
+        const int is = n_split - l + 1;
+        pos[l].assign((size_t)1 << (2 * is), -1);
+        for (int c = 1; c <= (1 << (2 * (is - 1))); ++c) {
+            int fin[4];
+            element_conversion(fin, c, is - 1);
+            for (int q = 0; q < 4; ++q) pos[l][fin[q] - 1] = 4 * pos[l + 1][c - 1] + q;
+        }
+    }
+}
+
 // Operator record of one (un_ele, level): tri_det_nlx (ShapFun.F90:1389-1454) scaled by
 // semi_tri_det_nlx_multigrid (:1678-1683), get_un_ele_mass_stiff_diffvol
 // (ShapFun_unstruc.F90:304-335), the diff_vol1 reduction (transport_tri_semi.F90:602-606)
@@ -175,10 +193,13 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
     std::vector<int> &surf = P.surf;
     loc_surf_ele(is, surf);
     P.n_told = 0;
+    // storage position of the reference's sub-element se (Level::pos; identity when none is
+    // set: the host-only plan of pamg_plan_build reports the reference's numbering)
+    auto spos = [&](int se) { return L.pos.empty() ? se - 1 : L.pos[se - 1]; };
     P.hsub.assign(L.nsub, make_int4(0, 0, 0, 0));
     for (int f = 1; f <= 3; ++f)
         for (int i = 1; i <= m; ++i) {
-            int4 &e = P.hsub[surf[(i - 1) + (f - 1) * m] - 1];
+            int4 &e = P.hsub[spos(surf[(i - 1) + (f - 1) * m])];
             (f == 1 ? e.x : f == 2 ? e.y : e.z) = i;
         }
     std::vector<std::pair<int, int>> remote_block((size_t)h->U * 3, std::make_pair(-1, -1));   // (peer, first index)
@@ -205,7 +226,7 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
                     return PAMG_ERR_STATE;
                 }
                 const int npos = neig[3 * (size_t)ug + f - 1];
-                const int src = q * L.nsub + se - 1;
+                const int src = q * L.nsub + spos(se);
                 if (npos == 0) {
                     double xl[3][2];
                     get_splitting(X, is, se, xl);
@@ -302,6 +323,8 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
         }
         if (P.recv_peer_off.empty()) P.recv_peer_off.push_back(0);
     }
+    // the device's surf table (k_told_halo, k_overlap_static) holds storage positions, 1-based
+    for (int &v : surf) v = spos(v) + 1;
     return PAMG_OK;
 }
 

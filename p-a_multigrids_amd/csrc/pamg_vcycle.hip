@@ -76,7 +76,14 @@ using namespace detail;
 #ifndef PAMG_CHAIN_PRIO
 #define PAMG_CHAIN_PRIO 3
 #endif
-constexpr int fine_tl(int S) { return 2 * S > PAMG_FINE_TL_MIN ? 2 * S : PAMG_FINE_TL_MIN; }
+// at n_split >= 6 a tile is a part of one un_ele (2**(2 n_split - 10) tiles each): the storage
+// order (pamg_internal.h Level::pos) gives every aligned block of 4**k level-1 sub-elements its
+// own coarser sub-elements, so a tile never needs another's data at any level
+constexpr int kFineTLMax = 10;
+constexpr int fine_tl(int S) {
+    return (2 * S < kFineTLMax ? 2 * S : kFineTLMax) > PAMG_FINE_TL_MIN ? (2 * S < kFineTLMax ? 2 * S : kFineTLMax)
+                                                                        : PAMG_FINE_TL_MIN;
+}
 // level-0 sub-elements per thread: an adjacent pair (16-byte accesses); one at n_split <=
 // PAMG_NP1_MAX_S (A/B builds: twice the waves for the single-round launches of small n_split).
 // Measured (scripts/ab2.sh, parity-tested): equal at n_split = 2 and 3 (those launches stream
@@ -101,7 +108,6 @@ struct VLevel {
     __device__ __forceinline__ double *RHSN() const { return base + 15 * pitch; }
     __device__ __forceinline__ double *SRC() const { return base + 18 * pitch; }   // level 0 only
     const double *stc;
-    const int4 *children;   // children (in-un_ele indices) of this level's sub-elements in the next finer level
     int64_t pitch;
     HaloArgs H;
 };
@@ -153,7 +159,10 @@ __device__ __forceinline__ void stamp_hwid(const VArgs &A) {
 }
 
 // tile geometry (0-based level l): 4**(S-l) sub-elements per un_ele; a tile holds
-// T >> 2l sub-elements of level l (T / 4**S un_eles), T = 2**TL
+// T >> 2l sub-elements of level l (T / 4**S un_eles, or a part of one), T = 2**TL. Tile b
+// covers the global indices b nt(l) .. (b + 1) nt(l) - 1 of every level l (the storage order
+// puts the children of global g at 4g .. 4g+3, Level::pos); an index is valid below
+// N_l = U 4**(S-l) (the last tile of a mesh whose U is not a multiple of its un_eles).
 template <int S, int L>
 struct Geo {
     static constexpr int C = L - 1;                                // coarsest level
@@ -161,12 +170,20 @@ struct Geo {
     static constexpr int T = 1 << TL;                              // level-0 sub-elements per tile
     static constexpr int NP = fine_np(S);                          // level-0 sub-elements per thread
     static constexpr int MT = T / NP;                              // threads of the level-1 launch
-    static constexpr int GL = TL - 2 * S;                          // log2 un_eles per tile
     static constexpr int lg(int l) { return 2 * (S - l); }
     static constexpr int nt(int l) { return T >> (2 * l); }
     // each wave inside one un_ele (a wave spans 64 NP level-0 sub-elements, 64 of any other level)
     static constexpr bool uni(int l) { return lg(l) >= (l == 0 ? (NP == 2 ? 7 : 6) : 6); }
 };
+
+// tile b of level l: global index of its local sub-element i (valid: below N_l = U 4**(S-l);
+// invalid ones are clamped to the tile's first index, so loads stay in bounds)
+template <int S>
+__device__ __forceinline__ uint32_t tile_index(const VArgs &A, int64_t b, int ntl, int l, int i, bool &valid) {
+    const uint32_t g0 = (uint32_t)(b * ntl), n = (uint32_t)(A.U << (2 * (S - l)));
+    valid = i < ntl && g0 + (uint32_t)i < n;
+    return g0 + (uint32_t)(valid ? i : 0);
+}
 
 // field access: wave-uniform plane base (SGPRs) + 32-bit sub-element index (one VGPR for all planes)
 // 8-byte accesses stay plain: non-temporal 8-B lanes measured 15 % slower on the pipelined
@@ -341,11 +358,10 @@ template <int S, int L>
 struct CGeo {
     using G = Geo<S, L>;
     static constexpr int C = G::C;
-    // tile: 2**TL level-1 sub-elements (the reference's finest level) = 2**GL un_eles; one
-    // un_ele at n_split = 5, at least 256 level-1 sub-elements below (enough waves for the
-    // small meshes, whose un_eles then share a wave)
-    static constexpr int TL = 2 * S > 8 ? 2 * S : 8;
-    static constexpr int GL = TL - 2 * S;
+    // tile: 2**TL level-1 sub-elements (the reference's finest level): one un_ele at n_split = 5,
+    // a quarter of one at 6 (and so on), at least 256 level-1 sub-elements below (enough waves for
+    // the small meshes, whose un_eles then share a wave)
+    static constexpr int TL = 2 * S > 8 ? (2 * S < kFineTLMax ? 2 * S : kFineTLMax) : 8;
     static constexpr int nt(int l) { return (1 << TL) >> (2 * l); }
     static constexpr int K(int l) { return nt(l) >= 64 ? nt(l) / 64 : 1; }
     // the lanes of a chunk inside one un_ele (operator record through the scalar cache)
@@ -381,8 +397,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
-    const int64_t u0 = ((int64_t)blockIdx.x + A.tile0) << Q::GL;
-    const int nue = Q::GL == 0 ? 1 : (int)min((int64_t)1 << Q::GL, A.U - u0);   // un_eles in this tile
+    const int64_t tb = (int64_t)blockIdx.x + A.tile0;   // tile
     stamp<kMTc>(A, 0);
     stamp_hwid<kMTc>(A);
     // chunk j = (level l, k): tile index t + 64 k; idle lanes (beyond the level or the
@@ -392,15 +407,14 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         const int l = Q::lev(j), i = t + 64 * Q::kk(j);
-        ok[j] = i < Q::nt(l) && i < (nue << G::lg(l));
-        gx[j] = ((uint32_t)u0 << G::lg(l)) + (uint32_t)(ok[j] ? i : 0);
+        gx[j] = tile_index<S>(A, tb, Q::nt(l), l, i, ok[j]);
     }
     // operator records, fetched once: one per level when the tile's level lies in one un_ele
     // (scalar registers), else one per chunk (vector registers when the chunk spans un_eles)
     ST SL[C + 1], SC[N];
 #pragma unroll
     for (int l = 1; l <= C; ++l)
-        if (Q::one(l)) stencil(Q::uni(l), SP[l], ((uint32_t)u0 << G::lg(l)) >> G::lg(l), SL[l]);
+        if (Q::one(l)) stencil(Q::uni(l), SP[l], (uint32_t)(tb * Q::nt(l)) >> G::lg(l), SL[l]);
 #pragma unroll
     for (int j = 0; j < N; ++j)
         if (!Q::one(Q::lev(j))) stencil(Q::uni(Q::lev(j)), SP[Q::lev(j)], gx[j] >> G::lg(Q::lev(j)), SC[j]);
@@ -460,11 +474,9 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
         for (int j = 0; j < N; ++j) {
             const int l = Q::lev(j);
             if (l < 2 || !ok[j]) continue;
-            const int i = t + 64 * Q::kk(j);
-            const int4 c4 = A.lv[l].children[gx[j] & ((1 << G::lg(l)) - 1)];
-            const int base = (i >> G::lg(l)) << G::lg(l - 1);
-            const double rn[3] = {lds[Q::M(l - 1) + base + c4.z], lds[Q::M(l - 1) + base + c4.w],
-                                  lds[Q::M(l - 1) + base + c4.x]};
+            const int i = t + 64 * Q::kk(j);   // children: 4i .. 4i+3 of level l - 1 (Level::pos)
+            const double rn[3] = {lds[Q::M(l - 1) + 4 * i + 2], lds[Q::M(l - 1) + 4 * i + 3],
+                                  lds[Q::M(l - 1) + 4 * i]};
             store3(A.lv[l].RHSN(), A.lv[l].pitch, gx[j], rn);
         }
     }
@@ -512,9 +524,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
             const int l = Q::lev(j);   // coarse side l, fine side l - 1 >= 1
             if (l < 2 || !ok[j]) continue;
             const int i = t + 64 * Q::kk(j);
-            const int4 c4 = A.lv[l].children[gx[j] & ((1 << G::lg(l)) - 1)];
-            const int base = (i >> G::lg(l)) << G::lg(l - 1);
-            const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+            const int fi[4] = {4 * i, 4 * i + 1, 4 * i + 2, 4 * i + 3};
             const double y[3] = {lds[Q::Y(l) + i], lds[Q::Y(l) + Q::nt(l) + i], lds[Q::Y(l) + 2 * Q::nt(l) + i]};
             prolong_cascade(lds + Q::F(l - 1), Q::nt(l - 1), fi, y);
         }
@@ -576,19 +586,19 @@ __device__ __forceinline__ bool coarsest_thread(int t) {
     return t >= P::T0(L - 1) && t < P::T0(L - 1) + P::NTH(L - 1);
 }
 template <int S, int L>
-__device__ __forceinline__ void coarsest_load(const VArgs &A, int t, int64_t u0, int nue, double x[3], double b[3]) {
+__device__ __forceinline__ void coarsest_load(const VArgs &A, int t, int64_t tb, double x[3], double b[3]) {
     using G = Geo<S, L>;
     using P = PGeo<S, L>;
     constexpr int C = G::C;
     const VLevel &V = A.lv[C];
     const int i = t - P::T0(C);
-    const bool v = i < P::nt(C) && i < (nue << G::lg(C));
-    const uint32_t gx = ((uint32_t)u0 << G::lg(C)) + (uint32_t)(v ? i : 0);
+    bool v;
+    const uint32_t gx = tile_index<S>(A, tb, P::nt(C), C, i, v);
     load3(V.T(), V.pitch, gx, x);
     load3(V.RHSN(), V.pitch, gx, b);
 }
 template <int S, int L, class ST>
-__device__ __forceinline__ void coarsest_chain(const VArgs &A, const double *__restrict__ sp, int t, int64_t u0, int nue,
+__device__ __forceinline__ void coarsest_chain(const VArgs &A, const double *__restrict__ sp, int t, int64_t tb,
                                                double x[3], const double b[3], double *lds) {
     using G = Geo<S, L>;
     using P = PGeo<S, L>;
@@ -597,8 +607,8 @@ __device__ __forceinline__ void coarsest_chain(const VArgs &A, const double *__r
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
     const int i = t - P::T0(C);
-    const bool v = i < P::nt(C) && i < (nue << G::lg(C));
-    const uint32_t gx = ((uint32_t)u0 << G::lg(C)) + (uint32_t)(v ? i : 0);
+    bool v;
+    const uint32_t gx = tile_index<S>(A, tb, P::nt(C), C, i, v);
     const bool keep = A.keep & kKeepCoarse;
     if (v && keep) store3(V.RHS(), V.pitch, gx, b);
     ST St;
@@ -631,7 +641,7 @@ __device__ __forceinline__ void coarsest_chain(const VArgs &A, const double *__r
 }
 
 template <int S, int L, class ST, bool HOIST>
-__device__ __forceinline__ void coarse_next(const VArgs &A, const double *__restrict__ const *SP, int t, int64_t u0, int nue,
+__device__ __forceinline__ void coarse_next(const VArgs &A, const double *__restrict__ const *SP, int t, int64_t tb,
                                             const double y1[3], const double rn1[3], double *lds) {
     using G = Geo<S, L>;
     using P = PGeo<S, L>;
@@ -643,7 +653,6 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
     bool v = false;
     uint32_t gx = 0;
     int i = 0;
-    int4 c4 = make_int4(0, 0, 0, 0);
     __syncthreads();   // the level-1 images are dead
     // ---- phase A
     static_for<1, C + 1>([&](auto lc) {
@@ -651,12 +660,8 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
         if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l)) return;   // wave-uniform
         const VLevel &V = A.lv[l];
         i = t - P::T0(l);
-        v = i < P::nt(l) && i < (nue << G::lg(l));
-        gx = ((uint32_t)u0 << G::lg(l)) + (uint32_t)(v ? i : 0);
-        if constexpr (HOIST && l == C) {   // phase A ran at the start of the launch (coarsest_chain)
-            c4 = V.children[gx & ((1 << G::lg(l)) - 1)];
-            return;
-        }
+        gx = tile_index<S>(A, tb, P::nt(l), l, i, v);
+        if constexpr (HOIST && l == C) return;   // phase A ran at the start of the launch (coarsest_chain)
         if constexpr (l == 1) {
             copy3(x, y1);   // final tnew of the previous cycle (:348 tnew_nonlin := tnew)
             copy3(b, rn1);  // the restriction of level 1's residual (:336)
@@ -667,7 +672,6 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
         const bool keep = A.keep & kKeepCoarse;
         if (v && keep) store3(V.RHS(), V.pitch, gx, b);
         stencil(G::uni(l), SP[l], gx >> G::lg(l), St);
-        if constexpr (l >= 2) c4 = V.children[gx & ((1 << G::lg(l)) - 1)];
         for (int it = 0; it < ns; ++it) {
             copy3(p, x);
             sweep(St, rdt, b, x);
@@ -690,11 +694,12 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
         constexpr int l = decltype(lc)::value;
         if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l)) return;
         const VLevel &V = A.lv[l];
-        const int base = (i >> G::lg(l)) << G::lg(l - 1);
-        if constexpr (l >= 2) {   // restrictor of the next cycle (splitting.F90:10-32, 146-151)
+        // restrictor of the next cycle (splitting.F90:10-32, 146-151); the children of the tile's
+        // sub-element i are 4i .. 4i+3 of level l - 1 (Level::pos)
+        if constexpr (l >= 2) {
             if (v) {
-                const double rn[3] = {lds[P::M(l - 1) + base + c4.z], lds[P::M(l - 1) + base + c4.w],
-                                      lds[P::M(l - 1) + base + c4.x]};
+                const double rn[3] = {lds[P::M(l - 1) + 4 * i + 2], lds[P::M(l - 1) + 4 * i + 3],
+                                      lds[P::M(l - 1) + 4 * i]};
                 store3(V.RHSN(), V.pitch, gx, rn);
             }
         }
@@ -714,7 +719,7 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
             //      coarse sub-element, from its final tnew, on the restriction-leg image of
             //      level l - 1 (complete since the phase-A barrier; each child has one parent)
             if constexpr (l >= 2) {
-                const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+                const int fi[4] = {4 * i, 4 * i + 1, 4 * i + 2, 4 * i + 3};
                 prolong_cascade(lds + P::F(l - 1), P::nt(l - 1), fi, p);
             }
         }
@@ -742,14 +747,13 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth;
-    const int64_t u0 = ((int64_t)blockIdx.x + A.tile0) << G::GL;
-    const int nue = G::GL == 0 ? 1 : (int)min((int64_t)1 << G::GL, A.U - u0);   // un_eles in this tile
+    const int64_t tb = (int64_t)blockIdx.x + A.tile0;   // tile
     stamp<MT>(A, 0);
     stamp_hwid<MT>(A);
     const VLevel &V0 = A.lv[0];
     const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo;
-    const bool v0 = NP * t < (nue << G::lg(0));
-    const uint32_t s0 = ((uint32_t)u0 << G::lg(0)) + (v0 ? NP * t : 0);   // clamped: loads stay in bounds
+    bool v0;
+    const uint32_t s0 = tile_index<S>(A, tb, T, 0, NP * t, v0);          // clamped: loads stay in bounds
     const uint32_t w0 = s0 >> G::lg(0);                                   // un_ele of the thread's sub-elements
     // ---- prologue
     int h0[NP];
@@ -758,7 +762,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     double x0[NP][3], b0[NP][3], p0[NP][3];
     double xc[3], bc[3];   // HOIST: the coarsest level's tnew and RHSN (coarsest_chain)
     if constexpr (HOIST)
-        if (coarsest_thread<S, L>(t)) coarsest_load<S, L>(A, t, u0, nue, xc, bc);
+        if (coarsest_thread<S, L>(t)) coarsest_load<S, L>(A, t, tb, xc, bc);
     if constexpr (RHSF) {
         // the start of a time step (:316-317, get_RHS :452-464): told := tnew and RHS from it
         // and the precomputed source term s', as k_rhs computes them (tnew_nonlin := tnew is
@@ -790,7 +794,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     }
     if constexpr (HOIST)
         if (coarsest_thread<S, L>(t)) coarsest_chain<S, L, ST>(A, G::C == 1 ? sp1 : G::C == 2 ? sp2 : G::C == 3 ? sp3 : sp4,
-                                                               t, u0, nue, xc, bc, F0);
+                                                               t, tb, xc, bc, F0);
     ST St;
     stencil(G::uni(0), sp0, w0, St);
     // ---- restriction leg: smoother (:331), get_residual (:338)
@@ -819,21 +823,18 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
         }
     }
     stamp<MT>(A, 2);
-    // level-1 sub-element t: its final tnew (coarse launch) for the prolongator, its children
-    // for the prolongator and the restrictor, fetched behind the prolongation-leg sweeps
-    // (threads 0..nt(1)-1: prolongator of sub-element t; the others: restrictor of t - nt(1);
-    //  PIPE: both on threads 0..nt(1)-1)
+    // level-1 sub-element j1 of the tile: its final tnew (coarse launch) for the prolongator,
+    // fetched behind the prolongation-leg sweeps; its children are 4 j1 .. 4 j1 + 3 of the tile
+    // (Level::pos) (threads 0..nt(1)-1: prolongator of sub-element t; the others: restrictor of
+    //  t - nt(1); PIPE: both on threads 0..nt(1)-1)
     const int j1 = t & (G::nt(1) - 1);
     const bool casc = t < G::nt(1);
     bool v1 = false;
     uint32_t s1 = 0;
     double y1[3] = {0.0, 0.0, 0.0};
-    int4 c4 = make_int4(0, 0, 0, 0);
     if constexpr (C > 0) {
-        v1 = j1 < (nue << G::lg(1));
-        s1 = ((uint32_t)u0 << G::lg(1)) + (v1 ? j1 : 0);
+        s1 = tile_index<S>(A, tb, G::nt(1), 1, j1, v1);
         if (casc) load3(A.lv[1].T(), A.lv[1].pitch, s1, y1);
-        c4 = A.lv[1].children[s1 & ((1 << G::lg(1)) - 1)];
     }
     // ---- prolongation leg (:367-376) from the restriction-leg tnew; with one level,
     //      the 15 coarse smoother calls (:344-359)
@@ -866,15 +867,14 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     if constexpr (C > 0) {
         __syncthreads();
         if (v1) {
-            const int base = (j1 >> G::lg(1)) << G::lg(0);
             if (casc) {
-                const int fi[4] = {base + c4.x, base + c4.y, base + c4.z, base + c4.w};
+                const int fi[4] = {4 * j1, 4 * j1 + 1, 4 * j1 + 2, 4 * j1 + 3};
                 prolong_cascade(F0, T, fi, y1);
             }
             if (PIPE ? casc : (!casc && t < 2 * G::nt(1))) {
-                rn[0] = M0[base + c4.z];
-                rn[1] = M0[base + c4.w];
-                rn[2] = M0[base + c4.x];
+                rn[0] = M0[4 * j1 + 2];
+                rn[1] = M0[4 * j1 + 3];
+                rn[2] = M0[4 * j1];
                 if constexpr (!PIPE) store3(A.rhsn2, A.lv[1].pitch, s1, rn);
             }
         }
@@ -882,7 +882,7 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     if constexpr (PIPE) {
         const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
         if (PAMG_TAIL_PRIO) __builtin_amdgcn_s_setprio(PAMG_TAIL_PRIO);
-        coarse_next<S, L, ST, HOIST>(A, SP, t, u0, nue, y1, rn, F0);
+        coarse_next<S, L, ST, HOIST>(A, SP, t, tb, y1, rn, F0);
     }
     stamp<MT>(A, 7);
 }
@@ -987,7 +987,6 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
             return hipErrorInvalidValue;
         if (l == 1 && rhsn2 != V.T + 15 * V.pitch && (!V.RHSN_alt || rhsn2 != V.RHSN_alt)) return hipErrorInvalidValue;
         o.base = V.T; o.stc = V.stc;
-        o.children = (l > 0) ? lv[l].children : nullptr;   // children of level l+1 in level l
         o.pitch = V.pitch;
         const HaloPlan &P = V.halo;
         o.H = HaloArgs{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, (l == 0 && send1) ? send1 : P.d_send,
@@ -1000,13 +999,14 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.rhsn2 = rhsn2;
     A.keep = keep;
     A.send_b = send_b;
-    // tile: 2**fine_tl level-1 sub-elements (level-1 launch) or 2**max(2 n_split, 8) (coarse launch)
-    const int GL = coarse ? std::max(2 * n_split, 8) - 2 * n_split : fine_tl(n_split) - 2 * n_split;
-    // un_eles [ua, ub) (ub < 0: all); ua a multiple of the tile, ub too unless it is U
+    // tile: 2**TL level-1 sub-elements, TL = fine_tl (level-1 launch) or CGeo's (coarse launch)
+    const int TL = coarse ? (2 * n_split > 8 ? std::min(2 * n_split, kFineTLMax) : 8) : fine_tl(n_split);
+    // un_eles [ua, ub) (ub < 0: all); ua on a tile boundary, ub too unless it is U
     if (ub < 0 || ub > U) ub = U;
-    if (ua < 0 || (ua & ((1 << GL) - 1)) || (ub != U && (ub & ((1 << GL) - 1)))) return hipErrorInvalidValue;
-    A.tile0 = ua >> GL;
-    const unsigned grid = ub > ua ? (unsigned)(((int64_t)ub - ua + (1 << GL) - 1) >> GL) : 0u;
+    const int64_t fa = (int64_t)ua << (2 * n_split), fb = (int64_t)ub << (2 * n_split), tm = (1ll << TL) - 1;
+    if (ua < 0 || (fa & tm) || (ub != U && (fb & tm))) return hipErrorInvalidValue;
+    A.tile0 = fa >> TL;
+    const unsigned grid = fb > fa ? (unsigned)((fb - fa + tm) >> TL) : 0u;
     if (grid == 0) return hipSuccess;
     // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_VCYCLE_STAMPS") : nullptr;
@@ -1025,6 +1025,8 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
         case 3: e = launch_s<3>(s, A, grid, L, part, lv[1].arith); break;
         case 4: e = launch_s<4>(s, A, grid, L, part, lv[1].arith); break;
         case 5: e = launch_s<5>(s, A, grid, L, part, lv[1].arith); break;
+        case 6: e = launch_s<6>(s, A, grid, L, part, lv[1].arith); break;
+        case 7: e = launch_s<7>(s, A, grid, L, part, lv[1].arith); break;
     }
     if (stamp_path) {
         std::vector<long long> hst(nst);
@@ -1045,7 +1047,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
 
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth) {
     (void)lv;
-    return solver != 2 && halo_mode == 0 && n_smooth > 0 && L >= 1 && L <= kMaxFusedLevels && n_split <= 5 &&
+    return solver != 2 && halo_mode == 0 && n_smooth > 0 && L >= 1 && L <= kMaxFusedLevels && n_split <= kMaxFusedSplit &&
            n_split >= L;
 }
 
@@ -1068,7 +1070,7 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
 // the RHSF instance streams adjacent pairs (fine_np == 2; A/B builds with PAMG_NP1_MAX_S may not)
 bool vcycle_rhsf_supported(int n_split) { return fine_np(n_split) == 2; }
 
-int vcycle_tile_un_eles(int n_split) { return 1 << (fine_tl(n_split) - 2 * n_split);
-}
+// un_eles per level-1 tile (1 when a tile is a part of one un_ele, n_split >= 6)
+int vcycle_tile_un_eles(int n_split) { return fine_tl(n_split) > 2 * n_split ? 1 << (fine_tl(n_split) - 2 * n_split) : 1; }
 
 }  // namespace pamg

@@ -235,7 +235,10 @@ def test_pipelined_vcycle_launches():
 @pytest.mark.parametrize("mesh,S,L,solver,ns", [
     ("untitled8.msh", 1, 1, 3, 1), ("untitled8.msh", 2, 2, 3, 2), ("untitled8.msh", 3, 3, 1, 1),
     ("irregular.msh", 3, 3, 3, 1), ("900_ele.msh", 2, 2, 3, 3), ("900_ele.msh", 4, 4, 1, 1),
-    ("untitled2048.msh", 5, 5, 3, 1), ("untitled8192.msh", 5, 3, 3, 4), ("test_sn2.msh", 4, 2, 3, 2)])
+    ("untitled2048.msh", 5, 5, 3, 1), ("untitled8192.msh", 5, 3, 3, 4), ("test_sn2.msh", 4, 2, 3, 2),
+    # n_split >= 6: a tile is a part of an un_ele (4 tiles at 6, 16 at 7)
+    ("irregular.msh", 6, 3, 3, 4), ("irregular.msh", 7, 4, 1, 2), ("untitled2048.msh", 6, 3, 3, 4),
+    ("900_ele.msh", 6, 5, 3, 1), ("test_sn2.msh", 7, 2, 3, 1)])
 @pytest.mark.parametrize("fused", [1, 2, 3])
 def test_fused_vcycle_equals_kernel_sequence_bitwise(mesh, S, L, solver, ns, fused):
     """The one-launch V-cycle (pamg_vcycle.hip) computes the same operations in
@@ -345,7 +348,8 @@ def test_contracted_time_loop_matches_reference(name):
         check_contracted(st, golden_ref(d), meta["levels"], err_of)
 
 
-@pytest.mark.parametrize("mesh,S,L", [("untitled8192.msh", 5, 3), ("irregular.msh", 6, 3), ("900_ele.msh", 3, 3)])
+@pytest.mark.parametrize("mesh,S,L", [("untitled8192.msh", 5, 3), ("irregular.msh", 6, 3), ("900_ele.msh", 3, 3),
+                                      ("untitled2048.msh", 6, 3), ("irregular.msh", 7, 4)])
 def test_contracted_full_size_against_oracle(mesh, S, L):
     """BASELINE sizes, one time step of two V-cycles, the pipelined fused schedule."""
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
@@ -361,7 +365,9 @@ def test_contracted_full_size_against_oracle(mesh, S, L):
 
 
 @pytest.mark.parametrize("mesh,S,L,ns", [("untitled8.msh", 3, 3, 1), ("irregular.msh", 3, 3, 4),
-                                         ("900_ele.msh", 4, 4, 2), ("untitled2048.msh", 5, 5, 3)])
+                                         ("900_ele.msh", 4, 4, 2), ("untitled2048.msh", 5, 5, 3),
+                                         ("irregular.msh", 6, 3, 4), ("untitled2048.msh", 6, 4, 2),
+                                         ("irregular.msh", 7, 5, 1)])
 @pytest.mark.parametrize("fused", [1, 2, 3])
 def test_contracted_fused_equals_kernel_sequence_bitwise(mesh, S, L, ns, fused):
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
@@ -376,7 +382,8 @@ def test_contracted_fused_equals_kernel_sequence_bitwise(mesh, S, L, ns, fused):
         np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize("mesh,S,L", [("untitled8192.msh", 5, 3), ("irregular.msh", 4, 4), ("900_ele.msh", 3, 2)])
+@pytest.mark.parametrize("mesh,S,L", [("untitled8192.msh", 5, 3), ("irregular.msh", 4, 4), ("900_ele.msh", 3, 2),
+                                      ("irregular.msh", 6, 3)])
 @pytest.mark.parametrize("arith", [0, 1])
 def test_pipelined_call_boundaries_are_invisible(mesh, S, L, arith):
     """fused = 3 pipelines the cycles of one pamg_vcycle call (coarse levels one cycle ahead
@@ -422,7 +429,8 @@ def test_call_schedules_equal_one_sequence(mesh, S, L, n, arith):
 
 
 @pytest.mark.parametrize("mesh,S,L,n", [("untitled8192.msh", 5, 3, 2), ("irregular.msh", 4, 4, 3),
-                                        ("900_ele.msh", 3, 2, 1), ("untitled2048.msh", 5, 5, 2)])
+                                        ("900_ele.msh", 3, 2, 1), ("untitled2048.msh", 5, 5, 2),
+                                        ("irregular.msh", 6, 3, 2), ("irregular.msh", 7, 3, 1)])
 @pytest.mark.parametrize("schedule", [1, 2])
 def test_time_loop_equals_public_steps(mesh, S, L, n, schedule):
     """pamg_run skips what a step leaves that the next step overwrites unread (the step-start
@@ -468,3 +476,26 @@ def test_partitioned_time_loop_matches_single_gpu(S, nparts):
             np.testing.assert_array_equal(v, ref_state[k][:, :, own], err_msg=k)
         for x, y in zip(p.overlap(), ref_ov):
             np.testing.assert_array_equal(x, y[:, :, own])
+
+
+@pytest.mark.parametrize("mesh,S,L", [("untitled8.msh", 3, 3), ("irregular.msh", 6, 4), ("900_ele.msh", 2, 2)])
+def test_state_round_trip_through_the_storage_order(mesh, S, L):
+    """set_state / get_state convert between the reference's (3, nsub, U) row-wise numbering and
+    the hierarchical storage order (Level::pos): every field of every level round-trips exactly,
+    and the fused cycle started from uploaded state equals the per-step kernels' (both read it
+    through the same permutation)."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    rng = np.random.default_rng(20251015)
+    a = pamg.SemiImplicitIterative(m, S, L, fused=3, arith=1)
+    b = pamg.SemiImplicitIterative(m, S, L, fused=0, arith=1)
+    for l in range(1, L + 1):
+        for what in (pamg.TNEW, pamg.TOLD, pamg.RHS, pamg.RESIDUAL):
+            v = rng.uniform(-1, 1, (3, a.nsub(l), a.U))
+            for s in (a, b):
+                s.set(what, l, v)
+                np.testing.assert_array_equal(s.get(what, l), v)
+    for s in (a, b):
+        s.vcycle(3)
+    sa, sb = a.state(), b.state()
+    for k in sb:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
