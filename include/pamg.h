@@ -118,6 +118,16 @@ int pamg_version(void);
 int pamg_msh_read(const char *path, pamg_mesh **m);
 /* structured strip of nx*ny*2 triangles on [0,lx]x[0,ly] (synthetic scaling meshes) */
 int pamg_msh_strip(int nx, int ny, double lx, double ly, pamg_mesh **m);
+/* gmsh 2.2 ASCII of a mesh (nodes deduplicated, coordinates to the last bit): the input format
+ * of ReadMSH, so synthetic meshes feed the reference too */
+int pamg_msh_write(const pamg_mesh *m, const char *path);
+/* binary mesh cache (the reference re-runs its O(N^2) CheckNeig on every start,
+ * grofiling.txt:6-8): X, region, Neig, fNeig, Dir with a checksum; pamg_msh_read_cached parses
+ * msh_path only when cache_path is missing or was made from other file contents (FNV-1a of the
+ * .msh bytes), then writes the cache; *hit = 1 when the cache was used */
+int pamg_msh_save(const pamg_mesh *m, const char *path);
+int pamg_msh_load(const char *path, pamg_mesh **m);
+int pamg_msh_read_cached(const char *msh_path, const char *cache_path, pamg_mesh **m, int *hit);
 int pamg_msh_size(const pamg_mesh *m, int *U);
 /* X(2,3,U) fp64, region(U), Neig/fNeig/Dir(3,U) */
 int pamg_msh_get(const pamg_mesh *m, double *X, int *region, int *neig, int *fneig, int *dir);

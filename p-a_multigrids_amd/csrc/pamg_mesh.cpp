@@ -262,6 +262,136 @@ int pamg_msh_strip(int nx, int ny, double lx, double ly, pamg_mesh **out) {
     return PAMG_OK;
 }
 
+// gmsh 2.2 ASCII of a mesh: one node per distinct vertex (exact coordinates, %.17g: the file
+// reads back bit for bit), one 3-node triangle (type 2, tags region region) per un_ele with
+// its vertices in the mesh's order -- the input ReadMSH (Msh2Tri.F90:132-334) takes, so
+// synthetic meshes can be fed to the reference as well
+int pamg_msh_write(const pamg_mesh *m, const char *path) {
+    if (!m || !path) return PAMG_ERR_ARG;
+    std::unordered_map<std::pair<uint64_t, uint64_t>, int, PairHash> vmap;
+    vmap.reserve(3 * (size_t)m->U);
+    std::vector<int> vid(3 * (size_t)m->U);
+    std::vector<int> first;   // first (element, vertex) of every node
+    for (int e = 0; e < m->U; ++e)
+        for (int a = 0; a < 3; ++a) {
+            auto key = std::make_pair(dbits(m->X[6 * e + 2 * a]), dbits(m->X[6 * e + 2 * a + 1]));
+            auto it = vmap.emplace(key, (int)vmap.size());
+            if (it.second) first.push_back(3 * e + a);
+            vid[3 * e + a] = it.first->second;
+        }
+    FILE *f = std::fopen(path, "w");
+    if (!f) return PAMG_ERR_IO;
+    std::fprintf(f, "$MeshFormat\n2.2 0 8\n$EndMeshFormat\n$Nodes\n%zu\n", first.size());
+    for (size_t n = 0; n < first.size(); ++n)
+        std::fprintf(f, "%zu %.17g %.17g 0\n", n + 1, m->X[2 * first[n]], m->X[2 * first[n] + 1]);
+    std::fprintf(f, "$EndNodes\n$Elements\n%d\n", m->U);
+    for (int e = 0; e < m->U; ++e)
+        std::fprintf(f, "%d 2 2 %d %d %d %d %d\n", e + 1, m->region[e], m->region[e], vid[3 * e] + 1, vid[3 * e + 1] + 1,
+                     vid[3 * e + 2] + 1);
+    std::fprintf(f, "$EndElements\n");
+    return std::fclose(f) == 0 ? PAMG_OK : PAMG_ERR_IO;
+}
+
+namespace {
+// binary mesh cache: magic, version, U, FNV-1a 64 of the source file, payload, FNV-1a 64 of it
+constexpr char kCacheMagic[8] = {'P', 'A', 'M', 'G', 'M', 'S', 'H', '1'};
+
+uint64_t fnv1a(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char *c = static_cast<const unsigned char *>(p);
+    for (size_t i = 0; i < n; ++i) { h ^= c[i]; h *= 1099511628211ull; }
+    return h;
+}
+
+int file_hash(const char *path, uint64_t *h) {
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return PAMG_ERR_IO;
+    std::vector<char> buf(1 << 20);
+    uint64_t v = 1469598103934665603ull;
+    size_t n;
+    while ((n = std::fread(buf.data(), 1, buf.size(), f)) > 0) v = fnv1a(buf.data(), n, v);
+    std::fclose(f);
+    *h = v;
+    return PAMG_OK;
+}
+
+uint64_t payload_hash(const pamg_mesh &m) {
+    uint64_t h = fnv1a(m.X.data(), m.X.size() * sizeof(double));
+    for (const auto *v : {&m.region, &m.neig, &m.fneig, &m.dir}) h = fnv1a(v->data(), v->size() * sizeof(int), h);
+    return h;
+}
+
+int cache_save(const pamg_mesh &m, const char *path, uint64_t src) {
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE *f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return PAMG_ERR_IO;
+    const int32_t ver = 1, U = m.U;
+    const uint64_t ph = payload_hash(m);
+    bool ok = std::fwrite(kCacheMagic, 8, 1, f) == 1 && std::fwrite(&ver, 4, 1, f) == 1 && std::fwrite(&U, 4, 1, f) == 1 &&
+              std::fwrite(&src, 8, 1, f) == 1 && std::fwrite(m.X.data(), sizeof(double), m.X.size(), f) == m.X.size();
+    for (const auto *v : {&m.region, &m.neig, &m.fneig, &m.dir})
+        ok = ok && std::fwrite(v->data(), sizeof(int), v->size(), f) == v->size();
+    ok = ok && std::fwrite(&ph, 8, 1, f) == 1;
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path) != 0) { std::remove(tmp.c_str()); return PAMG_ERR_IO; }
+    return PAMG_OK;
+}
+
+// loads a cache whose source hash equals `src` (src == 0: any); PAMG_ERR_STATE when stale or damaged
+int cache_load(const char *path, uint64_t src, pamg_mesh **out) {
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return PAMG_ERR_IO;
+    char magic[8];
+    int32_t ver = 0, U = 0;
+    uint64_t s = 0, ph = 0;
+    if (std::fread(magic, 8, 1, f) != 1 || std::memcmp(magic, kCacheMagic, 8) || std::fread(&ver, 4, 1, f) != 1 ||
+        ver != 1 || std::fread(&U, 4, 1, f) != 1 || U < 1 || std::fread(&s, 8, 1, f) != 1 || (src && s != src)) {
+        std::fclose(f);
+        return PAMG_ERR_STATE;
+    }
+    auto *m = new pamg_mesh;
+    m->U = U;
+    m->X.resize(6 * (size_t)U);
+    m->region.resize(U);
+    m->neig.resize(3 * (size_t)U);
+    m->fneig.resize(3 * (size_t)U);
+    m->dir.resize(3 * (size_t)U);
+    bool ok = std::fread(m->X.data(), sizeof(double), m->X.size(), f) == m->X.size();
+    for (auto *v : {&m->region, &m->neig, &m->fneig, &m->dir}) ok = ok && std::fread(v->data(), sizeof(int), v->size(), f) == v->size();
+    ok = ok && std::fread(&ph, 8, 1, f) == 1 && ph == payload_hash(*m);
+    std::fclose(f);
+    if (!ok) { delete m; return PAMG_ERR_STATE; }
+    *out = m;
+    return PAMG_OK;
+}
+}  // namespace
+
+int pamg_msh_save(const pamg_mesh *m, const char *path) {
+    if (!m || !path) return PAMG_ERR_ARG;
+    return cache_save(*m, path, 0);
+}
+
+int pamg_msh_load(const char *path, pamg_mesh **m) {
+    if (!path || !m) return PAMG_ERR_ARG;
+    return cache_load(path, 0, m);
+}
+
+int pamg_msh_read_cached(const char *msh_path, const char *cache_path, pamg_mesh **m, int *hit) {
+    if (!msh_path || !cache_path || !m) return PAMG_ERR_ARG;
+    if (hit) *hit = 0;
+    uint64_t h = 0;
+    int rc = file_hash(msh_path, &h);
+    if (rc != PAMG_OK) return rc;
+    if (h == 0) h = 1;   // 0 means "any source" in the cache header
+    if (cache_load(cache_path, h, m) == PAMG_OK) {
+        if (hit) *hit = 1;
+        return PAMG_OK;
+    }
+    rc = pamg_msh_read(msh_path, m);
+    if (rc != PAMG_OK) return rc;
+    (void)cache_save(**m, cache_path, h);   // a cache that cannot be written is not an error
+    return PAMG_OK;
+}
+
 int pamg_msh_size(const pamg_mesh *m, int *U) {
     if (!m || !U) return PAMG_ERR_ARG;
     *U = m->U;

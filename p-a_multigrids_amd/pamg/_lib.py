@@ -56,6 +56,10 @@ def lib():
         "pamg_default_params": (None, [C.POINTER(PamgParams)]),
         "pamg_msh_read": (I, [C.c_char_p, C.POINTER(P)]),
         "pamg_msh_strip": (I, [I, I, D, D, C.POINTER(P)]),
+        "pamg_msh_write": (I, [P, C.c_char_p]),
+        "pamg_msh_save": (I, [P, C.c_char_p]),
+        "pamg_msh_load": (I, [C.c_char_p, C.POINTER(P)]),
+        "pamg_msh_read_cached": (I, [C.c_char_p, C.c_char_p, C.POINTER(P), C.POINTER(I)]),
         "pamg_msh_size": (I, [P, C.POINTER(I)]),
         "pamg_msh_get": (I, [P, dp, ip, ip, ip, ip]),
         "pamg_msh_free": (None, [P]),

@@ -52,6 +52,29 @@ class Mesh:
         _check("pamg_msh_strip", lib().pamg_msh_strip(nx, ny, lx, ly, C.byref(p)))
         return cls(p)
 
+    @classmethod
+    def load(cls, path):
+        """binary mesh cache written by save() (pamg_msh_load)"""
+        p = C.c_void_p()
+        _check("pamg_msh_load", lib().pamg_msh_load(os.fsencode(path), C.byref(p)))
+        return cls(p)
+
+    @classmethod
+    def read_cached(cls, msh_path, cache_path):
+        """ReadMSH with a binary cache: (mesh, hit) -- the .msh is parsed only when the cache is
+        missing or was made from other file contents (pamg_msh_read_cached)"""
+        p, hit = C.c_void_p(), C.c_int()
+        _check("pamg_msh_read_cached", lib().pamg_msh_read_cached(os.fsencode(msh_path), os.fsencode(cache_path),
+                                                                  C.byref(p), C.byref(hit)))
+        return cls(p), bool(hit.value)
+
+    def save(self, path):
+        _check("pamg_msh_save", lib().pamg_msh_save(self._ptr, os.fsencode(path)))
+
+    def write_msh(self, path):
+        """gmsh 2.2 ASCII (pamg_msh_write), readable by the reference's ReadMSH"""
+        _check("pamg_msh_write", lib().pamg_msh_write(self._ptr, os.fsencode(path)))
+
     def __del__(self):
         if getattr(self, "_ptr", None):
             lib().pamg_msh_free(self._ptr)
