@@ -80,35 +80,74 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline():
-    """Reference CPU path on this host: the reference Fortran itself (fp64
-    build, oracle/_ref, 1 core, its own `cpu_time for time_loop` window) on a
-    bounded sample -- 1 V-cycle of untitled8192 at n_split = 3, which is 1/16 of
-    the n_split = 5 work on every level -- scaled to the benchmarked config."""
+def host_cpu():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def run_reference(mesh_path, nsplit, ntime, nmg, timeout=900):
+    """The reference's own fp64 build (oracle/_ref/pamg_ref_fp64, 1 core) on a mesh: the seconds
+    of its `cpu_time for time_loop` window (transport_tri_semi.F90:297-387), or None."""
     exe = os.path.join(ROOT, "oracle", "_ref", "pamg_ref_fp64")
-    kind = "reference"
     if not os.path.exists(exe):
         return None
     tmp = tempfile.mkdtemp(prefix="pamg_cpu_")
     try:
-        shutil.copy(MESH, tmp)
+        shutil.copy(mesh_path, os.path.join(tmp, "mesh.msh"))
         with open(os.path.join(tmp, "pamg_ref.nml"), "w") as f:
-            f.write("&pamg_ref\n pamg_mesh='untitled8192.msh', pamg_dump_prefix='', pamg_nsplit=3, pamg_ntime=1,\n"
-                    " pamg_nmultigrid=1, pamg_solver=3, pamg_levels=3, pamg_nsmooth=4, pamg_vtk=100000\n/\n")
+            f.write(f"&pamg_ref\n pamg_mesh='mesh.msh', pamg_dump_prefix='', pamg_nsplit={nsplit}, "
+                    f"pamg_ntime={ntime},\n pamg_nmultigrid={nmg}, pamg_solver=3, pamg_levels=3, pamg_nsmooth=4, "
+                    f"pamg_vtk=100000\n/\n")
         env = dict(os.environ, OMP_NUM_THREADS="1")
         r = subprocess.run(["taskset", "-c", "0", exe] if shutil.which("taskset") else [exe], cwd=tmp,
-                           capture_output=True, text=True, timeout=900, env=env)
+                           capture_output=True, text=True, timeout=timeout, env=env)
         m = re.search(r"cpu_time for time_loop =\s*([0-9.Ee+-]+)", r.stdout)
         if r.returncode != 0 or not m:
             return None
-        t = float(m.group(1))
+        return float(m.group(1))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    return dict(value=1.0 / (16.0 * t), unit="V-cycles/s", cores=1, kind=kind,
-                sample=f"reference fp64 build (flang -O2), 1 V-cycle of untitled8192 at n_split=3, multi_levels=3 "
-                       f"took {t:.2f} s in its time_loop window on 1 core; n_split=5 has 16x the sub-elements on "
-                       f"every level, value = 1/(16*{t:.2f} s)",
-                nsplit3_vcycles_per_s=1.0 / t)
+
+
+CPU_STRIP = (32, 8)   # 512 un_eles: 1/16 of untitled8192's, the same 4**5 sub-elements each
+
+
+def cpu_baseline():
+    """Reference CPU path on this host, measured at the benchmarked n_split = 5 and L = 3: the
+    reference Fortran itself (fp64 build, oracle/_ref, 1 core, its own `cpu_time for time_loop`
+    window) on a bounded sample -- one time step of 1 and of 2 V-cycles on a 512-element
+    synthetic strip; the difference is the steady-state cost of one V-cycle (the first cycle of
+    a run carries a one-off cost the second does not). The reference's work is per un_ele
+    (stencils re-derived per un_ele visit, then its 4**n_split sub-elements; nothing couples
+    un_eles in mode 9), so untitled8192's 8192 un_eles take 16x as long; the 16x is checked
+    against the full-size run by scripts/cpu_baseline_probe.py (profiles/r02_cpu_baseline_probe*.txt)."""
+    import pamg
+    tmp = tempfile.mkdtemp(prefix="pamg_cpu_msh_")
+    try:
+        path = os.path.join(tmp, "strip.msh")
+        strip = pamg.Mesh.strip(*CPU_STRIP)
+        strip.write_msh(path)
+        U = strip.U
+        t1 = run_reference(path, 5, 1, 1)
+        t2 = run_reference(path, 5, 1, 2)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    if t1 is None or t2 is None or t2 <= t1:
+        return None
+    scale = 8192 / U
+    tc = t2 - t1
+    return dict(value=1.0 / (scale * tc), unit="V-cycles/s", cores=1, kind="reference",
+                sample=f"reference fp64 build (flang -O2) on 1 core of '{host_cpu()}' at n_split=5, multi_levels=3, "
+                       f"n_smooth=4 on a {U}-element synthetic strip ({CPU_STRIP[0]}x{CPU_STRIP[1]}x2): one time step "
+                       f"of 1 V-cycle took {t1:.2f} s and of 2 V-cycles {t2:.2f} s in its time_loop window; value = "
+                       f"1 / ({scale:g} x {tc:.2f} s), the steady-state V-cycle scaled to untitled8192's 8192 "
+                       f"elements (the reference's work is linear in the element count)",
+                seconds_1cycle=t1, seconds_2cycles=t2, host_cpu=host_cpu())
 
 
 def pmc_traffic(kernel, nsplit, levels):
@@ -352,8 +391,10 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline()
-        if cpu and "nsplit3_vcycles_per_s" in extra:
-            extra["nsplit3_speedup_vs_cpu"] = round(extra["nsplit3_vcycles_per_s"] / cpu["nsplit3_vcycles_per_s"], 1)
+        if cpu:
+            extra["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+            if time_loop:
+                extra["time_loop_speedup_vs_cpu"] = round(time_loop["vcycles_per_s"] / cpu["value"], 1)
     if rank == 0:
         line = {
             "metric": "multigrid V-cycles/sec + smoother HBM GB/s vs roofline, 8192-ele tri mesh",

@@ -45,6 +45,8 @@ extern "C" {
 #define PAMG_RHS 2         /* tracer(l)%RHS */
 #define PAMG_RESIDUAL 3    /* tracer(l)%residuale */
 #define PAMG_TNEW_NONLIN 4 /* tnew_nonlin (transport_tri_semi.F90:85), shape of its current level */
+#define PAMG_SOURCE 5      /* tracer(1)%source after get_RHS: level 1's cascaded source term s' (:452-464,
+                              :593), formed once at upload; level 1 only, pamg_get_state only */
 
 /* timed kernel classes (pamg_timing_*) */
 #define PAMG_K_SMOOTH_L1 0

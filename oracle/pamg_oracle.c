@@ -36,10 +36,23 @@
 #define NLOC 3
 #define NGI 3
 
+/* The per-un_ele loops of the mode-9 path are independent (block-diagonal operator; every halo
+ * word has one writer), so the checker splits them over OpenMP threads when built with
+ * -fopenmp: the results are the same bits for any thread count. */
+#ifdef _OPENMP
+#define PAMG_ORC_PARALLEL _Pragma("omp parallel for schedule(static)")
+#else
+#define PAMG_ORC_PARALLEL
+#endif
+
 typedef struct {
     int n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid;
     double dt, k, omega, theta;
     int coarse_solver;   /* 0: the reference (:351-353); 1: exact local solve (the build's direct path) */
+    int arith;           /* 0: the reference's operation order; 1: the build's contracted arithmetic
+                            (pamg_params.arith = 1): A_e = rdt M + Kd formed once, one fma chain per
+                            row -- the same algebra, other roundings; checks the HIP path's arith = 1
+                            bit for bit (solvers 1 / 3) */
 } orc_cfg;
 
 typedef struct {
@@ -58,6 +71,10 @@ typedef struct {
     double *nx[16];     /* (ngi,2,3,U) per level */
     double *t_overlap, *t_overlap_old; /* (2^S*3, 3, U) */
     int slots;
+    /* test hook (orc_set_source): level 1's cascaded source term s' taken from here instead of
+     * being evaluated with the host libm sin -- so that a comparison with the HIP path, whose
+     * device sin may differ in the last bit, can be bitwise everywhere else */
+    double *src_override;
 } orc_state;
 
 /* ---------------------------------------------------------------- helpers */
@@ -376,6 +393,7 @@ static void update_overlaps(orc_state *s, int l) {
     const double *T = s->tnew[l - 1], *To = s->told[l - 1];
     int nsub = s->nsub[l - 1];
     static const int face_order[3] = {1, 3, 2};
+    PAMG_ORC_PARALLEL
     for (int u = 0; u < s->U; ++u) {
         for (int fo = 0; fo < 3; ++fo) {
             int f = face_order[fo];
@@ -430,12 +448,43 @@ static void get_A_x(const orc_state *s, const double M[3][3], const double Kd[3]
 
 /* source (:593) + get_RHS (:452-464), level 1 only; writes rhs[3] and source */
 static void get_rhs_l1(const orc_state *s, const double M[3][3], const double xl[3][2],
-                       const double mo[3], double *src, double *rhs) {
+                       const double mo[3], double *src, double *rhs, const double *ovr) {
     double theta = s->c.theta, k = s->c.k;
     for (int i = 0; i < 3; ++i) src[i] = -(2 * k * boundary(xl[i][0], xl[i][1]));
     for (int i = 0; i < 3; ++i) {
-        src[i] = M[i][0] * src[0] + M[i][1] * src[1] + M[i][2] * src[2];
+        src[i] = ovr ? ovr[i] : M[i][0] * src[0] + M[i][1] * src[1] + M[i][2] * src[2];
         rhs[i] = theta * (mo[i] + src[i]) + (1. - theta) * (mo[i] + src[i]);
+    }
+}
+
+/* The contracted operator of the build's arith = 1 (not the reference's arithmetic): the element
+ * matrix A_e = rdt M + Kd formed once (pamg_setup.cpp level_stencil, kStcA), w = omega / D
+ * (get_diagonal :481-486); a sweep x_i += w_i (b_i - sum_j A_ij x_j) and the residual
+ * sum_j A_ij x_j - b_i as fma chains (pamg_device.h StcF). */
+static void contracted_ops(const double M[3][3], const double Kd[3][3], const double ml[3], double rdt, double om,
+                           double Ae[3][3], double w[3]) {
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) Ae[i][j] = rdt * M[i][j] + Kd[i][j];
+        double D = rdt * ml[i] + Kd[i][i] + 0.0;
+        w[i] = om / D;
+    }
+}
+
+static void contracted_sweep(const double Ae[3][3], const double w[3], const double *b, double *x) {
+    double t[3];
+    for (int i = 0; i < 3; ++i) {
+        t[i] = fma(-Ae[i][0], x[0], b[i]);
+        t[i] = fma(-Ae[i][1], x[1], t[i]);
+        t[i] = fma(-Ae[i][2], x[2], t[i]);
+    }
+    for (int i = 0; i < 3; ++i) x[i] = fma(w[i], t[i], x[i]);
+}
+
+static void contracted_residual(const double Ae[3][3], const double *x, const double *b, double *r) {
+    for (int i = 0; i < 3; ++i) {
+        double t = fma(Ae[i][0], x[0], -b[i]);
+        t = fma(Ae[i][1], x[1], t);
+        r[i] = fma(Ae[i][2], x[2], t);
     }
 }
 
@@ -447,6 +496,7 @@ static void smoother(orc_state *s, int l) {
     for (int sm = 0; sm < s->c.n_smooth; ++sm) {
         memcpy(T, s->tnn, lvl_len(s, l) * sizeof(double));     /* :550 */
         update_overlaps(s, l);                                  /* :555 */
+        PAMG_ORC_PARALLEL
         for (int u = 0; u < s->U; ++u) {
             double M[3][3], Kd[3][3], ml[3];
             stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
@@ -463,8 +513,16 @@ static void smoother(orc_state *s, int l) {
                 double A[3], mo[3], D[3];
                 const double *xin = (s->c.solver == 3) ? tnn : T + o;   /* get_A_x(.true./.false.) */
                 get_A_x(s, M, Kd, rdt, xin, To + o, A, mo);
-                if (l == 1) get_rhs_l1(s, M, xl, mo, Src + o, R + o);
+                if (l == 1) get_rhs_l1(s, M, xl, mo, Src + o, R + o, s->src_override ? s->src_override + o : NULL);
                 else for (int i = 0; i < 3; ++i) Src[o + i] = -(2 * s->c.k * boundary(xl[i][0], xl[i][1]));
+                if (s->c.arith == 1) {   /* the build's contracted arithmetic (Jacobi = GS here) */
+                    double Ae[3][3], w[3], x[3];
+                    contracted_ops(M, Kd, ml, rdt, om, Ae, w);
+                    for (int i = 0; i < 3; ++i) x[i] = xin[i];
+                    contracted_sweep(Ae, w, R + o, x);
+                    for (int i = 0; i < 3; ++i) tnn[i] = x[i];
+                    continue;
+                }
                 for (int i = 0; i < 3; ++i) D[i] = rdt * ml[i] + Kd[i][i] + 0.0;   /* get_diagonal :481-486 */
                 for (int i = 0; i < 3; ++i) {
                     double base = (s->c.solver == 3) ? tnn[i] : T[o + i];   /* :504 vs :494 */
@@ -480,6 +538,7 @@ static void get_residual(orc_state *s, int l) {
     int i_split = s->c.n_split - l + 1, nsub = s->nsub[l - 1];
     double rdt = 1 / s->c.dt;
     double *T = s->tnew[l - 1], *To = s->told[l - 1], *R = s->rhs[l - 1], *Src = s->source[l - 1];
+    PAMG_ORC_PARALLEL
     for (int u = 0; u < s->U; ++u) {
         double M[3][3], Kd[3][3], ml[3];
         stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
@@ -488,8 +547,14 @@ static void get_residual(orc_state *s, int l) {
             double xl[3][2], A[3], mo[3];
             get_splitting(s->X + 6 * u, i_split, se, xl);
             get_A_x(s, M, Kd, rdt, T + o, To + o, A, mo);
-            if (l == 1) get_rhs_l1(s, M, xl, mo, Src + o, R + o);
+            if (l == 1) get_rhs_l1(s, M, xl, mo, Src + o, R + o, s->src_override ? s->src_override + o : NULL);
             else for (int i = 0; i < 3; ++i) Src[o + i] = -(2 * s->c.k * boundary(xl[i][0], xl[i][1]));
+            if (s->c.arith == 1 && s->c.solver != 2) {
+                double Ae[3][3], w[3];
+                contracted_ops(M, Kd, ml, rdt, s->c.omega, Ae, w);
+                contracted_residual(Ae, T + o, R + o, s->res[l - 1] + o);
+                continue;
+            }
             for (int i = 0; i < 3; ++i) s->res[l - 1][o + i] = A[i] - R[o + i];
         }
     }
@@ -501,6 +566,7 @@ static void restrictor(orc_state *s, int l) {
     int i_split = s->c.n_split - l + 1, nf = s->nsub[l - 1], nc = s->nsub[l];
     const double *r = s->res[l - 1];
     double *b = s->rhs[l];
+    PAMG_ORC_PARALLEL
     for (int u = 0; u < s->U; ++u)
         for (int c = 1; c <= nc; ++c) {
             int fin[4];
@@ -518,6 +584,7 @@ static void prolongator(orc_state *s, int l) {
     int i_split = s->c.n_split - l + 1, nf = s->nsub[l - 1], nc = s->nsub[l];
     double *F = s->tnew[l - 1];
     const double *Y = s->tnew[l];
+    PAMG_ORC_PARALLEL
     for (int u = 0; u < s->U; ++u)
         for (int c = 1; c <= nc; ++c) {
             int fin[4];
@@ -688,7 +755,7 @@ void orc_free(orc_state *s) {
         free(s->tnew[l]); free(s->told[l]); free(s->rhs[l]); free(s->res[l]); free(s->source[l]);
         free(s->detwei[l]); free(s->nx[l]);
     }
-    free(s->tnn); free(s->t_overlap); free(s->t_overlap_old);
+    free(s->tnn); free(s->t_overlap); free(s->t_overlap_old); free(s->src_override);
     free(s->X); free(s->region); free(s->neig); free(s->fneig); free(s->dir);
     free(s);
 }
@@ -723,6 +790,17 @@ int orc_set(orc_state *s, int what, int l, const double *in) {
 }
 
 int orc_tnn_level(orc_state *s) { return s->tnn_level; }
+
+/* test hook: level 1's cascaded source term s' in the (3, nsub_1, U) layout (NULL: evaluate it) */
+int orc_set_source(orc_state *s, const double *src1) {
+    free(s->src_override);
+    s->src_override = NULL;
+    if (!src1) return 0;
+    s->src_override = malloc(lvl_len(s, 1) * sizeof(double));
+    if (!s->src_override) return -1;
+    memcpy(s->src_override, src1, lvl_len(s, 1) * sizeof(double));
+    return 0;
+}
 
 void orc_get_overlap(orc_state *s, double *tov, double *tovo) {
     size_t n = (size_t)s->slots * 3 * s->U;

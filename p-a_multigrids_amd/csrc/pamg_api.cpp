@@ -160,6 +160,7 @@ double *field_ptr(pamg_handle *h, int l, int what) {
         case PAMG_RHS: return L.RHS;
         case PAMG_RESIDUAL: return L.RES;
         case PAMG_TNEW_NONLIN: return L.TNN;
+        case PAMG_SOURCE: return L.SRC;   // level 1 only (null elsewhere)
     }
     return nullptr;
 }
@@ -1026,7 +1027,7 @@ int pamg_set_state(pamg_handle *h, int level, int what, const double *host) {
     if (what == PAMG_TNEW_NONLIN) { CHK(check_level(h, level)); h->tnn_level = level; }
     CHK(check_level(h, level));
     Level &L = h->lv[level];
-    double *dst = field_ptr(h, level, what);
+    double *dst = what == PAMG_SOURCE ? nullptr : field_ptr(h, level, what);   // the source is read-only
     if (!dst) return PAMG_ERR_ARG;
     CHK(ensure_scratch(h, 3 * (size_t)L.N * sizeof(double)));
     HIPCHK(h, hipMemcpyAsync(h->scratch, host, 3 * (size_t)L.N * sizeof(double), hipMemcpyHostToDevice, h->stream));

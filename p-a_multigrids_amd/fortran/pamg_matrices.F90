@@ -2,22 +2,20 @@
 ! (matrices.F90:172-193) over the reference's `type sparse` (Structures.F90:196-201),
 ! computed on the GPU by libpamg's csr kernel -- bitwise equal to the reference's routine
 ! (fp64: the reference's REAL built with -fdefault-real-8; tests/test_csr.py).
-! `sparse` here has the reference's components; a code base adopting the module takes the
-! type from it (`use pamg_matrices, only: sparse` where Structures defines it), or calls
-! csr_mul_array_arrays with the components of its own type. Each call uploads the matrix;
+! `sparse` is module structures' (the reference's Structures.F90 type, structures.F90), so a
+! caller's own type(sparse) matrices pass straight in; csr_mul_array_arrays takes the bare
+! components. Each call uploads the matrix;
 ! a constant matrix used every step is uploaded once with csr_upload / csr_mul_array_gpu.
 module pamg_matrices
   use iso_c_binding
   use pamg
+  use structures, only: sparse
   implicit none
   private
   type(c_ptr), save :: h_csr = c_null_ptr
 
-  type, public :: sparse
-    integer, allocatable :: g_iloc(:)
-    integer, allocatable :: g_jloc(:)
-    doubleprecision, allocatable :: val(:)
-  end type sparse
+  ! the reference's type sparse (Structures.F90:196-201), from module structures
+  public :: sparse
 
   type, public :: csr_gpu
     type(c_ptr) :: m = c_null_ptr

@@ -12,7 +12,7 @@ module pamg
 
   integer(c_int), parameter, public :: PAMG_OK = 0
   integer(c_int), parameter, public :: PAMG_TNEW = 0, PAMG_TOLD = 1, PAMG_RHS = 2, PAMG_RESIDUAL = 3
-  integer(c_int), parameter, public :: PAMG_TNEW_NONLIN = 4
+  integer(c_int), parameter, public :: PAMG_TNEW_NONLIN = 4, PAMG_SOURCE = 5
 
   type, bind(C), public :: pamg_params
     integer(c_int) :: n_split, multi_levels, n_smooth, n_coarse, solver, device
@@ -31,7 +31,7 @@ module pamg
   public :: pamg_begin_timestep, pamg_copy_to_nonlin, pamg_smoother, pamg_sweep, pamg_restrictor
   public :: pamg_get_residual, pamg_prolongator, pamg_vcycle, pamg_run, pamg_synchronize
   public :: pamg_destroy, pamg_last_error, pamg_check, c_path, pamg_block_inverse, pamg_direct_solve
-  public :: pamg_write_vtu, pamg_csr_create, pamg_csr_mul_array, pamg_csr_free
+  public :: pamg_write_vtu, pamg_csr_create, pamg_csr_mul_array, pamg_csr_free, pamg_tnn_level
 
   interface
     subroutine pamg_default_params(p) bind(C, name='pamg_default_params')
@@ -130,6 +130,10 @@ module pamg
       import :: c_int, c_ptr
       type(c_ptr), value :: h
       integer(c_int), value :: ntime, n_multigrid
+    end function
+    integer(c_int) function pamg_tnn_level(h) bind(C, name='pamg_tnn_level')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
     end function
     integer(c_int) function pamg_synchronize(h) bind(C, name='pamg_synchronize')
       import :: c_int, c_ptr

@@ -19,7 +19,8 @@
 program pamg_transport
   use iso_c_binding
   use pamg
-  use LinearSolvers, only: MeshRec => Mesh, pamg_bind_handle, GSsolver_MeshSD
+  use structures, only: MeshRec => Mesh
+  use LinearSolvers, only: pamg_bind_handle, GSsolver_MeshSD
   use pamg_dump, only: write_dump
   implicit none
 
@@ -78,7 +79,7 @@ program pamg_transport
     meshList(u_)%Dir = dir(3*(u_-1)+1:3*u_) /= 0
     meshList(u_)%region_id = region(u_)
   end do
-  call pamg_bind_handle(h)
+  call pamg_bind_handle(h, int(U), n_split, multi_levels)
 
   print *, '|   n_split =', n_split
   print *, '|   multigrid levels =', multi_levels

@@ -17,7 +17,7 @@ PAMG_OK = 0
 ERRORS = {-1: "PAMG_ERR_ARG", -2: "PAMG_ERR_HIP", -3: "PAMG_ERR_IO", -4: "PAMG_ERR_STATE",
           -5: "PAMG_ERR_COMM", -6: "PAMG_ERR_NODEV"}
 
-TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN = 0, 1, 2, 3, 4
+TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN, SOURCE = 0, 1, 2, 3, 4, 5
 (K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH, K_VCYCLE,
  K_VCYCLE_COARSE) = range(10)
 K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle",

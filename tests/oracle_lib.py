@@ -21,7 +21,7 @@ class OrcCfg(C.Structure):
     _fields_ = [("n_split", C.c_int), ("levels", C.c_int), ("n_smooth", C.c_int),
                 ("n_coarse", C.c_int), ("solver", C.c_int), ("ntime", C.c_int),
                 ("n_multigrid", C.c_int), ("dt", C.c_double), ("k", C.c_double),
-                ("omega", C.c_double), ("theta", C.c_double), ("coarse_solver", C.c_int)]
+                ("omega", C.c_double), ("theta", C.c_double), ("coarse_solver", C.c_int), ("arith", C.c_int)]
 
 
 _lib = None
@@ -48,6 +48,7 @@ def lib():
         L.orc_get.restype = C.c_long
         L.orc_get.argtypes = [P, C.c_int, C.c_int, C.c_void_p]
         L.orc_set.argtypes = [P, C.c_int, C.c_int, dp]
+        L.orc_set_source.argtypes = [P, C.c_void_p]
         L.orc_tnn_level.argtypes = [P]
         L.orc_get_overlap.argtypes = [P, dp, dp]
         L.orc_level_geometry.argtypes = [P, C.c_int, dp, dp, dp, dp]
@@ -89,11 +90,11 @@ def read_msh(path):
 
 class Oracle:
     def __init__(self, mesh, n_split, levels, n_smooth=4, solver=3, ntime=2, n_multigrid=2,
-                 n_coarse=15, dt=1.25e-5, k=1.0, omega=0.8, theta=1.0, coarse_solver=0):
+                 n_coarse=15, dt=1.25e-5, k=1.0, omega=0.8, theta=1.0, coarse_solver=0, arith=0):
         self.L = lib()
         self.mesh = mesh
         self.cfg = OrcCfg(n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid, dt, k, omega, theta,
-                          coarse_solver)
+                          coarse_solver, arith)
         self.h = self.L.orc_create(C.byref(self.cfg), mesh.U, mesh.X, mesh.region, mesh.neig,
                                    mesh.fneig, mesh.dir)
         if not self.h:
@@ -118,6 +119,17 @@ class Oracle:
     def set(self, what, level, arr):
         a = np.ascontiguousarray(np.asarray(arr, np.float64).reshape(-1, order="F"))
         assert self.L.orc_set(self.h, what, level, a) == 0
+
+    def set_source(self, src1):
+        """test hook: level 1's cascaded source term s' (3, nsub_1, U) used instead of evaluating
+        it with the host's sin (None: evaluate it again)"""
+        if src1 is None:
+            assert self.L.orc_set_source(self.h, None) == 0
+            return
+        a = np.ascontiguousarray(np.asarray(src1, np.float64).reshape(-1, order="F"))
+        assert a.size == 3 * self.nsub(1) * self.mesh.U
+        self._src = a
+        assert self.L.orc_set_source(self.h, a.ctypes.data) == 0
 
     def overlap(self):
         n = (2 ** self.n_split) * 3 * 3 * self.mesh.U

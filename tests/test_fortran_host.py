@@ -58,6 +58,42 @@ def test_linear_solvers_facade_runs(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+FACADE = os.path.join(ROOT, "p-a_multigrids_amd", "bin", "facade_host")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,it", [("untitled8.msh", 3, 3, 5), ("irregular.msh", 4, 2, 3),
+                                         ("900_ele.msh", 2, 2, -1), ("untitled8.msh", 2, 1, 1)])
+def test_gssolver_mesh_sd_facade_matches_oracle(tmp_path, mesh, S, L, it):
+    """A reference-shaped Fortran caller (fortran/facade_host.F90) builds meshL(:) of the
+    reference's type(mesh) from module structures, binds it and calls
+    GSsolver_MeshSD(meshL, 1, it) with LinearSolvers.F90:719-733's signature (it = -1: the
+    argument omitted, the reference's default size(meshL)/2). After it sweeps its
+    tracer(1)%tnew and tnew_nonlin (read back as type(fields)) equal the oracle's smoother state
+    after begin_timestep, tnew_nonlin := tnew and `it` sweeps, bit for bit (the oracle takes the
+    device's source term s', tests/test_contracted_oracle.py)."""
+    import numpy as np
+
+    import oracle_lib as O
+    out = str(tmp_path / "facade.bin")
+    r = subprocess.run([FACADE, os.path.join(goldens.MESHES, mesh), str(S), str(L), "1", str(it), out],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = np.fromfile(out, np.float64)
+    U, nsub, lv, used = (int(v) for v in raw[:4])
+    n = 3 * nsub * U
+    tnew, tnn, rhs, src = (raw[4 + q * n:4 + (q + 1) * n].reshape((3, nsub, U), order="F") for q in range(4))
+    assert lv == 1 and used == (it if it >= 0 else U // 2) and raw.size == 4 + 4 * n
+    o = O.Oracle(O.read_msh(os.path.join(goldens.MESHES, mesh)), S, L, n_smooth=used)
+    o.set_source(src)
+    o.begin_timestep()
+    o.copy_to_tnn(1)
+    o.smoother(1)
+    np.testing.assert_array_equal(tnew, o.get(O.TNEW, 1))
+    np.testing.assert_array_equal(tnn, o.get(O.TNN, 1))
+    np.testing.assert_array_equal(rhs, o.get(O.RHS, 1))
+
+
 @pytest.mark.gpu
 def test_host_vtu_call_site_matches_reference(tmp_path):
     """vtk_interval = 1: the host writes Tracer_<itime>.vtu at the reference's get_vtu call
