@@ -108,7 +108,15 @@ typedef struct {
                          correction (P1 interpolation of the coarse iterate) is added to the iterate
                          the next smoother call starts from; per-step kernels; no reference output
                          exists, pinned to the oracle's restatement */
-    int reserved[2];
+    int op;           /* 0 (default): the reference's mode-9 operator, block diagonal (its surface terms are
+                         commented out, transport_tri_semi.F90:619-688); 1: the face-coupled interior-penalty
+                         diffusion operator of SURVEY.md 8(f) rank 1 -- the surface terms with
+                         the reference's t_overlap halo as the values across un_ele faces (read every sweep,
+                         exchanged every sweep between ranks), red-black (up / down) Gauss-Seidel for
+                         solver 3, Jacobi for solver 1; per-step kernels; no reference output exists (the
+                         reference cannot run the block), pinned to the oracle's restatement.
+                         Not with solver 2 or coarse_solver 1 */
+    int reserved[1];
 } pamg_params;
 
 /* mode-9 defaults of the reference (main.F90:46-47, transport_tri_semi.F90:117-140) */

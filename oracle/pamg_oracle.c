@@ -49,6 +49,8 @@ typedef struct {
     int n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid;
     double dt, k, omega, theta;
     int coarse_solver;   /* 0: the reference (:351-353); 1: exact local solve (the build's direct path) */
+    int op;              /* 0: the reference's mode-9 operator (block diagonal); 1: the face-coupled
+                            interior-penalty operator of SURVEY.md 8(f) rank 1 (face_* below) */
     int arith;           /* 0: the reference's operation order; 1: the build's contracted arithmetic
                             (pamg_params.arith = 1): A_e = rdt M + Kd formed once, one fma chain per
                             row -- the same algebra, other roundings; checks the HIP path's arith = 1
@@ -75,6 +77,13 @@ typedef struct {
      * being evaluated with the host libm sin -- so that a comparison with the HIP path, whose
      * device sin may differ in the last bit, can be bitwise everywhere else */
     double *src_override;
+    /* op = 1, per level: fnb (nsub, 3) the neighbour str_ele across each face (> 0) or -sp (the
+     * sub-element's position along its un_ele face, < 0); fw (U, 9) the face weights w_in[3] (inner
+     * faces by face index), w_b[3] (un_ele faces 1..3) and D0[3] = rdt ml + Kd_ii; fsx (U, 3) per
+     * un_ele face the neighbour-local nodes S(F1) | S(F2) << 2 holding the values at my face nodes */
+    int *fnb[16];
+    double *fw[16];
+    int *fsx[16];
 } orc_state;
 
 /* ---------------------------------------------------------------- helpers */
@@ -488,6 +497,270 @@ static void contracted_residual(const double Ae[3][3], const double *x, const do
     }
 }
 
+/* ---------------------------------------------- the face-coupled operator (op = 1)
+ *
+ * the surface terms the reference leaves commented out in its smoother
+ * and residual (transport_tri_semi.F90:619-688, :789-857) -- the diffusion surface integral of
+ * add_diffusion_surf (matrices.F90:66-117), (k / delta_x) int_f N_i (t - t2) ds, assembled as
+ * get_diff_surf_stencl (:468-477) my_diff_surf / Neig_diff_surf, added to A x in get_A_x (:426-446)
+ * and its self part to the diagonal in get_diagonal (:481-486). The reference cannot run it
+ * (Mesh%S_nodes is never allocated, Structures.F90:157; the FORALL of :437-447 is a many-to-one
+ * assignment), so this restatement DEFINES it, using the reference's own data:
+ *  - faces of a sub-element: face_nodes F(1) = (1,3), F(2) = (3,2), F(3) = (2,1) (:142-147);
+ *  - neighbour across face f inside the un_ele: str_neig(f, e) (get_str_neig_multigrid,
+ *    splitting.F90:732-776); its nodes at my face nodes F1, F2 are its F2, F1 (the up and down
+ *    sub-elements are point reflections of each other);
+ *  - across an un_ele face (str_neig = 0): sp and mface as the commented loop (:626-637): f = 1 ->
+ *    (ipos/2 + 1, un_ele face 1), f = 2 -> (irow, 3), f = 3 -> (irow, 2); the neighbour's three
+ *    values are t_overlap(3sp-2 : 3sp, mface), written by update_overlaps (splitting.F90:1210-1397)
+ *    -- its slot geometry checked against the coordinates (scripts in DESIGN.md 7) -- and
+ *    S_nodes, which of them sit at my face nodes, is derived from the coordinates here; at a
+ *    domain boundary the slot holds the boundary values sin(x + y) at my own face nodes;
+ *  - face matrix: the P1 edge mass matrix |e| / 6 [[2, 1], [1, 2]] (the 2-point rule of the
+ *    reference's face shape functions integrates it exactly) times k / delta_x, delta_x the
+ *    distance between the two sub-elements' centroids (between the centroid and the face
+ *    midpoint at a domain boundary, add_diffusion_surf's :90-104);
+ *  - smoothing: the block (3x3) smoother of the reference with the face terms, as red-black
+ *    Gauss-Seidel -- up sub-elements, then down ones (every inner neighbour of an up sub-element
+ *    is a down one) -- for solver 3, Jacobi for solver 1; the values across un_ele faces are
+ *    the halo snapshot update_overlaps takes at the start of every sweep (:555);
+ *  - get_residual refreshes the halo from tnew first, so res = A tnew - RHS is consistent. */
+static const int FNODE[3][2] = {{1, 3}, {3, 2}, {2, 1}};
+static const int FMFACE[3] = {1, 3, 2};
+
+/* splitting.F90:732-776 get_str_neig_multigrid: sn[(f - 1) + 3 (e - 1)] */
+static void get_str_neig(int n, int *sn) {
+    int total = (1 << (n + 1)) - 1, current = total, irow = (1 << n) - 1, ele;
+#define SN(f, e) sn[((f) - 1) + 3 * ((e) - 1)]
+    SN(1, 1) = 0; SN(2, 1) = 0; SN(3, 1) = 2;
+    ele = 2;
+    while (ele <= total) {
+        SN(2, ele) = ele + 1; SN(3, ele) = ele - 1; SN(1, ele) = ele + total - 1;
+        ele = ele + 1;
+        SN(2, ele) = ele - 1; SN(1, ele) = 0; SN(3, ele) = ele + 1;
+        ele = ele + 1;
+    }
+    SN(3, ele - 1) = 0;
+    while (irow >= 1) {
+        total = total + current - 2;
+        current = current - 2;
+        SN(2, ele) = 0; SN(3, ele) = ele + 1; SN(1, ele) = ele - current - 1;
+        ele = ele + 1;
+        while (ele <= total) {
+            SN(2, ele) = ele + 1; SN(3, ele) = ele - 1; SN(1, ele) = ele + current - 1;
+            ele = ele + 1;
+            SN(2, ele) = ele - 1; SN(3, ele) = ele + 1; SN(1, ele) = ele - current - 1;
+            ele = ele + 1;
+        }
+        SN(3, ele - 1) = 0;
+        irow = irow - 1;
+    }
+#undef SN
+}
+
+static double dist2d(const double a[2], const double b[2]) {
+    double dx = a[0] - b[0], dy = a[1] - b[1];
+    return sqrt(dx * dx + dy * dy);
+}
+
+static void centroid(double xl[3][2], double c[2]) {
+    for (int d = 0; d < 2; ++d) c[d] = (xl[0][d] + xl[1][d] + xl[2][d]) / 3.0;
+}
+
+/* face weight k / delta_x * |e| / 6 */
+static double face_weight(double k, double delta, double len) { return k / delta * len / 6.0; }
+
+/* slot that update_overlaps gives the sub-element at position i of face f of un_ele q (splitting.F90:1297-1391) */
+static int overlap_kslot(const orc_state *s, int q, int f, int i_split, int i) {
+    int m = 1 << i_split, *surf = malloc(sizeof(int) * 3 * m), irow = 0, ipos = 0, orient = 0, fwd, rev;
+    loc_surf_ele(i_split, surf);
+    get_str_info(i_split, surf[(i - 1) + (f - 1) * m], &irow, &ipos, &orient);
+    free(surf);
+    if (f == 1) { fwd = ipos / 2 + 1; rev = m - (ipos / 2 + 1) + 1; }
+    else { fwd = irow; rev = m - irow + 1; }
+    if (f == 2) { int t = fwd; fwd = rev; rev = t; }
+    int nside = s->fneig[3 * q + f - 1], dr = s->dir[3 * q + f - 1];
+    return (nside == 2) ? (dr ? rev : fwd) : (dr ? fwd : rev);
+}
+
+static int face_setup(orc_state *s) {
+    double rdt = 1 / s->c.dt;
+    for (int l = 1; l <= s->c.levels; ++l) {
+        int is = s->c.n_split - l + 1, nsub = s->nsub[l - 1], m = 1 << is;
+        int *sn = malloc(sizeof(int) * 3 * nsub), *surf = malloc(sizeof(int) * 3 * m);
+        get_str_neig(is, sn);
+        loc_surf_ele(is, surf);
+        s->fnb[l - 1] = malloc(sizeof(int) * 3 * nsub);
+        s->fw[l - 1] = calloc((size_t)9 * s->U, sizeof(double));
+        s->fsx[l - 1] = calloc((size_t)3 * s->U, sizeof(int));
+        for (int e = 1; e <= nsub; ++e) {
+            int irow = 0, ipos = 0, orient = 0;
+            get_str_info(is, e, &irow, &ipos, &orient);
+            for (int f = 1; f <= 3; ++f) {
+                int nb = sn[(f - 1) + 3 * (e - 1)];
+                int sp = (f == 1) ? ipos / 2 + 1 : irow;
+                s->fnb[l - 1][(f - 1) + 3 * (e - 1)] = nb ? nb : -sp;
+            }
+        }
+        for (int u = 0; u < s->U; ++u) {
+            const double *X = s->X + 6 * u;
+            double *w = s->fw[l - 1] + 9 * u;
+            /* inner faces: the first up sub-element (str_ele order) with a neighbour across f */
+            for (int f = 1; f <= 3; ++f) {
+                for (int e = 1; e <= nsub; ++e) {
+                    int irow = 0, ipos = 0, orient = 0, nb = sn[(f - 1) + 3 * (e - 1)];
+                    get_str_info(is, e, &irow, &ipos, &orient);
+                    if (!(ipos % 2) || !nb) continue;
+                    double xe[3][2], xn[3][2], ce[2], cn[2];
+                    get_splitting(X, is, e, xe);
+                    get_splitting(X, is, nb, xn);
+                    centroid(xe, ce);
+                    centroid(xn, cn);
+                    w[f - 1] = face_weight(s->c.k, dist2d(ce, cn), dist2d(xe[FNODE[f - 1][0] - 1], xe[FNODE[f - 1][1] - 1]));
+                    break;
+                }
+            }
+            /* un_ele faces: the boundary sub-element at sp = 1 and what faces it */
+            for (int fi = 0; fi < 3; ++fi) {
+                int mface = FMFACE[fi], se = surf[0 + (mface - 1) * m];
+                int a = FNODE[fi][0], b = FNODE[fi][1];
+                double xe[3][2], ce[2];
+                get_splitting(X, is, se, xe);
+                centroid(xe, ce);
+                double len = dist2d(xe[a - 1], xe[b - 1]);
+                int npos = s->neig[3 * u + mface - 1];
+                if (npos == 0) {
+                    double mid[2] = {(xe[a - 1][0] + xe[b - 1][0]) / 2.0, (xe[a - 1][1] + xe[b - 1][1]) / 2.0};
+                    w[3 + mface - 1] = face_weight(s->c.k, dist2d(ce, mid), len);
+                    s->fsx[l - 1][3 * u + mface - 1] = a | (b << 2);
+                    continue;
+                }
+                int q = npos - 1, nside = s->fneig[3 * u + mface - 1], found = 0;
+                for (int i = 1; i <= m && !found; ++i) {
+                    if (overlap_kslot(s, q, nside, is, i) != 1) continue;
+                    double xn[3][2], cn[2];
+                    get_splitting(s->X + 6 * q, is, surf[(i - 1) + (nside - 1) * m], xn);
+                    centroid(xn, cn);
+                    int S[2] = {0, 0};
+                    for (int t = 0; t < 2; ++t) {
+                        const double *p = xe[(t ? b : a) - 1];
+                        double best = 1e300;
+                        for (int r = 0; r < 3; ++r) {
+                            double d = dist2d(p, xn[r]);
+                            if (d < best) { best = d; S[t] = r + 1; }
+                        }
+                        if (best > 1e-9 * len) { free(sn); free(surf); return -1; }   /* slot geometry broken */
+                    }
+                    w[3 + mface - 1] = face_weight(s->c.k, dist2d(ce, cn), len);
+                    s->fsx[l - 1][3 * u + mface - 1] = S[0] | (S[1] << 2);
+                    found = 1;
+                }
+                if (!found) { free(sn); free(surf); return -2; }
+            }
+            /* D0 = rdt ml + Kd_ii + 0.0 (get_diagonal :481-486) */
+            double M[3][3], Kd[3][3], ml[3];
+            stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+            for (int i = 0; i < 3; ++i) w[6 + i] = rdt * ml[i] + Kd[i][i] + 0.0;
+        }
+        free(sn);
+        free(surf);
+    }
+    return 0;
+}
+
+/* the face terms of sub-element e (0-based index o = 3 (u nsub + e - 1)) and its diagonal:
+ * ds_i = sum_{f ∋ i} w_f ((2 x_i + x_j) - 2 y_i - y_j) (faces in order), D_i = D0_i + sum_{f ∋ i} 2 w_f;
+ * y = the neighbour's values at my face nodes: inner ones from `src` (the level's array the
+ * neighbour's iterate is read from), across an un_ele face from t_overlap */
+static void face_terms(const orc_state *s, int l, int u, int e, const double *x, const double *src, double ds[3],
+                       double D[3]) {
+    int nsub = s->nsub[l - 1], sl = s->slots;
+    const double *w = s->fw[l - 1] + 9 * u;
+    for (int i = 0; i < 3; ++i) { ds[i] = 0.0; D[i] = w[6 + i]; }
+    for (int fi = 0; fi < 3; ++fi) {
+        int a = FNODE[fi][0] - 1, b = FNODE[fi][1] - 1, nb = s->fnb[l - 1][fi + 3 * (e - 1)];
+        double ya, yb, wf;
+        if (nb > 0) {
+            const double *yn = src + (size_t)3 * ((size_t)u * nsub + nb - 1);
+            ya = yn[b];
+            yb = yn[a];
+            wf = w[fi];
+        } else {
+            int mface = FMFACE[fi], sx = s->fsx[l - 1][3 * u + mface - 1];
+            const double *slot = s->t_overlap + (size_t)u * sl * 3 + (size_t)(mface - 1) * sl + (size_t)(-nb - 1) * 3;
+            if (l > 1 && s->neig[3 * u + mface - 1] == 0) {
+                ya = 0.0;   /* the coarse levels carry the error equation: homogeneous boundary data */
+                yb = 0.0;
+            } else {
+                ya = slot[(sx & 3) - 1];
+                yb = slot[((sx >> 2) & 3) - 1];
+            }
+            wf = w[3 + mface - 1];
+        }
+        ds[a] = ds[a] + wf * (((2.0 * x[a] + x[b]) - 2.0 * ya) - yb);
+        ds[b] = ds[b] + wf * (((x[a] + 2.0 * x[b]) - ya) - 2.0 * yb);
+        D[a] = D[a] + 2.0 * wf;
+        D[b] = D[b] + 2.0 * wf;
+    }
+}
+
+/* one smoother sweep of the face-coupled operator after the halo snapshot: solver 3 red-black
+ * (up sub-elements from tnn, then down ones, in place), solver 1 Jacobi (from tnew, the sweep's
+ * start) */
+static void face_sweep(orc_state *s, int l) {
+    int nsub = s->nsub[l - 1], i_split = s->c.n_split - l + 1;
+    double rdt = 1 / s->c.dt, om = s->c.omega;
+    double *T = s->tnew[l - 1], *To = s->told[l - 1], *R = s->rhs[l - 1], *Src = s->source[l - 1];
+    for (int color = 1; color >= 0; --color) {
+        PAMG_ORC_PARALLEL
+        for (int u = 0; u < s->U; ++u) {
+            double M[3][3], Kd[3][3], ml[3];
+            stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+            for (int se = 1; se <= nsub; ++se) {
+                int irow = 0, ipos = 0, orient = 0;
+                get_str_info(i_split, se, &irow, &ipos, &orient);
+                if (s->c.solver == 3 && (ipos % 2) != color) continue;
+                if (s->c.solver != 3 && color == 0) continue;   /* Jacobi: one pass */
+                size_t o = (size_t)3 * ((size_t)u * nsub + se - 1);
+                double xl[3][2], A[3], mo[3], ds[3], D[3];
+                get_splitting(s->X + 6 * u, i_split, se, xl);
+                const double *xin = (s->c.solver == 3) ? s->tnn + o : T + o;
+                get_A_x(s, M, Kd, rdt, xin, To + o, A, mo);
+                if (l == 1) get_rhs_l1(s, M, xl, mo, Src + o, R + o, s->src_override ? s->src_override + o : NULL);
+                face_terms(s, l, u, se, xin, (s->c.solver == 3) ? s->tnn : T, ds, D);
+                double x[3] = {xin[0], xin[1], xin[2]};
+                for (int i = 0; i < 3; ++i) A[i] = A[i] + ds[i];
+                for (int i = 0; i < 3; ++i) s->tnn[o + i] = x[i] + om / D[i] * (R[o + i] - A[i]);
+            }
+        }
+    }
+}
+
+/* res = A tnew - RHS (neg: RHS - A tnew) of the face-coupled operator, halo refreshed from tnew */
+static void face_residual(orc_state *s, int l, int neg) {
+    int nsub = s->nsub[l - 1], i_split = s->c.n_split - l + 1;
+    double rdt = 1 / s->c.dt;
+    double *T = s->tnew[l - 1], *To = s->told[l - 1], *R = s->rhs[l - 1], *Src = s->source[l - 1];
+    update_overlaps(s, l);
+    PAMG_ORC_PARALLEL
+    for (int u = 0; u < s->U; ++u) {
+        double M[3][3], Kd[3][3], ml[3];
+        stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+        for (int se = 1; se <= nsub; ++se) {
+            size_t o = (size_t)3 * ((size_t)u * nsub + se - 1);
+            double xl[3][2], A[3], mo[3], ds[3], D[3];
+            get_splitting(s->X + 6 * u, i_split, se, xl);
+            get_A_x(s, M, Kd, rdt, T + o, To + o, A, mo);
+            if (l == 1) get_rhs_l1(s, M, xl, mo, Src + o, R + o, s->src_override ? s->src_override + o : NULL);
+            face_terms(s, l, u, se, T + o, T, ds, D);
+            for (int i = 0; i < 3; ++i) {
+                double a = A[i] + ds[i];
+                s->res[l - 1][o + i] = neg ? R[o + i] - a : a - R[o + i];
+            }
+        }
+    }
+}
+
 /* transport_tri_semi.F90:543-722 smoother */
 static void smoother(orc_state *s, int l) {
     int i_split = s->c.n_split - l + 1, nsub = s->nsub[l - 1];
@@ -496,6 +769,10 @@ static void smoother(orc_state *s, int l) {
     for (int sm = 0; sm < s->c.n_smooth; ++sm) {
         memcpy(T, s->tnn, lvl_len(s, l) * sizeof(double));     /* :550 */
         update_overlaps(s, l);                                  /* :555 */
+        if (s->c.op == 1) {
+            face_sweep(s, l);
+            continue;
+        }
         PAMG_ORC_PARALLEL
         for (int u = 0; u < s->U; ++u) {
             double M[3][3], Kd[3][3], ml[3];
@@ -535,6 +812,10 @@ static void smoother(orc_state *s, int l) {
 
 /* transport_tri_semi.F90:725-873 get_residual */
 static void get_residual(orc_state *s, int l) {
+    if (s->c.op == 1) {
+        face_residual(s, l, 0);
+        return;
+    }
     int i_split = s->c.n_split - l + 1, nsub = s->nsub[l - 1];
     double rdt = 1 / s->c.dt;
     double *T = s->tnew[l - 1], *To = s->told[l - 1], *R = s->rhs[l - 1], *Src = s->source[l - 1];
@@ -711,6 +992,8 @@ int orc_msh_load(const char *path, int U, double *X, int *region, int *neig, int
     return 0;
 }
 
+void orc_free(orc_state *s);
+
 orc_state *orc_create(const orc_cfg *cfg, int U, const double *X, const int *region, const int *neig,
                       const int *fneig, const int *dir) {
     if (cfg->levels < 1 || cfg->levels > cfg->n_split || cfg->n_split > 12) return NULL;  /* :120-123 */
@@ -746,6 +1029,10 @@ orc_state *orc_create(const orc_cfg *cfg, int U, const double *X, const int *reg
     s->t_overlap = calloc((size_t)s->slots * 3 * U, sizeof(double));
     s->t_overlap_old = calloc((size_t)s->slots * 3 * U, sizeof(double));
     copy_to_tnn(s, 1);
+    if (cfg->op == 1 && (cfg->solver == 2 || cfg->coarse_solver == 1 || face_setup(s) != 0)) {
+        orc_free(s);
+        return NULL;
+    }
     return s;
 }
 
@@ -754,6 +1041,7 @@ void orc_free(orc_state *s) {
     for (int l = 0; l < s->c.levels; ++l) {
         free(s->tnew[l]); free(s->told[l]); free(s->rhs[l]); free(s->res[l]); free(s->source[l]);
         free(s->detwei[l]); free(s->nx[l]);
+        free(s->fnb[l]); free(s->fw[l]); free(s->fsx[l]);
     }
     free(s->tnn); free(s->t_overlap); free(s->t_overlap_old); free(s->src_override);
     free(s->X); free(s->region); free(s->neig); free(s->fneig); free(s->dir);
@@ -869,6 +1157,10 @@ void orc_vcycle(orc_state *s) {
 
 /* res_l = RHS_l - A_l tnew_l (get_residual's products, :725-873, with the b - A x sign) */
 static void residual_corrected(orc_state *s, int l) {
+    if (s->c.op == 1) {
+        face_residual(s, l, 1);
+        return;
+    }
     int nsub = s->nsub[l - 1];
     double rdt = 1 / s->c.dt;
     double *T = s->tnew[l - 1], *To = s->told[l - 1], *R = s->rhs[l - 1];
@@ -919,7 +1211,7 @@ void orc_vcycle_corrected(orc_state *s) {
         residual_corrected(s, l);
         restrictor(s, l);
     }
-    memset(s->tnew[L - 1], 0, lvl_len(s, L) * sizeof(double));
+    if (L > 1) memset(s->tnew[L - 1], 0, lvl_len(s, L) * sizeof(double));   /* a coarse level starts from zero */
     if (L == 1) {
         smooth_to_tnew(s, 1, 1);
         residual_corrected(s, 1);

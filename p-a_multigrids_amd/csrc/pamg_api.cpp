@@ -346,6 +346,21 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
     const double rdt = 1 / h->p.dt;
     const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
     const double bytes = 96.0 * (double)L.N + 168.0 * h->U;
+    if (h->p.op == 1) {   // face-coupled operator: the halo is read, so it is refreshed (and exchanged) every sweep
+        if (src_is_T) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
+        for (int s = 0; s < sweeps; ++s) {
+            HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, true));   // tnew := tnew_nonlin (:550), :555
+            CHK(halo(h, l));
+            Span sp(h, kid, bytes + 72.0 * (double)L.N);
+            if (h->p.solver == 3) {   // red-black Gauss-Seidel: up sub-elements, then down ones
+                HIPCHK(h, launch_face_sweep(h->stream, L, h->tov, 0, l == 1, rdt, h->p.omega, h->slots));
+                HIPCHK(h, launch_face_sweep(h->stream, L, h->tov, 1, l == 1, rdt, h->p.omega, h->slots));
+            } else {
+                HIPCHK(h, launch_face_sweep(h->stream, L, h->tov, 2, l == 1, rdt, h->p.omega, h->slots));
+            }
+        }
+        return PAMG_OK;
+    }
     if (h->p.halo_mode == 1) {
         for (int s = 0; s < sweeps; ++s) {
             {
@@ -393,7 +408,7 @@ int refresh_told_halo(pamg_handle *h, int l) {
 int restrict_residual(pamg_handle *h, int l) {
     Level &L = h->lv[l];
     h->rhsn_valid = false;
-    if (l >= h->p.multi_levels) {
+    if (l >= h->p.multi_levels || h->p.op == 1) {
         CHK(restrict_(h, l));
         return residual(h, l);
     }
@@ -403,8 +418,21 @@ int restrict_residual(pamg_handle *h, int l) {
     return PAMG_OK;
 }
 
+// face-coupled operator: residual A tnew - RHS (neg: RHS - A tnew) with the halo refreshed from tnew
+int face_residual(pamg_handle *h, int l, bool neg) {
+    Level &L = h->lv[l];
+    h->rhsn_valid = false;
+    h->overlap_static_l1 = false;
+    HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, false));
+    CHK(halo(h, l));
+    Span sp(h, PAMG_K_RESIDUAL, 144.0 * (double)L.N + 168.0 * h->U);
+    HIPCHK(h, launch_face_residual(h->stream, L, h->tov, neg, l == 1, 1 / h->p.dt, h->slots));
+    return PAMG_OK;
+}
+
 int residual(pamg_handle *h, int l) {
     Level &L = h->lv[l];
+    if (h->p.op == 1) return face_residual(h, l, false);
     h->rhsn_valid = false;
     if (l == 1 && h->p.solver == 2) CHK(rhs_level1(h, 0));   // get_RHS inside get_residual (:865-867)
     Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)L.N + 168.0 * h->U);
@@ -516,6 +544,7 @@ int smooth_to_tnew(pamg_handle *h, int l, int sweeps) {
 }
 
 int residual_corrected(pamg_handle *h, int l) {
+    if (h->p.op == 1) return face_residual(h, l, true);
     h->rhsn_valid = false;
     Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)h->lv[l].N + 168.0 * h->U);
     HIPCHK(h, launch_residual(h->stream, h->lv[l], 1 / h->p.dt, true));
@@ -532,7 +561,7 @@ int vcycle_corrected(pamg_handle *h) {
         CHK(restrict_(h, l));
     }
     Level &C = h->lv[L];
-    HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));
+    if (L > 1) HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));   // a coarse level starts from zero
     if (L == 1) {
         CHK(smooth_to_tnew(h, 1, ns));
         CHK(residual_corrected(h, 1));
@@ -747,6 +776,7 @@ void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
         Level &L = h->lv[l];
         dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.d_pos); dev_free(L.blocks);
+        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
         dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
@@ -788,7 +818,8 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
         p->theta != 1.0 || (p->halo_mode != 0 && p->halo_mode != 1) ||
         (p->coarse_solver != 0 && p->coarse_solver != 1) || p->fused < 0 || p->fused > 3 ||
         (p->arith != 0 && p->arith != 1) || (p->halo_exchange != 0 && p->halo_exchange != 1) ||
-        (p->cycle != 0 && p->cycle != 1) || (p->cycle == 1 && p->solver == 2))
+        (p->cycle != 0 && p->cycle != 1) || (p->cycle == 1 && p->solver == 2) || (p->op != 0 && p->op != 1) ||
+        (p->op == 1 && (p->solver == 2 || p->coarse_solver == 1)))
         return PAMG_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PAMG_ERR_NODEV;
@@ -976,6 +1007,15 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         CHK(dev_upload(h, &L.d_pos, L.pos));
         if (l == 1) HIPCHK(h, launch_source(h->stream, L, h->geo1, h->p.k));   // s' of get_RHS, once
         CHK(build_halo(h, l, X, neig, fneig, dir));
+        if (h->p.op == 1) {
+            std::vector<int4> fnb;
+            std::vector<double> fface;
+            std::vector<int> fsx;
+            CHK(build_face(h, l, X, neig, fneig, dir, fnb, fface, fsx));
+            CHK(dev_upload(h, &L.fnb, fnb));
+            CHK(dev_upload(h, &L.fface, fface));
+            CHK(dev_upload(h, &L.fsx, fsx));
+        }
         HaloPlan &P = L.halo;
         CHK(dev_upload(h, &P.d_local, P.local));
         CHK(dev_upload(h, &P.d_bc, P.bc));
@@ -1149,7 +1189,7 @@ int vcycle(pamg_handle *h, int n, bool dead_after) {
         for (int c = 0; c < n; ++c) CHK(vcycle_corrected(h));
         return PAMG_OK;
     }
-    if (h->p.fused && h->p.coarse_solver == 0 &&
+    if (h->p.fused && h->p.coarse_solver == 0 && h->p.op == 0 &&
         vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth))
         return vcycle_fused(h, n, dead_after);
     for (int c = 0; c < n; ++c) CHK(vcycle_steps(h));
@@ -1197,7 +1237,7 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
     if (!h || ntime < 0 || n_multigrid < 0) return PAMG_ERR_ARG;
     for (int t = 0; t < ntime; ++t) {
         const int L = h->p.multi_levels;
-        const bool fused_next = n_multigrid > 0 && h->p.cycle == 0 && h->p.fused && h->p.coarse_solver == 0 &&
+        const bool fused_next = n_multigrid > 0 && h->p.cycle == 0 && h->p.fused && h->p.coarse_solver == 0 && h->p.op == 0 &&
                                 vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth);
         // told := tnew and the RHS inside the step's first level-1 launch when that launch is a
         // pipelined one on the one-stream schedule

@@ -1,0 +1,158 @@
+// The face-coupled operator (pamg_params.op = 1) on gfx950.
+//
+// A x of a sub-element adds to the reference's element operator (1/dt) M x + Kd x the
+// interior-penalty diffusion surface terms its smoother and residual leave commented out
+// (transport_tri_semi.F90:619-688, :789-857; add_diffusion_surf, matrices.F90:66-117): per face
+// f with nodes (a, b) and the neighbour's values (ya, yb) at those nodes,
+//   ds_a += w_f ((2 x_a + x_b) - 2 ya - yb),  ds_b += w_f ((x_a + 2 x_b) - ya - 2 yb),
+//   w_f = k / delta_x |e_f| / 6 (the P1 edge mass matrix), D_a += 2 w_f (get_diagonal's surface
+// term, :481-486). Inner neighbours are read from the level's field; across an un_ele face the
+// values come from t_overlap, the halo update_overlaps writes at the start of every sweep (:555)
+// -- with several ranks, after the exchange: the first consumer of the halo. A sweep is
+// red-black Gauss-Seidel on the up / down sub-elements (solver 3: every inner neighbour of an up
+// sub-element is a down one) or Jacobi (solver 1). The operation order is the oracle's
+// (oracle/pamg_oracle.c face_terms / face_sweep), so the results are bitwise its own; these
+// kernels gather neighbours and stay off the fused V-cycle (per-step kernels only).
+#include <hip/hip_runtime.h>
+
+#include "pamg_device.h"
+#include "pamg_internal.h"
+
+namespace pamg {
+namespace {
+
+using namespace detail;
+
+__constant__ int cFNode[3][2] = {{0, 2}, {2, 1}, {1, 0}};   // face_nodes, 0-based (:142-147)
+__constant__ int cFMface[3] = {1, 3, 2};                     // the un_ele face under sub-element face f
+
+// halo words of level L from its tnew, the sweep start: copy = tnew := tnew_nonlin first (:550)
+__global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *__restrict__ TNN, int64_t pitch,
+                                                      int64_t npairs, int nsub_log2, HaloArgs H, int copy) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= npairs) return;
+    const int64_t s = 2 * p;
+    double2 v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        v[c] = ld2((copy ? TNN : T) + c * pitch + s);
+        if (copy) st2(T + c * pitch + s, v[c]);
+    }
+    HaloPre hp;
+    halo_prefetch(H, s, s >> nsub_log2, nsub_log2, hp);
+    const double p0[3] = {v[0].x, v[1].x, v[2].x}, p1[3] = {v[0].y, v[1].y, v[2].y};
+    halo_write(H, hp, p0, p1);
+}
+
+// MODE 0 / 1: one colour of a red-black sweep (up / down sub-elements), X = OUT = tnew_nonlin;
+// MODE 2: a Jacobi sweep, X = tnew, OUT = tnew_nonlin; MODE 3 / 4: residual A X - RHS / RHS - A X
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, const double *__restrict__ RHS,
+                                                 const double *__restrict__ stc, const int4 *__restrict__ fnb,
+                                                 const double *__restrict__ fface, const int *__restrict__ fsx,
+                                                 const double *__restrict__ tov, int64_t pitch, int64_t N,
+                                                 int nsub_log2, int slots, int level1, double rdt, double omega) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= N) return;
+    const int64_t u = s >> nsub_log2, base = u << nsub_log2;
+    const int4 nb = fnb[s & ((1ll << nsub_log2) - 1)];
+    if ((MODE == 0 && !nb.w) || (MODE == 1 && nb.w)) return;
+    double x[3], b[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        x[c] = X[c * pitch + s];
+        b[c] = RHS[c * pitch + s];
+    }
+    Stc S;
+    load_stc(stc + u * kStcStride, S);
+    double A[3];
+    apply_A(S, rdt, x, A);
+    const double *w = fface + u * kFaceStride;
+    double ds[3] = {0.0, 0.0, 0.0}, D[3] = {w[6], w[7], w[8]};
+    const int nbf[3] = {nb.x, nb.y, nb.z};
+#pragma unroll
+    for (int fi = 0; fi < 3; ++fi) {
+        const int a = cFNode[fi][0], bb = cFNode[fi][1];
+        double ya, yb, wf;
+        if (nbf[fi] >= 0) {   // inner neighbour: its nodes at my face nodes a, b are its b, a
+            const int64_t o = base + nbf[fi];
+            ya = X[bb * pitch + o];
+            yb = X[a * pitch + o];
+            wf = w[fi];
+        } else {              // across the un_ele face: the halo (t_overlap slot sp)
+            const int mface = cFMface[fi], sx = fsx[4 * u + mface - 1];
+            if (!level1 && (sx & 16)) {
+                ya = 0.0;     // coarse levels carry the error equation: homogeneous boundary data
+                yb = 0.0;
+            } else {
+                const double *slot = tov + u * slots * 3 + (int64_t)(mface - 1) * slots + (int64_t)(-nbf[fi] - 1) * 3;
+                ya = slot[(sx & 3) - 1];
+                yb = slot[((sx >> 2) & 3) - 1];
+            }
+            wf = w[3 + mface - 1];
+        }
+        ds[a] = ds[a] + wf * (((2.0 * x[a] + x[bb]) - 2.0 * ya) - yb);
+        ds[bb] = ds[bb] + wf * (((x[a] + 2.0 * x[bb]) - ya) - 2.0 * yb);
+        D[a] = D[a] + 2.0 * wf;
+        D[bb] = D[bb] + 2.0 * wf;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double ai = A[i] + ds[i];
+        double r;
+        if (MODE <= 2) r = x[i] + omega / D[i] * (b[i] - ai);
+        else if (MODE == 3) r = ai - b[i];
+        else r = b[i] - ai;
+        OUT[i * pitch + s] = r;
+    }
+}
+
+inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+inline int log2i(int v) { int r = 0; while ((1 << r) < v) ++r; return r; }
+
+}  // namespace
+
+hipError_t launch_face_halo(hipStream_t s, const Level &L, double *tov, double *tovo, bool copy) {
+    const int64_t npairs = L.N / 2;
+    if (npairs == 0) return hipSuccess;
+    const HaloPlan &P = L.halo;
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << L.isplit};
+    hipLaunchKernelGGL(k_face_halo, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.TNN, L.pitch, npairs,
+                       log2i(L.nsub), H, copy ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, int mode, bool level1, double rdt,
+                             double omega, int slots) {
+    if (L.N == 0) return hipSuccess;
+    if (!L.fnb || !L.fface || !L.fsx) return hipErrorInvalidValue;
+    const dim3 g(grid_for(L.N)), b(kBlock);
+    const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0;
+    switch (mode) {
+        case 0: hipLaunchKernelGGL(k_face<0>, g, b, 0, s, L.TNN, L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch,
+                                   L.N, lg, slots, l1, rdt, omega); break;
+        case 1: hipLaunchKernelGGL(k_face<1>, g, b, 0, s, L.TNN, L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch,
+                                   L.N, lg, slots, l1, rdt, omega); break;
+        case 2: hipLaunchKernelGGL(k_face<2>, g, b, 0, s, L.T, L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch,
+                                   L.N, lg, slots, l1, rdt, omega); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov, bool neg, bool level1, double rdt,
+                                int slots) {
+    if (L.N == 0) return hipSuccess;
+    if (!L.fnb || !L.fface || !L.fsx) return hipErrorInvalidValue;
+    const dim3 g(grid_for(L.N)), b(kBlock);
+    const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0;
+    if (neg)
+        hipLaunchKernelGGL(k_face<4>, g, b, 0, s, L.T, L.RES, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch, L.N, lg,
+                           slots, l1, rdt, 0.0);
+    else
+        hipLaunchKernelGGL(k_face<3>, g, b, 0, s, L.T, L.RES, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch, L.N, lg,
+                           slots, l1, rdt, 0.0);
+    return hipGetLastError();
+}
+
+}  // namespace pamg

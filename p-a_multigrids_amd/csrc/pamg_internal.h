@@ -97,6 +97,13 @@ struct Level {
     // for the (3, nsub, U) boundary layout converters.
     std::vector<int> pos;
     int *d_pos = nullptr;
+    // face-coupled operator (pamg_params.op = 1): per storage position fnb = {the
+    // neighbour's position across faces 1..3, or -sp (position along the un_ele face), up flag};
+    // per local un_ele fface = {w_in[3], w_b[3], D0[3], pad} (kFaceStride doubles) and fsx[4] =
+    // per un_ele face: S(F1) | S(F2) << 2 | domain boundary << 4
+    int4 *fnb = nullptr;
+    double *fface = nullptr;
+    int *fsx = nullptr;
     double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
     int arith = 0;                    // operator arithmetic of this level's kernels (pamg_params.arith)
@@ -177,10 +184,15 @@ void loc_surf_ele(int n, std::vector<int> &surf);
 void get_splitting(const double *un_x, int n_split, int str_ele, double str_x[3][2]);
 // storage positions of every level (see Level::pos): levels 1..L of a split n_split
 void hier_positions(int n_split, int L, std::vector<int> pos[]);
-void level_stencil(const double *X, int i_split, double k, double dt, double omega, double *rec);
+// D0 (optional, 3): get_diagonal's rdt ml_i + Kd_ii + 0.0 (:481-486)
+void level_stencil(const double *X, int i_split, double k, double dt, double omega, double *rec, double *D0 = nullptr);
 // M == c [[2,1,1],[1,2,1],[1,1,2]] bit for bit (the form the smoother kernels evaluate)
 bool mass_is_p1_midpoint(const double *rec);
 int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const int *fneig, const int *dir);
+// face-coupled operator tables of level l (Level::fnb / fface / fsx, host copies returned)
+constexpr int kFaceStride = 12;
+int build_face(pamg_handle *h, int l, const double *Xg, const int *neig, const int *fneig, const int *dir,
+               std::vector<int4> &fnb, std::vector<double> &fface, std::vector<int> &fsx);
 }  // namespace pamg
 
 // ---- kernels (pamg_kernels.hip) ----
@@ -243,6 +255,15 @@ hipError_t launch_block_ops(hipStream_t s, const Level &L, int U, double rdt, do
 hipError_t launch_block_solve(hipStream_t s, const Level &L, const double *Ainv);
 hipError_t launch_to_aos(hipStream_t s, const Level &L, const double *soa, double *aos);
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt);
+// face-coupled operator (pamg_face.hip): the halo words of level L from its tnew (copy: tnew :=
+// tnew_nonlin first, the sweep start :550); one sweep (mode 0 up sub-elements, 1 down ones --
+// red-black Gauss-Seidel in place on tnew_nonlin -- 2 Jacobi from tnew); the residual A tnew - RHS
+// (neg: RHS - A tnew); level1: the domain-boundary values enter (coarse levels: zero)
+hipError_t launch_face_halo(hipStream_t s, const Level &L, double *tov, double *tovo, bool copy);
+hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, int mode, bool level1, double rdt,
+                             double omega, int slots);
+hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov, bool neg, bool level1, double rdt,
+                                int slots);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg

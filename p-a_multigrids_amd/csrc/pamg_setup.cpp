@@ -5,8 +5,10 @@
 // reference's operation order (see oracle/pamg_oracle.c for the literal
 // restatement these mirror); the device kernels then reproduce the
 // reference's arithmetic bit for bit except the sine of the source term.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "pamg_internal.h"
@@ -109,7 +111,7 @@ void hier_positions(int n_split, int L, std::vector<int> pos[]) {
 // (ShapFun_unstruc.F90:304-335), the diff_vol1 reduction (transport_tri_semi.F90:602-606)
 // and get_diagonal (:481-486). The quadrature is TRIQUAold's ngi=3 edge-midpoint rule
 // (ShapFun.F90:554-563) with SHATRIold's P1 functions (:1036-1048).
-void level_stencil(const double *X, int i_split, double k, double dt, double omega, double *rec) {
+void level_stencil(const double *X, int i_split, double k, double dt, double omega, double *rec, double *D0) {
     static const double N[3][3] = {{0.5, 0.5, 0.0}, {0.0, 0.5, 0.5}, {0.5, 0.0, 0.5}};
     static const double NLX[2][3] = {{1.0, 0.0, -1.0}, {0.0, 1.0, -1.0}};
     const double weight = 1.0 / 3.0;
@@ -163,6 +165,7 @@ void level_stencil(const double *X, int i_split, double k, double dt, double ome
         }
         double D = rdt * ml[i] + Kd[i][i] + 0.0;
         rec[kStcW + i] = omega / D;
+        if (D0) D0[i] = D;
         for (int j = 0; j < 3; ++j) rec[kStcA + 3 * i + j] = rdt * M[i][j] + Kd[i][j];
     }
     rec[kStcC] = M[0][1];
@@ -325,6 +328,149 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
     }
     // the device's surf table (k_told_halo, k_overlap_static) holds storage positions, 1-based
     for (int &v : surf) v = spos(v) + 1;
+    return PAMG_OK;
+}
+
+
+// ---- the face-coupled operator (pamg_params.op = 1; oracle/pamg_oracle.c face_setup
+// is the restatement these tables follow, operation for operation)
+namespace {
+const int kFNode[3][2] = {{1, 3}, {3, 2}, {2, 1}};   // face_nodes (transport_tri_semi.F90:142-147)
+const int kFMface[3] = {1, 3, 2};                     // un_ele face of sub-element face f (:626-637)
+
+// splitting.F90:732-776 get_str_neig_multigrid: sn[(f - 1) + 3 (e - 1)]
+void get_str_neig(int n, std::vector<int> &sn) {
+    int total = (1 << (n + 1)) - 1, current = total, irow = (1 << n) - 1, ele;
+    sn.assign(3 * ((size_t)1 << (2 * n)) + 3, 0);
+    auto SN = [&](int f, int e) -> int & { return sn[(f - 1) + 3 * (size_t)(e - 1)]; };
+    SN(1, 1) = 0; SN(2, 1) = 0; SN(3, 1) = 2;
+    ele = 2;
+    while (ele <= total) {
+        SN(2, ele) = ele + 1; SN(3, ele) = ele - 1; SN(1, ele) = ele + total - 1;
+        ele = ele + 1;
+        SN(2, ele) = ele - 1; SN(1, ele) = 0; SN(3, ele) = ele + 1;
+        ele = ele + 1;
+    }
+    SN(3, ele - 1) = 0;
+    while (irow >= 1) {
+        total = total + current - 2;
+        current = current - 2;
+        SN(2, ele) = 0; SN(3, ele) = ele + 1; SN(1, ele) = ele - current - 1;
+        ele = ele + 1;
+        while (ele <= total) {
+            SN(2, ele) = ele + 1; SN(3, ele) = ele - 1; SN(1, ele) = ele + current - 1;
+            ele = ele + 1;
+            SN(2, ele) = ele - 1; SN(3, ele) = ele + 1; SN(1, ele) = ele - current - 1;
+            ele = ele + 1;
+        }
+        SN(3, ele - 1) = 0;
+        irow = irow - 1;
+    }
+}
+
+double dist2d(const double a[2], const double b[2]) {
+    double dx = a[0] - b[0], dy = a[1] - b[1];
+    return std::sqrt(dx * dx + dy * dy);
+}
+void centroid(double xl[3][2], double c[2]) {
+    for (int d = 0; d < 2; ++d) c[d] = (xl[0][d] + xl[1][d] + xl[2][d]) / 3.0;
+}
+double face_weight(double k, double delta, double len) { return k / delta * len / 6.0; }
+
+// the slot update_overlaps gives the sub-element at position i of face f of un_ele q (splitting.F90:1297-1391)
+int overlap_kslot(int is, const std::vector<int> &surf, int f, int i, int nside, int dr) {
+    const int m = 1 << is;
+    int irow, ipos, orient, fwd, rev;
+    get_str_info(is, surf[(i - 1) + (f - 1) * m], &irow, &ipos, &orient);
+    if (f == 1) { fwd = ipos / 2 + 1; rev = m - (ipos / 2 + 1) + 1; }
+    else { fwd = irow; rev = m - irow + 1; }
+    if (f == 2) std::swap(fwd, rev);
+    return (nside == 2) ? (dr ? rev : fwd) : (dr ? fwd : rev);
+}
+}  // namespace
+
+int build_face(pamg_handle *h, int l, const double *Xg, const int *neig, const int *fneig, const int *dir,
+               std::vector<int4> &fnb, std::vector<double> &fface, std::vector<int> &fsx) {
+    Level &L = h->lv[l];
+    const int is = L.isplit, nsub = L.nsub, m = 1 << is;
+    std::vector<int> sn, surf;
+    get_str_neig(is, sn);
+    loc_surf_ele(is, surf);
+    fnb.assign(nsub, make_int4(0, 0, 0, 0));
+    for (int e = 1; e <= nsub; ++e) {
+        int irow, ipos, orient, v[3];
+        get_str_info(is, e, &irow, &ipos, &orient);
+        for (int f = 1; f <= 3; ++f) {
+            const int nb = sn[(f - 1) + 3 * (size_t)(e - 1)];
+            v[f - 1] = nb ? L.pos[nb - 1] : -((f == 1) ? ipos / 2 + 1 : irow);
+        }
+        fnb[L.pos[e - 1]] = make_int4(v[0], v[1], v[2], ipos % 2);
+    }
+    fface.assign((size_t)std::max(h->U, 1) * kFaceStride, 0.0);
+    fsx.assign((size_t)std::max(h->U, 1) * 4, 0);
+    for (int q = 0; q < h->U; ++q) {
+        const int ug = h->owned.empty() ? q : h->owned[q];
+        const double *X = Xg + 6 * (size_t)ug;
+        double *w = &fface[(size_t)q * kFaceStride];
+        for (int f = 1; f <= 3; ++f)   // inner faces: the first up sub-element with a neighbour across f
+            for (int e = 1; e <= nsub; ++e) {
+                int irow, ipos, orient;
+                const int nb = sn[(f - 1) + 3 * (size_t)(e - 1)];
+                get_str_info(is, e, &irow, &ipos, &orient);
+                if (!(ipos % 2) || !nb) continue;
+                double xe[3][2], xn[3][2], ce[2], cn[2];
+                get_splitting(X, is, e, xe);
+                get_splitting(X, is, nb, xn);
+                centroid(xe, ce);
+                centroid(xn, cn);
+                w[f - 1] = face_weight(h->p.k, dist2d(ce, cn), dist2d(xe[kFNode[f - 1][0] - 1], xe[kFNode[f - 1][1] - 1]));
+                break;
+            }
+        for (int fi = 0; fi < 3; ++fi) {   // un_ele faces, from the boundary sub-element at sp = 1
+            const int mface = kFMface[fi], se = surf[0 + (mface - 1) * m];
+            const int a = kFNode[fi][0], b = kFNode[fi][1];
+            double xe[3][2], ce[2];
+            get_splitting(X, is, se, xe);
+            centroid(xe, ce);
+            const double len = dist2d(xe[a - 1], xe[b - 1]);
+            const int npos = neig[3 * (size_t)ug + mface - 1];
+            if (npos == 0) {
+                const double mid[2] = {(xe[a - 1][0] + xe[b - 1][0]) / 2.0, (xe[a - 1][1] + xe[b - 1][1]) / 2.0};
+                w[3 + mface - 1] = face_weight(h->p.k, dist2d(ce, mid), len);
+                fsx[4 * (size_t)q + mface - 1] = a | (b << 2) | (1 << 4);
+                continue;
+            }
+            const int nq = npos - 1, nside = fneig[3 * (size_t)ug + mface - 1];
+            bool found = false;
+            for (int i = 1; i <= m && !found; ++i) {
+                if (overlap_kslot(is, surf, nside, i, fneig[3 * (size_t)nq + nside - 1], dir[3 * (size_t)nq + nside - 1]) != 1)
+                    continue;
+                double xn[3][2], cn[2];
+                get_splitting(Xg + 6 * (size_t)nq, is, surf[(i - 1) + (nside - 1) * m], xn);
+                centroid(xn, cn);
+                int S[2] = {0, 0};
+                for (int t = 0; t < 2; ++t) {
+                    const double *p = xe[(t ? b : a) - 1];
+                    double best = 1e300;
+                    for (int r = 0; r < 3; ++r) {
+                        const double d = dist2d(p, xn[r]);
+                        if (d < best) { best = d; S[t] = r + 1; }
+                    }
+                    if (best > 1e-9 * len) {
+                        h->err = "face operator: the halo slot of un_ele " + std::to_string(ug + 1) + " face " +
+                                 std::to_string(mface) + " holds no sub-element sharing that face";
+                        return PAMG_ERR_STATE;
+                    }
+                }
+                w[3 + mface - 1] = face_weight(h->p.k, dist2d(ce, cn), len);
+                fsx[4 * (size_t)q + mface - 1] = S[0] | (S[1] << 2);
+                found = true;
+            }
+            if (!found) { h->err = "face operator: no halo slot 1 on a neighbour's face"; return PAMG_ERR_STATE; }
+        }
+        double rec[kStcStride];
+        level_stencil(X, is, h->p.k, h->p.dt, h->p.omega, rec, w + 6);   // D0 = rdt ml + Kd_ii + 0.0
+    }
     return PAMG_OK;
 }
 

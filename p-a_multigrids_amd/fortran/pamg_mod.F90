@@ -23,7 +23,8 @@ module pamg
     integer(c_int) :: arith
     integer(c_int) :: halo_exchange
     integer(c_int) :: cycle
-    integer(c_int) :: reserved(2)
+    integer(c_int) :: op
+    integer(c_int) :: reserved(1)
   end type pamg_params
 
   public :: pamg_default_params, pamg_msh_read, pamg_msh_size, pamg_msh_get, pamg_msh_free

@@ -29,7 +29,7 @@ class PamgParams(C.Structure):
                 ("n_coarse", C.c_int), ("solver", C.c_int), ("device", C.c_int),
                 ("dt", C.c_double), ("k", C.c_double), ("omega", C.c_double), ("theta", C.c_double),
                 ("halo_mode", C.c_int), ("fused", C.c_int), ("coarse_solver", C.c_int), ("arith", C.c_int),
-                ("halo_exchange", C.c_int), ("cycle", C.c_int), ("reserved", C.c_int * 2)]
+                ("halo_exchange", C.c_int), ("cycle", C.c_int), ("op", C.c_int), ("reserved", C.c_int * 1)]
 
 
 class PamgError(RuntimeError):

@@ -112,13 +112,13 @@ class SemiImplicitIterative:
 
     def __init__(self, mesh, n_split, multi_levels, n_smooth=4, solver=3, n_coarse=15, device=0,
                  dt=1.0 * 0.0000125, k=1.0, omega=0.8, halo_mode=0, comm=None, fused=3, coarse_solver=0,
-                 arith=0, halo_exchange=0, cycle=0):
+                 arith=0, halo_exchange=0, cycle=0, op=0):
         self.L = lib()
         self.mesh = mesh
         self.params = default_params(n_split=n_split, multi_levels=multi_levels, n_smooth=n_smooth,
                                      solver=solver, n_coarse=n_coarse, device=device, dt=dt, k=k,
                                      omega=omega, halo_mode=halo_mode, fused=fused, coarse_solver=coarse_solver,
-                                     arith=arith, halo_exchange=halo_exchange, cycle=cycle)
+                                     arith=arith, halo_exchange=halo_exchange, cycle=cycle, op=op)
         h = C.c_void_p()
         _check("pamg_create", self.L.pamg_create(C.byref(self.params), C.byref(h)))
         self.h = h

@@ -38,6 +38,11 @@ for mesh, S, L, n in CASES:
         row.append(f"res/max|RHS_{l}| {float(np.abs(a[f'res_L{l}'] - b[f'res_L{l}']).max()) / amax(f'RHS_L{l}'):8.1e}")
         if l >= 2:
             row.append(f"RHS/max|RHS_{l - 1}| {float(np.abs(a[f'RHS_L{l}'] - b[f'RHS_L{l}']).max()) / amax(f'RHS_L{l - 1}'):8.1e}")
+        # the bound of tests/test_gpu_parity.py check_contracted: 1e-12 of the level-1 scales
+        e_res = float(np.abs(a[f"res_L{l}"] - b[f"res_L{l}"]).max()) / amax("RHS_L1")
+        e_rhs = float(np.abs(a[f"RHS_L{l}"] - b[f"RHS_L{l}"]).max()) / amax("RHS_L1")
+        e_t = float(np.abs(a[f"tnew_L{l}"] - b[f"tnew_L{l}"]).max()) / amax("tnew_L1")
+        row.append(f"[res, RHS]/max|RHS_1| {e_res:8.1e} {e_rhs:8.1e}, tnew/max|tnew_1| {e_t:8.1e}")
         print(", ".join(row), flush=True)
     d = float(np.abs(a["tnew_nonlin"] - b["tnew_nonlin"]).max()) / amax("tnew_nonlin")
     print(f"  tnew_nonlin (level 1) {d:8.1e}", flush=True)

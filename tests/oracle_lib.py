@@ -21,7 +21,8 @@ class OrcCfg(C.Structure):
     _fields_ = [("n_split", C.c_int), ("levels", C.c_int), ("n_smooth", C.c_int),
                 ("n_coarse", C.c_int), ("solver", C.c_int), ("ntime", C.c_int),
                 ("n_multigrid", C.c_int), ("dt", C.c_double), ("k", C.c_double),
-                ("omega", C.c_double), ("theta", C.c_double), ("coarse_solver", C.c_int), ("arith", C.c_int)]
+                ("omega", C.c_double), ("theta", C.c_double), ("coarse_solver", C.c_int), ("op", C.c_int),
+                ("arith", C.c_int)]
 
 
 _lib = None
@@ -90,11 +91,11 @@ def read_msh(path):
 
 class Oracle:
     def __init__(self, mesh, n_split, levels, n_smooth=4, solver=3, ntime=2, n_multigrid=2,
-                 n_coarse=15, dt=1.25e-5, k=1.0, omega=0.8, theta=1.0, coarse_solver=0, arith=0):
+                 n_coarse=15, dt=1.25e-5, k=1.0, omega=0.8, theta=1.0, coarse_solver=0, arith=0, op=0):
         self.L = lib()
         self.mesh = mesh
         self.cfg = OrcCfg(n_split, levels, n_smooth, n_coarse, solver, ntime, n_multigrid, dt, k, omega, theta,
-                          coarse_solver, arith)
+                          coarse_solver, op, arith)
         self.h = self.L.orc_create(C.byref(self.cfg), mesh.U, mesh.X, mesh.region, mesh.neig,
                                    mesh.fneig, mesh.dir)
         if not self.h:

@@ -1,0 +1,133 @@
+"""The face-coupled operator (pamg_params.op = 1).
+
+The reference leaves its surface terms commented out and cannot run them (Mesh%S_nodes is never
+allocated), so there is no reference output: the operator is defined by the oracle's restatement
+(oracle/pamg_oracle.c face_setup / face_terms / face_sweep) and the HIP path is held to it bit
+for bit (the oracle takes the device's source term s', as in tests/test_contracted_oracle.py).
+CPU tests: the restatement is a well-posed operator for multigrid -- the corrected V-cycle
+contracts the level-1 residual cycle after cycle -- and it really couples elements.
+GPU tests: every field of every level and t_overlap equal the oracle's, single domain and on
+partitions, where the halo is now read every sweep (exchanged through the multi-rank path)."""
+import os
+
+import numpy as np
+import pytest
+
+import goldens
+import oracle_lib as O
+
+
+def oracle(mesh, S, L, **kw):
+    return O.Oracle(O.read_msh(os.path.join(goldens.MESHES, mesh)), S, L, op=1, **kw)
+
+
+@pytest.mark.parametrize("mesh,S,L,rate", [("untitled8.msh", 3, 3, 0.3), ("irregular.msh", 3, 3, 0.3),
+                                           ("900_ele.msh", 3, 3, 0.3), ("test_sn2.msh", 4, 3, 0.5)])
+@pytest.mark.parametrize("solver", [1, 3])
+def test_corrected_cycle_converges_with_the_face_operator(mesh, S, L, rate, solver):
+    o = oracle(mesh, S, L, solver=solver, ntime=1, n_multigrid=1)
+    o.begin_timestep()
+    r = []
+    for _ in range(8):
+        o.vcycle_corrected()
+        r.append(float(np.abs(o.get(O.RES, 1)).max()))
+    assert all(np.isfinite(r))
+    assert r[-1] < r[0] * rate ** 6, r
+    assert r[-1] < r[-2] < r[-3], r
+
+
+def test_face_coupling_is_not_block_diagonal():
+    """A sweep of op = 1 differs from op = 0 only through the face terms: with a random iterate
+    the two differ, and they agree again when the neighbours are frozen at the sub-element's own
+    values and k = 0 (no diffusion, no penalty)."""
+    rng = np.random.default_rng(20251015)
+    a = oracle("untitled8.msh", 2, 1, ntime=1, n_multigrid=1)
+    b = O.Oracle(O.read_msh(os.path.join(goldens.MESHES, "untitled8.msh")), 2, 1, ntime=1, n_multigrid=1)
+    x = rng.uniform(-1, 1, (3, a.nsub(1), 8))
+    for o in (a, b):
+        o.set(O.TNEW, 1, x)
+        o.begin_timestep()
+        o.copy_to_tnn(1)
+        o.smoother(1)
+    assert np.abs(a.get(O.TNN, 1) - b.get(O.TNN, 1)).max() > 1e-6
+    a0 = oracle("untitled8.msh", 2, 1, ntime=1, n_multigrid=1, k=0.0)
+    b0 = O.Oracle(O.read_msh(os.path.join(goldens.MESHES, "untitled8.msh")), 2, 1, ntime=1, n_multigrid=1, k=0.0)
+    for o in (a0, b0):
+        o.set(O.TNEW, 1, x)
+        o.begin_timestep()
+        o.copy_to_tnn(1)
+        o.smoother(1)
+    np.testing.assert_array_equal(a0.get(O.TNN, 1), b0.get(O.TNN, 1))
+
+
+def test_face_operator_rejects_unsupported_configs():
+    m = O.read_msh(os.path.join(goldens.MESHES, "untitled8.msh"))
+    for kw in (dict(solver=2), dict(coarse_solver=1)):
+        with pytest.raises(ValueError):
+            O.Oracle(m, 2, 2, op=1, **kw)
+
+
+# ---------------------------------------------------------------- GPU parity
+def gpu_pair(mesh, S, L, solver=3, cycle=0, ns=4):
+    import pamg
+    path = os.path.join(goldens.MESHES, mesh)
+    g = pamg.SemiImplicitIterative(pamg.Mesh.read(path), S, L, n_smooth=ns, solver=solver, cycle=cycle, op=1)
+    o = oracle(mesh, S, L, n_smooth=ns, solver=solver)
+    o.set_source(g.get(pamg.SOURCE, 1))
+    return g, o
+
+
+def drive(s, is_oracle, cycle, steps=2, cycles=2):
+    for _ in range(steps):
+        s.begin_timestep()
+        for _ in range(cycles):
+            if is_oracle:
+                s.vcycle_corrected() if cycle else s.vcycle()
+        if not is_oracle:
+            s.vcycle(cycles)
+
+
+def assert_identical(sg, so):
+    for k in so:
+        np.testing.assert_array_equal(sg[k], so[k], err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,solver,ns", [
+    ("untitled8.msh", 3, 3, 3, 4), ("untitled8.msh", 3, 3, 1, 2), ("irregular.msh", 4, 3, 3, 2),
+    ("900_ele.msh", 3, 2, 3, 3), ("test_sn2.msh", 4, 2, 1, 1), ("untitled8192.msh", 3, 3, 3, 4)])
+@pytest.mark.parametrize("cycle", [0, 1])
+def test_face_operator_is_bitwise_the_oracle(mesh, S, L, solver, ns, cycle):
+    g, o = gpu_pair(mesh, S, L, solver, cycle, ns)
+    drive(g, False, cycle)
+    drive(o, True, cycle)
+    sg, so = g.state(), o.state()
+    sg["t_overlap"], sg["t_overlap_old"] = g.overlap()
+    so["t_overlap"], so["t_overlap_old"] = o.overlap()
+    assert_identical(sg, so)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,parts,kind,solver,cycle", [
+    ("untitled8192.msh", 3, 3, 4, "strip", 3, 0), ("untitled8192.msh", 3, 2, 8, "strip", 3, 1),
+    ("irregular.msh", 4, 2, 8, "strip", 1, 1), ("900_ele.msh", 2, 2, 3, "block", 3, 0)])
+def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, solver, cycle):
+    """The halo is consumed every sweep: the partitions' exchanges (the multi-rank path with the
+    device-copy transport, tests/test_multirank.py) carry the values the sweeps read."""
+    import pamg
+    from pamg.solver import local_group, run_ranks
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    full = pamg.SemiImplicitIterative(m, S, L, solver=solver, cycle=cycle, op=1)
+    drive(full, False, cycle)
+    owner = m.x_strip_owner(parts) if kind == "strip" else m.block_owner(parts)
+    ps = [pamg.SemiImplicitIterative(m, S, L, solver=solver, cycle=cycle, op=1, comm=(parts, r, None, owner))
+          for r in range(parts)]
+    local_group(ps)
+    run_ranks(ps, lambda p: drive(p, False, cycle))
+    ref, ref_ov = full.state(), full.overlap()
+    for r, p in enumerate(ps):
+        own = np.flatnonzero(owner == r)
+        for k, v in p.state().items():
+            np.testing.assert_array_equal(v, ref[k][:, :, own], err_msg=f"rank {r} {k}")
+        for x, y in zip(p.overlap(), ref_ov):
+            np.testing.assert_array_equal(x, y[:, :, own])

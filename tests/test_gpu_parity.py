@@ -292,33 +292,39 @@ def test_fused_vcycle_interleaved_with_call_sites_bitwise(mesh, S, L, fused):
 
 
 # ---- contracted operator arithmetic (pamg_params.arith = 1): A_e = (1/dt) M + Kd assembled
-# once per un_ele, one fma chain per row. Same algebra as the reference, different roundings.
-# The solution (level-1 tnew / tnew_nonlin / told / RHS and the halo arrays -- the north
-# star's "solution vector") is held to 1e-12 relative, 100x inside its 1e-10 bar (observed
-# ~1e-15). Residuals are differences of nearly equal terms (A x vs RHS): an fp64 evaluation
-# of res_l in ANY operation order, the reference's included, is only determined to
-# eps * kappa_l with kappa_l = max|RHS_l| / max|res_l|, and the coarse levels inherit that
-# through the restrictor. Residual-derived fields of level l (res_l; RHS_l, tnew_l for l >= 2)
-# are therefore held to 1e-12 * prod_{m <= l} kappa_m, kappa taken from the reference's own
-# output (observed: error / prod kappa ~ 3e-16). With arith = 0 every field is bitwise.
+# once per un_ele, one fma chain per row. Exact parity of that arithmetic is
+# tests/test_contracted_oracle.py (bitwise against the oracle's restatement of it, the bench
+# config included). Here it is held against the reference's operation order, whose roundings
+# differ: the solution (level-1 tnew / tnew_nonlin / told / RHS and the halo arrays -- the north
+# star's "solution vector") to 1e-12 relative, 100x inside its 1e-10 bar (observed ~1e-15). The
+# residual-derived fields (res_l; RHS_l, tnew_l for l >= 2) are differences of nearly equal
+# terms: an fp64 evaluation in ANY operation order, the reference's included, fixes them only to
+# eps times the magnitude of the terms, which is the scale of the level-1 data they come from
+# (RHS_{l+1} is the restriction of res_l = A x_l - RHS_l). They are held to 1e-12 of that
+# scale -- max|RHS_1| for the RHS-unit fields (res, RHS), max|tnew_1| for the solution-unit
+# ones (tnew) -- a bound that does not depend on how far the levels have converged (observed
+# <= 2e-15 of it; on bench.py's workload every level is well conditioned, kappa_l =
+# max|RHS_l| / max|res_l| <= 8, and the same numbers are <= 4e-13 of each level's own RHS scale:
+# profiles/r02_conditioning.txt). With arith = 0 every field is bitwise.
 TOL_CONTRACTED = 1e-12
 SOLUTION = ("tnew_L1", "told_L1", "RHS_L1", "tnew_nonlin", "t_overlap", "t_overlap_old")
 
 
 def check_contracted(st, ref, levels, err_of):
-    kap = 1.0
+    """err_of(k, v) -> max abs difference of field k from the reference's"""
+    rhs1 = float(np.abs(ref("RHS_L1")).max())
+    t1 = float(np.abs(ref("tnew_L1")).max())
     for l in range(1, levels + 1):
-        r, b = ref(f"res_L{l}"), ref(f"RHS_L{l}")
-        if r is not None and b is not None and np.abs(r).max() > 0:
-            kap *= max(1.0, float(np.abs(b).max() / np.abs(r).max()))
-        for k in (f"res_L{l}",) + ((f"RHS_L{l}", f"tnew_L{l}", f"told_L{l}") if l >= 2 else ()):
+        for k, scale in ((f"res_L{l}", rhs1),) + (((f"RHS_L{l}", rhs1), (f"tnew_L{l}", t1), (f"told_L{l}", t1))
+                                                    if l >= 2 else ()):
             if k in st:
                 e = err_of(k, st[k])
-                assert e <= TOL_CONTRACTED * kap, (k, e, kap)
+                assert e <= TOL_CONTRACTED * scale, (k, e, scale)
     for k in SOLUTION:
         if k in st:
+            r = ref(k)
             e = err_of(k, st[k])
-            assert e <= TOL_CONTRACTED, (k, e)
+            assert e <= TOL_CONTRACTED * max(float(np.abs(r).max()), 1e-300), (k, e)
 
 
 def golden_ref(d):
@@ -337,8 +343,10 @@ def test_contracted_time_loop_matches_reference(name):
     if meta["solver"] == 2:
         pytest.skip("Richardson has no operator product (arith applies to solver 1/3)")
 
-    def err_of(k, v):
-        return goldens.rel_err(v, d[k]) if k in d else goldens.compare_sampled(d, k, v)
+    def err_of(k, v):   # max abs difference (sampled fields: on the stored sample)
+        if k in d:
+            return float(np.abs(np.asarray(v) - d[k]).max())
+        return goldens.compare_sampled(d, k, v) * float(np.abs(golden_ref(d)(k)).max())
 
     for fused in (0, 1, 2, 3):
         s = gpu_solver(meta, arith=1, fused=fused)
@@ -361,7 +369,7 @@ def test_contracted_full_size_against_oracle(mesh, S, L):
     so, sg = o.state(), s.state()
     so["t_overlap"], so["t_overlap_old"] = o.overlap()
     sg["t_overlap"], sg["t_overlap_old"] = s.overlap()
-    check_contracted(sg, so.get, L, lambda k, v: goldens.rel_err(v, so[k]))
+    check_contracted(sg, so.get, L, lambda k, v: float(np.abs(np.asarray(v) - so[k]).max()))
 
 
 @pytest.mark.parametrize("mesh,S,L,ns", [("untitled8.msh", 3, 3, 1), ("irregular.msh", 3, 3, 4),
