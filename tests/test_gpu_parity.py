@@ -313,7 +313,10 @@ SOLUTION = ("tnew_L1", "told_L1", "RHS_L1", "tnew_nonlin", "t_overlap", "t_overl
 def check_contracted(st, ref, levels, err_of):
     """err_of(k, v) -> max abs difference of field k from the reference's"""
     rhs1 = float(np.abs(ref("RHS_L1")).max())
-    t1 = float(np.abs(ref("tnew_L1")).max())
+    # the level-1 iterate's scale: tnew_L1, or the last sweep (tnew_nonlin) when tnew is still zero
+    # (n_smooth = 1 keeps the fine tnew at exactly 0, SURVEY.md 8c fact 4)
+    t1 = max(float(np.abs(ref("tnew_L1")).max()),
+             float(np.abs(ref("tnew_nonlin")).max()) if ref("tnew_nonlin") is not None else 0.0)
     for l in range(1, levels + 1):
         for k, scale in ((f"res_L{l}", rhs1),) + (((f"RHS_L{l}", rhs1), (f"tnew_L{l}", t1), (f"told_L{l}", t1))
                                                     if l >= 2 else ()):
