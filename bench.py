@@ -210,6 +210,32 @@ def measure_time_loop(s):
     return out
 
 
+def measure_workload(pamg, m, S, L, ns, arith, device, cycles=100):
+    """V-cycles/s of one pamg_vcycle(cycles) call on mesh m at n_split S (after a warm-up call),
+    and the pipelined launch's roofline from a sampled-event pass"""
+    s = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=3, device=device, arith=arith, fused=3)
+    s.begin_timestep()
+    s.vcycle(cycles)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.vcycle(cycles)
+    s.synchronize()
+    v = cycles / (time.perf_counter() - t0)
+    s.timing_enable(0xF7F)
+    s.timing_stride(EVENT_STRIDE)
+    s.timing_reset()
+    s.vcycle(cycles)
+    s.synchronize()
+    k = s.timing()["vcycle_pipe"]
+    out = dict(U=m.U, n_split=S, fine_sub_elements=m.U * 4 ** S, vcycles_per_s=round(v, 1))
+    if k["launches"]:
+        ms = k["ms"] / k["launches"]
+        out.update(pipe_ms=round(ms, 4), pipe_alg_bytes=k["bytes"] / k["launches"],
+                   pipe_frac=round(k["bytes"] / k["launches"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+    s.close()
+    return out
+
+
 def comm_report(s, world, dist):
     kind, ver, path = s.comm_info()
     mine = {"transport": kind, "rccl_version": ver, "librccl": path}
@@ -368,6 +394,13 @@ def main():
         s3.synchronize()
         extra["nsplit3_vcycles_per_s"] = round(max(a.steps, 200) / (time.perf_counter() - t0), 1)
         s3.close()
+        # the other workloads of the north star on one GPU: config 5's mesh at n_split = 6 (tiles are
+        # quarters of an un_ele there), config 3 at n_split = 6, and a synthetic structured strip
+        # 4x untitled8192 (256 x 64 x 2, pamg_msh_strip) at the benchmarked n_split = 5
+        for tag, m_, S_ in (("irregular_nsplit6", pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "irregular.msh")), 6),
+                            ("untitled8192_nsplit6", mesh, 6),
+                            ("strip256x64_nsplit5", pamg.Mesh.strip(256, 64), 5)):
+            extra[tag] = measure_workload(pamg, m_, S_, a.levels, a.nsmooth, a.arith, device)
     if world > 1 and not a.no_extra:
         # the other exchange mode on the same partition (timed region the same shape): halo words
         # exchanged after every cycle, overlapped with the next one
