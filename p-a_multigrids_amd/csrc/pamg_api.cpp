@@ -80,10 +80,16 @@ int dev_alloc(pamg_handle *h, T **p, size_t count) {
     return PAMG_OK;
 }
 
+// every setup transfer runs on the handle's stream: its streams are non-blocking, so work on
+// them is not ordered against the null stream a blocking hipMemcpy uses (a memset queued on
+// h->stream could land after such a copy)
 template <class T>
 int dev_upload(pamg_handle *h, T **p, const std::vector<T> &v) {
     CHK(dev_alloc(h, p, v.size()));
-    if (!v.empty()) HIPCHK(h, hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    if (!v.empty()) {
+        HIPCHK(h, hipMemcpyAsync(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));   // v may be freed on return
+    }
     return PAMG_OK;
 }
 
@@ -1042,7 +1048,9 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
                 if (region[h->owned[q]] == 4)
                     for (int c = 0; c < 3; ++c)
                         for (int e = 0; e < L1.nsub; ++e) t[c * L1.pitch + (size_t)q * L1.nsub + e] = 1.0;
-            HIPCHK(h, hipMemcpy(L1.T, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+            // behind the memset of the level's planes on the same stream
+            HIPCHK(h, hipMemcpyAsync(L1.T, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
         }
         HIPCHK(h, launch_copy(h->stream, L1.T, L1.TNN, 3 * L1.pitch));
         h->tnn_level = 1;

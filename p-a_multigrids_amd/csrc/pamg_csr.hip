@@ -77,8 +77,9 @@ int pamg_csr_create(pamg_handle *h, long nrows, long nnz, const int *g_jloc, con
     hipError_t e;
     if ((e = hipSetDevice(h->device)) != hipSuccess || (e = hipMalloc(&m->jloc, used * sizeof(int))) != hipSuccess ||
         (e = hipMalloc(&m->val, used * sizeof(double))) != hipSuccess ||
-        (e = hipMemcpy(m->jloc, g_jloc, used * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(m->val, val, used * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess) {
+        (e = hipMemcpyAsync(m->jloc, g_jloc, used * sizeof(int), hipMemcpyHostToDevice, h->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(m->val, val, used * sizeof(double), hipMemcpyHostToDevice, h->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(h->stream)) != hipSuccess) {   // on h's stream, as the SpMV that reads them
         pamg_csr_free(m);
         return fail(h, e, "pamg_csr_create");
     }

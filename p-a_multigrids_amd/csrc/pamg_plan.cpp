@@ -102,8 +102,10 @@ int pamg_halo_loopback(pamg_handle *const *hs, int n, int level) {
             const size_t ns = qa < 0 ? 0 : (size_t)(Pa.send_peer_off[qa + 1] - Pa.send_peer_off[qa]);
             if (nr != ns) { hb->err = "loopback: send/recv counts differ"; return PAMG_ERR_STATE; }
             if (nr == 0) continue;
-            if (hipMemcpy(Pb.d_recv + 6 * (size_t)Pb.recv_peer_off[qb], Pa.send_buf(Pa.send_cur) + 6 * (size_t)Pa.send_peer_off[qa],
-                          6 * nr * sizeof(double), hipMemcpyDeviceToDevice) != hipSuccess)
+            // on the receiver's stream, so its unpack below is ordered behind the copy (a blocking
+            // hipMemcpy runs on the null stream, which the non-blocking handle streams do not wait for)
+            if (hipMemcpyAsync(Pb.d_recv + 6 * (size_t)Pb.recv_peer_off[qb], Pa.send_buf(Pa.send_cur) + 6 * (size_t)Pa.send_peer_off[qa],
+                               6 * nr * sizeof(double), hipMemcpyDeviceToDevice, hb->stream) != hipSuccess)
                 return PAMG_ERR_HIP;
         }
         if (pamg::launch_halo_unpack(hb->stream, hb->lv[level], hb->tov, hb->tovo) != hipSuccess) return PAMG_ERR_HIP;
