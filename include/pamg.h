@@ -61,7 +61,9 @@ extern "C" {
 #define PAMG_K_VCYCLE_COARSE 9   /* fused V-cycle, levels 2..L launch */
 #define PAMG_K_VCYCLE_PIPE 10    /* pipelined fused V-cycle: level 1 of cycle c + levels 2..L of cycle c+1 */
 #define PAMG_K_VCYCLE_RHSF 11    /* the pipelined launch that starts a pamg_run step (told, RHS) */
-#define PAMG_K_COUNT 12
+#define PAMG_K_VCYCLE_RES 12     /* resident V-cycle call: every cycle of a pamg_vcycle call in one launch */
+#define PAMG_K_VCYCLE_RES_RHSF 13 /* the resident launch that starts a pamg_run step */
+#define PAMG_K_COUNT 14
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;
@@ -186,9 +188,13 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid);
 /* launch schedule of pipelined V-cycle calls (fused = 3, halo exchanged once per call).
  * Every operation of a call is local to an un_ele, so tiles need no ordering until the
  * call's end: 1 one launch per cycle; 2 the tiles as two halves on two HIP streams;
- * 0 automatic (one GPU: 1; a partition of a multi-rank run: 2). The state after the call
- * is bitwise the same in all. */
+ * 3 resident: every cycle of the call in one launch, each tile's state on-chip between
+ * cycles; 0 automatic (3 where supported: two levels or more; else one GPU: 1, a partition
+ * of a multi-rank run: 2). The state after the call is bitwise the same in all. */
 int pamg_set_call_schedule(pamg_handle *h, int schedule);
+/* fp64 operations of one V-cycle of the handle's configuration (the resident launch's
+ * roofline: every sweep, residual, restriction and prolongation cascade) */
+int pamg_vcycle_flops(pamg_handle *h, double *flops_per_cycle);
 int pamg_synchronize(pamg_handle *h);
 
 /* ---- measurement ---- */

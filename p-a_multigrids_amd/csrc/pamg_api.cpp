@@ -490,6 +490,36 @@ double vcycle_pipe_bytes(pamg_handle *h, int keep) {
         for (int l = 2; l <= h->p.multi_levels; ++l) b -= 48.0 * h->lv[l].N;
     return b;
 }
+//   resident launch (a whole call): every level's state in and out once -- level 1 reads
+//                     tnew and RHS (the source s' when it starts a step) and writes tnew,
+//                     and with PAMG_KEEP_L1 its residual and tnew_nonlin (and the RHS it
+//                     formed); told with PAMG_KEEP_TOLD; a coarse level reads tnew and RHSN
+//                     and writes tnew and RHSN (level 2's RHSN: the restriction of level 1's
+//                     last residual), with PAMG_KEEP_COARSE its RHS and residual
+double vcycle_res_bytes(pamg_handle *h, int keep, bool rhsf) {
+    const int L = h->p.multi_levels;
+    double b = (72.0 + (keep & PAMG_KEEP_L1 ? (rhsf ? 72.0 : 48.0) : 0.0) + (keep & PAMG_KEEP_TOLD ? 24.0 : 0.0)) *
+               h->lv[1].N;
+    for (int l = 2; l <= L; ++l) b += (96.0 + (keep & PAMG_KEEP_COARSE ? 48.0 : 0.0)) * h->lv[l].N;
+    return b + 104.0 * h->U * L;
+}
+// fp64 operations of one V-cycle (fma = 2): a sweep is 12 fma (contracted) or 42 operations
+// (the reference's order, apply_A + update), get_residual 9 fma or 36; the restrictor's input
+// mean 3 per sub-element of the levels < L; the prolongator cascade 21 per coarse
+// sub-element (splitting.F90:59-88, executed although dead)
+double vcycle_flops(pamg_handle *h) {
+    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    const bool f = h->p.arith == 1;
+    const double sw = f ? 24.0 : 42.0, rs = f ? 18.0 : 36.0;
+    double fl = 0.0;
+    for (int l = 1; l <= L; ++l) {
+        const double n = (double)h->lv[l].N;
+        if (l < L) fl += n * (2.0 * ns * sw + rs + 3.0);
+        else fl += n * ((ns + (double)ns * h->p.n_coarse) * sw + rs);
+        if (l >= 2) fl += n * 21.0;
+    }
+    return fl;
+}
 // PAMG_PIPE_KEEP=<mask> forces stores into every pipelined launch (A/B runs; 7 = all)
 int pipe_keep_env() {
     static const int k = getenv("PAMG_PIPE_KEEP") ? atoi(getenv("PAMG_PIPE_KEEP")) & PAMG_KEEP_ALL : 0;
@@ -588,10 +618,14 @@ int vcycle_corrected(pamg_handle *h) {
 
 // n V-cycles as two fused launches each (pamg_vcycle.hip)
 // pipelined-call schedule (pamg_set_call_schedule; PAMG_CALL_SCHEDULE=<s> overrides for A/B runs)
+// 0 automatic: the resident form where it applies (two levels or more, the halo words exchanged
+// once per call), else one launch per cycle (one GPU) or two tile streams (a partition)
 int call_schedule(pamg_handle *h) {
     static const int cs_env = getenv("PAMG_CALL_SCHEDULE") ? atoi(getenv("PAMG_CALL_SCHEDULE")) : -1;
     const int s = cs_env >= 0 ? cs_env : h->call_schedule;
-    return s ? s : (h->nranks > 1 ? 2 : 1);
+    if (s) return s;
+    if (vcycle_resident_supported(h->p.n_split, h->p.multi_levels) && h->p.halo_exchange == 0) return 3;
+    return h->nranks > 1 ? 2 : 1;
 }
 
 // dead_after (pamg_run, every step but the last): the next call rewrites the fields this one
@@ -653,6 +687,38 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
     const int tile = vcycle_tile_un_eles(h->p.n_split);
     const int ntiles = (h->U + tile - 1) / tile;
     const int sched = call_schedule(h);
+    // schedule 3, resident: the call's n cycles in one launch (pamg_vcycle.hip k_vc_res), every
+    // tile's state on-chip between them; the final-cycle stores as the pipelined schedule makes
+    // them (the call's last launch stores all, or inside pamg_run the fields the next step reads)
+    if (pipe && n >= 1 && sched == 3 && h->p.halo_exchange == 0 && !h->coarse_ahead &&
+        vcycle_resident_supported(h->p.n_split, L)) {
+        const int buf = two ? 1 - P1.send_cur : 0;
+        if (h->sent_pending[buf]) {
+            HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[buf], 0));
+            h->sent_pending[buf] = false;
+        }
+        const bool rhsf = rhs_first;
+        const int kt = rhsf && !dead_after ? PAMG_KEEP_TOLD : 0;
+        const int keep = (dead_after ? pipe_keep_env() : PAMG_KEEP_ALL) | kt;
+        if (kt) CHK(join_comm(h));   // the send buffers' told halves are rewritten
+        {
+            Span sp(h, rhsf ? PAMG_K_VCYCLE_RES_RHSF : PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, rhsf));
+            HIPCHK(h, launch_vcycle_resident(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
+                                             h->tovo, P1.send_buf(buf), L2.RHSN, keep, rhsf,
+                                             two ? P1.send_buf(1 - buf) : nullptr, n));
+        }
+        if (rhsf) {
+            h->overlap_static_l1 = kt != 0;
+            h->told_halo_stale_l1 = kt == 0;
+        }
+        h->tnn_level = 1;
+        if (dead_after) {
+            P1.send_cur = buf;
+            return join_comm(h);
+        }
+        CHK(halo_async(h, buf));
+        return join_comm(h);
+    }
     if (pipe && n > 1 && sched == 2 && h->p.halo_exchange == 0 && ntiles >= 2 && !h->coarse_ahead) {
         const int buf = two ? 1 - P1.send_cur : 0;
         if (h->sent_pending[buf]) {
@@ -1249,10 +1315,13 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
                                 vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth);
         // told := tnew and the RHS inside the step's first level-1 launch when that launch is a
         // pipelined one on the one-stream schedule
+        // (the resident schedule starts the step in its one launch, for any n_multigrid)
+        const int cs = call_schedule(h);
         const bool defer_rhs = fused_next && h->p.fused == 3 && L > 1 && h->p.halo_exchange == 0 &&
                                vcycle_rhsf_supported(h->p.n_split) &&
-                               call_schedule(h) == 1 && (n_multigrid > 1 || t + 1 < ntime) && !PAMG_RHS_TOLD_HALO &&
-                               getenv("PAMG_NO_RHS_FUSION") == nullptr;
+                               (cs == 3 ? vcycle_resident_supported(h->p.n_split, L)
+                                        : cs == 1 && (n_multigrid > 1 || t + 1 < ntime)) &&
+                               !PAMG_RHS_TOLD_HALO && getenv("PAMG_NO_RHS_FUSION") == nullptr;
         int rc = begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0, fused_next, defer_rhs);
         if (rc == PAMG_OK) rc = vcycle(h, n_multigrid, t + 1 < ntime);   // a step's leftovers die in the next one
         if (rc != PAMG_OK) {
@@ -1285,8 +1354,15 @@ int pamg_timing_reset(pamg_handle *h) {
     return PAMG_OK;
 }
 
+int pamg_vcycle_flops(pamg_handle *h, double *flops_per_cycle) {
+    if (!h || !flops_per_cycle) return PAMG_ERR_ARG;
+    if (!h->mesh_ready) return PAMG_ERR_STATE;
+    *flops_per_cycle = vcycle_flops(h);
+    return PAMG_OK;
+}
+
 int pamg_set_call_schedule(pamg_handle *h, int schedule) {
-    if (!h || schedule < 0 || schedule > 2) return PAMG_ERR_ARG;
+    if (!h || schedule < 0 || schedule > 3) return PAMG_ERR_ARG;
     h->call_schedule = schedule;
     return PAMG_OK;
 }

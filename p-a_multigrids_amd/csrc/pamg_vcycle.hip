@@ -124,6 +124,7 @@ struct VArgs {
     // RHSF launches (the first of a pamg_run step, told := tnew and level 1's RHS from it) with
     // kKeepTold: the second send buffer, whose told halves it writes too
     double *send_b;
+    int cycles;             // the resident launch: cycles of the call
 };
 
 // Stores of a pipelined launch whose values the rest of the call overwrites before any read
@@ -887,6 +888,228 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
     stamp<MT>(A, 7);
 }
 
+// ===================================================================== resident call
+// A whole pamg_vcycle call of m cycles in one launch (fused = 3, the resident form): a
+// workgroup carries its tile through every cycle of the call with all of the tile's state
+// on-chip. It can, because nothing of a V-cycle crosses a tile (see the header) and the
+// cycle's data dependences only run from cycle c-1 to cycle c:
+//   * level l's restriction-leg call (:331) starts from its own tnew (:327 / :348) and reads
+//     as RHS the restriction of level l-1's residual of the PREVIOUS cycle (:336);
+//   * its prolongation-leg call starts from its own restriction-leg tnew (:367), the
+//     prolongated values being overwritten at its first sweep (:550);
+// so in cycle c every level runs its calls at once, from registers: level 1 on every thread
+// (the adjacent pair, as k_vc_fine), level l >= 2 on the threads PGeo assigns it (one coarse
+// sub-element each, as the pipelined tail), the coarsest level's 1 + n_coarse calls at raised
+// priority. One barrier per cycle publishes the residual means and restriction-leg images
+// in LDS; behind it every coarse owner forms its RHS of the next cycle (the restrictor, :336)
+// and runs the prolongator cascade (:370) from its final tnew (dead, :550, executed as in
+// the other forms). A second barrier closes the cycle before those LDS images are reused.
+// HBM sees the tile's state twice per call: loaded at the start (tnew and RHS or, starting
+// a time step (RHSF), tnew and the source s' of level 1; tnew and RHSN of the coarse
+// levels) and stored at the end, with the same final-cycle store policy as the pipelined
+// launches (VArgs::keep). Every sweep, residual, restriction and prolongation of every cycle
+// runs, in the same order on the same values: the state after the call is bitwise the
+// per-step kernel sequence's (tests/test_gpu_parity.py). The cycle is fp64-issue-bound here,
+// no longer HBM-bound.
+#ifndef PAMG_RES_WAVES
+#define PAMG_RES_WAVES 4
+#endif
+template <int S, int L>
+struct RGeo {
+    using P = PGeo<S, L>;
+    static constexpr int C = L - 1;
+    static constexpr int CI() { return 4 * Geo<S, L>::T; }   // coarse images behind F0 | M0
+    static constexpr int LDS() { return CI() + (C >= 2 ? P::M(C) : 0); }
+};
+
+// the operator records are re-fetched (scalar loads) where each phase uses them: an index the
+// compiler cannot see through keeps it from hoisting every level's record out of the cycle
+// loop into SGPRs it does not have (they spilled to VGPRs)
+__device__ __forceinline__ uint32_t opaque(uint32_t u) {
+    __asm__ volatile("" : "+v"(u));
+    return u;
+}
+
+template <int S, int L, class ST, bool RHSF>
+__global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, const double *__restrict__ sp0,
+                                                                      const double *__restrict__ sp1,
+                                                                      const double *__restrict__ sp2,
+                                                                      const double *__restrict__ sp3,
+                                                                      const double *__restrict__ sp4) {
+    using G = Geo<S, L>;
+    using P = PGeo<S, L>;
+    using R = RGeo<S, L>;
+    constexpr int C = G::C;
+    static_assert(C > 0 && G::NP == 2, "the resident launch needs a coarse level and streams pairs");
+    constexpr int T = G::T, NP = 2;
+    __shared__ __attribute__((aligned(16))) double F0[R::LDS()];
+    double *const M0 = F0 + 3 * T;
+    double *const CI = F0 + R::CI();
+    const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
+    const int t = threadIdx.x;
+    const double rdt = A.rdt;
+    const int ns = A.n_smooth, m = A.cycles;
+    const int64_t tb = (int64_t)blockIdx.x + A.tile0;   // tile
+    const VLevel &V0 = A.lv[0];
+    const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo, keepc = A.keep & kKeepCoarse;
+    bool v0;
+    const uint32_t s0 = tile_index<S>(A, tb, T, 0, NP * t, v0);   // clamped: loads stay in bounds
+    const uint32_t w0 = s0 >> G::lg(0);
+    int h0[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) h0[k] = v0 ? hs_pack(V0.H.hsub[(s0 + k) & ((1 << G::lg(0)) - 1)]) : 0;
+    double x0[NP][3], b0[NP][3], p0[NP][3];
+    // ---- level 1: tnew (tnew_nonlin := tnew, :327) and the RHS
+    if constexpr (RHSF) {   // the start of a time step (:316-317, get_RHS :452-464), as k_vc_fine
+        double q0[3], q1[3];
+        load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
+        load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, s0, q0, q1);
+        const uint32_t wu = G::uni(0) ? (uint32_t)__builtin_amdgcn_readfirstlane(w0) : w0;
+        const double c = sp0[(size_t)wu * kStcStride + kStcC];
+        rhs_from_source(c, rdt, x0[0], q0, b0[0]);
+        rhs_from_source(c, rdt, x0[1], q1, b0[1]);
+        if (v0) {
+            if (A.keep & kKeepTold) {
+                store3p(V0.TOLD(), V0.pitch, s0, x0[0], x0[1]);
+#pragma unroll
+                for (int k = 0; k < NP; ++k) hs_write_static(V0.H, A.send_b, w0, h0[k], x0[k]);
+            }
+            // the RHS lives in registers for the call; stored for an observer (dead inside pamg_run)
+            if (keep1) store3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
+        }
+    } else {
+        load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
+        load3p<PAMG_NT_RL>(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
+    }
+    // ---- the thread's coarse sub-element (level rl, tile-local ic): tnew and RHS of cycle 1
+    //      (the RHS: RHSN, the restriction of the previous call's last residual)
+    double xs[3] = {0.0, 0.0, 0.0}, bs[3] = {0.0, 0.0, 0.0};
+    uint32_t gxc = 0;
+    bool vc = false;
+    int ic = 0;
+    static_for<1, C + 1>([&](auto lc) {
+        constexpr int l = decltype(lc)::value;
+        if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l)) return;
+        const VLevel &V = A.lv[l];
+        ic = t - P::T0(l);
+        gxc = tile_index<S>(A, tb, P::nt(l), l, ic, vc);
+        load3(V.T(), V.pitch, gxc, xs);
+        load3(l == 1 ? A.rhsn2 : V.RHSN(), V.pitch, gxc, bs);
+    });
+    // one cycle; LAST: the call's last, which makes the final-cycle stores (peeled, so that no
+    // store address stays live across the loop)
+    auto cycle = [&](int c, auto lastc) {
+        constexpr bool last = decltype(lastc)::value;
+        // ---- the coarsest level: restriction-leg call (:331 via :351), get_residual (:338),
+        //      the 1 + n_coarse calls (:351-353) -- the tile's longest dependent chain, first
+        if (t >= P::T0(C) && t < P::T0(C) + P::NTH(C)) {
+            const VLevel &V = A.lv[C];
+            ST St;
+            stencil(G::uni(C), SP[C], opaque(gxc >> G::lg(C)), St);
+            constexpr int prio = std::is_same<ST, StcF>::value ? PAMG_CHAIN_PRIO : 0;
+            if (prio) __builtin_amdgcn_s_setprio(prio);
+            if (last && keepc && vc) store3(V.RHS(), V.pitch, gxc, bs);
+            double x[3], p[3];
+            copy3(x, xs);
+            for (int it = 0; it < ns; ++it) {
+                copy3(p, x);
+                sweep(St, rdt, bs, x);
+            }
+            double r[3];
+            residual(St, rdt, p, bs, r);
+            if (last && keepc && vc) store3(V.RES(), V.pitch, gxc, r);
+            copy3(x, p);   // tnew_nonlin := tnew (:348)
+            const int nB = ns * A.n_coarse;
+            for (int it = 0; it < nB; ++it) {
+                copy3(p, x);
+                sweep(St, rdt, bs, x);
+            }
+            copy3(xs, p);
+            if (prio) __builtin_amdgcn_s_setprio(0);
+            if (last && vc) store3(V.T(), V.pitch, gxc, xs);
+        }
+        // ---- level 1: restriction-leg call (:331), get_residual (:338), prolongation-leg call
+        //      (:367-376) from the restriction-leg tnew
+        if (c > 0) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) copy3(x0[k], p0[k]);   // tnew_nonlin := tnew (:327)
+        }
+        ST St0;
+        stencil(G::uni(0), sp0, opaque(w0), St0);
+        sweeps2(St0, rdt, ns, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
+        if (v0) {
+            double r[NP][3];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) residual(St0, rdt, p0[k], b0[k], r[k]);
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                *reinterpret_cast<double2 *>(F0 + q * T + 2 * t) = make_double2(p0[0][q], p0[1][q]);
+            if (last && keep1) store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
+            *reinterpret_cast<double2 *>(M0 + 2 * t) =
+                make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k) copy3(x0[k], p0[k]);
+        sweeps2(St0, rdt, ns, b0[0], b0[1], x0[0], x0[1], p0[0], p0[1]);
+        if (last && v0) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                if (keeph) hs_write(false, V0.H, w0, h0[k], p0[k]);
+            store3p<PAMG_NT_TS>(V0.T(), V0.pitch, s0, p0[0], p0[1]);
+            if (keep1) store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
+        }
+        // ---- levels 2 .. C-1 (1-based): both smoother calls and get_residual of the cycle
+        static_for<1, C>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l)) return;   // wave-uniform
+            const VLevel &V = A.lv[l];
+            ST St;
+            stencil(G::uni(l), SP[l], opaque(gxc >> G::lg(l)), St);
+            if (last && keepc && vc) store3(V.RHS(), V.pitch, gxc, bs);
+            double x[3], p[3];
+            copy3(x, xs);
+            for (int it = 0; it < ns; ++it) {
+                copy3(p, x);
+                sweep(St, rdt, bs, x);
+            }
+            double r[3];
+            residual(St, rdt, p, bs, r);
+            if (last && keepc && vc) store3(V.RES(), V.pitch, gxc, r);
+            if (vc) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) CI[P::F(l) + q * P::nt(l) + ic] = p[q];
+                CI[P::M(l) + ic] = (r[0] + r[1] + r[2]) / 3.;
+            }
+            copy3(x, p);   // tnew_nonlin := tnew (:367)
+            for (int it = 0; it < ns; ++it) {
+                copy3(p, x);
+                sweep(St, rdt, bs, x);
+            }
+            copy3(xs, p);
+            if (last && vc) store3(V.T(), V.pitch, gxc, xs);
+        });
+        __syncthreads();
+        // ---- every coarse owner: the restrictor (:336) of the finer level's residual of this
+        //      cycle -- its RHS of the next cycle (stored as RHSN after the call's last) -- and
+        //      the prolongator cascade (:370) from its final tnew into the finer level's
+        //      restriction-leg image (dead, :550); the children of i are 4i .. 4i+3 (Level::pos)
+        static_for<1, C + 1>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l) || !vc) return;
+            const double *Mf = l == 1 ? M0 : CI + P::M(l - 1);
+            bs[0] = Mf[4 * ic + 2];
+            bs[1] = Mf[4 * ic + 3];
+            bs[2] = Mf[4 * ic];
+            if (last) store3(l == 1 ? A.rhsn2 : A.lv[l].RHSN(), A.lv[l].pitch, gxc, bs);
+            const int fi[4] = {4 * ic, 4 * ic + 1, 4 * ic + 2, 4 * ic + 3};
+            prolong_cascade(l == 1 ? F0 : CI + P::F(l - 1), G::nt(l - 1), fi, xs);
+        });
+        __syncthreads();
+    };
+    for (int c = 0; c + 1 < m; ++c) cycle(c, std::false_type{});
+    cycle(m - 1, std::true_type{});
+}
+
 // part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
 template <int S, int L, class ST, bool W8>
 hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
@@ -908,6 +1131,17 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
                                A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         else
             return hipErrorInvalidValue;
+    } else if (part == 4 || part == 5) {   // the resident call (5: starting a time step)
+        if constexpr (L >= 2 && fine_np(S) == 2) {
+            if (part == 5)
+                hipLaunchKernelGGL((k_vc_res<S, L, ST, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
+                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+            else
+                hipLaunchKernelGGL((k_vc_res<S, L, ST, false>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
+                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+        } else {
+            return hipErrorInvalidValue;
+        }
     } else {
         hipLaunchKernelGGL((k_vc_fine<S, L, ST, false, W8>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc, nullptr,
                            nullptr, nullptr, nullptr);
@@ -940,6 +1174,7 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     const long w8_max = w8_env >= 0 ? w8_env : ((std::is_same<ST, Stc>::value || part >= 2) ? (1l << 40) : 4 * n_cu);
     // (and only instances that fit 64 VGPRs without scratch: several L >= 4 and n_split = 3
     // instances spill there and stay at their natural register count)
+    if (part >= 4) return launch_sltw<S, L, ST, false>(s, A, grid, part);
     if constexpr (S >= 3) {
         static const bool fits[3] = {no_scratch((const void *)k_vc_fine<S, L, ST, false, true>),
                                      L >= 2 && no_scratch((const void *)k_vc_fine<S, L, ST, (L >= 2), true>),
@@ -971,9 +1206,10 @@ hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, int par
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
                        double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part, int keep,
-                       int ua, int ub, double *send_b = nullptr) {
+                       int ua, int ub, double *send_b = nullptr, int cycles = 1) {
     const bool coarse = part == 1;
-    if ((part == 2 || part == 3) && L < 2) return hipErrorInvalidValue;
+    if (part >= 2 && L < 2) return hipErrorInvalidValue;
+    if (part >= 4 && cycles < 1) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
     VArgs A{};
     for (int l = 0; l < L; ++l) {
@@ -983,7 +1219,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
         VLevel &o = A.lv[l];
         if (V.TNN != V.T + 3 * V.pitch || V.RHS != V.T + 6 * V.pitch || V.RES != V.T + 9 * V.pitch ||
             V.TOLD != V.T + 12 * V.pitch || (l != 1 && V.RHSN != V.T + 15 * V.pitch) ||
-            (l == 0 && part == 3 && V.SRC != V.T + 18 * V.pitch))
+            (l == 0 && (part == 3 || part == 5) && V.SRC != V.T + 18 * V.pitch))
             return hipErrorInvalidValue;
         if (l == 1 && rhsn2 != V.T + 15 * V.pitch && (!V.RHSN_alt || rhsn2 != V.RHSN_alt)) return hipErrorInvalidValue;
         o.base = V.T; o.stc = V.stc;
@@ -999,6 +1235,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.rhsn2 = rhsn2;
     A.keep = keep;
     A.send_b = send_b;
+    A.cycles = cycles;
     // tile: 2**TL level-1 sub-elements, TL = fine_tl (level-1 launch) or CGeo's (coarse launch)
     const int TL = coarse ? (2 * n_split > 8 ? std::min(2 * n_split, kFineTLMax) : 8) : fine_tl(n_split);
     // un_eles [ua, ub) (ub < 0: all); ua on a tile boundary, ub too unless it is U
@@ -1066,6 +1303,16 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, L > 1 ? rhsn2 : nullptr,
                        pipe ? (rhsf ? 3 : 2) : 0, keep, ua, ub, send_b);
 }
+
+hipError_t launch_vcycle_resident(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                                  int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
+                                  int keep, bool rhsf, double *send_b, int cycles) {
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, rhsn2, rhsf ? 5 : 4, keep, 0, -1,
+                       send_b, cycles);
+}
+
+// the resident form: two levels or more, adjacent pairs (fine_np == 2)
+bool vcycle_resident_supported(int n_split, int L) { return L >= 2 && fine_np(n_split) == 2; }
 
 // the RHSF instance streams adjacent pairs (fine_np == 2; A/B builds with PAMG_NP1_MAX_S may not)
 bool vcycle_rhsf_supported(int n_split) { return fine_np(n_split) == 2; }

@@ -21,7 +21,7 @@ TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN, SOURCE = 0, 1, 2, 3, 4, 5
 (K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH, K_VCYCLE,
  K_VCYCLE_COARSE) = range(10)
 K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle",
-           "vcycle_coarse", "vcycle_pipe", "vcycle_rhsf"]
+           "vcycle_coarse", "vcycle_pipe", "vcycle_rhsf", "vcycle_res", "vcycle_res_rhsf"]
 
 
 class PamgParams(C.Structure):
@@ -84,6 +84,7 @@ def lib():
         "pamg_timing_reset": (I, [P]),
         "pamg_timing_stride": (I, [P, I]),
         "pamg_set_call_schedule": (I, [P, I]),
+        "pamg_vcycle_flops": (I, [P, C.POINTER(C.c_double)]),
         "pamg_timing_issued": (I, [P, I, C.POINTER(C.c_long)]),
         "pamg_timing_read": (I, [P, I, C.POINTER(D), C.POINTER(C.c_long), C.POINTER(D)]),
         "pamg_sweep_bench": (I, [P, I, I, C.POINTER(D), C.POINTER(D)]),

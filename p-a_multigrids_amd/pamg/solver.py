@@ -218,8 +218,14 @@ class SemiImplicitIterative:
     def timing_reset(self): self._call("pamg_timing_reset")
     def timing_stride(self, every): self._call("pamg_timing_stride", every)
 
+    def vcycle_flops(self):
+        """fp64 operations of one V-cycle (pamg_vcycle_flops)"""
+        f = C.c_double()
+        self._call("pamg_vcycle_flops", C.byref(f))
+        return f.value
+
     def set_call_schedule(self, schedule):
-        """Pipelined calls: 0 automatic, 1 one launch per cycle, 2 two tile streams
+        """Pipelined calls: 0 automatic, 1 one launch per cycle, 2 two tile streams, 3 resident
         (pamg_set_call_schedule)."""
         self._call("pamg_set_call_schedule", schedule)
 

@@ -217,6 +217,7 @@ def test_pipelined_vcycle_launches():
     cycle, so 2 steps of 3 cycles are coarse, 5 pipelined, level 1."""
     meta, _ = goldens.load("u8_s3_l3_gs")
     s = gpu_solver(meta, fused=3)
+    s.set_call_schedule(1)
     s.timing_enable(0xF7F)
     s.timing_reset()
     s.vcycle(3)
@@ -230,6 +231,26 @@ def test_pipelined_vcycle_launches():
     assert t["vcycle_coarse"]["launches"] == 1 and t["vcycle_rhsf"]["launches"] == 2
     assert t["vcycle_pipe"]["launches"] == 3 and t["rhs"]["launches"] == 0
     assert t["vcycle"]["launches"] == 1 and t["smooth_L1"]["launches"] == 0
+
+
+def test_resident_vcycle_launches():
+    """fused = 3, schedule 3 (automatic where it applies): a call of n cycles is one launch; a
+    pamg_run step is one launch that also starts the step (told, RHS: vcycle_res_rhsf)."""
+    meta, _ = goldens.load("u8_s3_l3_gs")
+    s = gpu_solver(meta, fused=3)
+    s.timing_enable(0x3F7F)
+    s.timing_reset()
+    s.vcycle(3)
+    t = s.timing()
+    assert t["vcycle_res"]["launches"] == 1 and t["vcycle_coarse"]["launches"] == 0
+    assert t["vcycle_pipe"]["launches"] == 0 and t["vcycle"]["launches"] == 0
+    s.timing_reset()
+    s.run(2, 3)
+    t = s.timing()
+    assert t["vcycle_res_rhsf"]["launches"] == 2 and t["vcycle_res"]["launches"] == 0
+    assert t["rhs"]["launches"] == 0 and t["vcycle_pipe"]["launches"] == 0 and t["smooth_L1"]["launches"] == 0
+    # one launch moves every level's state in and out once, whatever the number of cycles
+    assert t["vcycle_res_rhsf"]["bytes"] > 0
 
 
 @pytest.mark.parametrize("mesh,S,L,solver,ns", [
@@ -420,11 +441,12 @@ def test_pipelined_call_boundaries_are_invisible(mesh, S, L, arith):
                                         ("untitled8192.msh", 5, 4, 4), ("untitled2048.msh", 5, 5, 3)])
 @pytest.mark.parametrize("arith", [0, 1])
 def test_call_schedules_equal_one_sequence(mesh, S, L, n, arith):
-    """Pipelined calls as two tile halves on two streams (schedule 2) leave the state of one
-    launch per cycle, bit for bit, t_overlap included."""
+    """Pipelined calls as two tile halves on two streams (schedule 2) and resident calls (every
+    cycle of the call in one launch, schedule 3) leave the state of one launch per cycle, bit
+    for bit, t_overlap included."""
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
     runs = []
-    for ts in (1, 2):
+    for ts in (1, 2, 3):
         s = pamg.SemiImplicitIterative(m, S, L, arith=arith, fused=3)
         s.set_call_schedule(ts)
         s.begin_timestep()
@@ -442,7 +464,7 @@ def test_call_schedules_equal_one_sequence(mesh, S, L, n, arith):
 @pytest.mark.parametrize("mesh,S,L,n", [("untitled8192.msh", 5, 3, 2), ("irregular.msh", 4, 4, 3),
                                         ("900_ele.msh", 3, 2, 1), ("untitled2048.msh", 5, 5, 2),
                                         ("irregular.msh", 6, 3, 2), ("irregular.msh", 7, 3, 1)])
-@pytest.mark.parametrize("schedule", [1, 2])
+@pytest.mark.parametrize("schedule", [1, 2, 3])
 def test_time_loop_equals_public_steps(mesh, S, L, n, schedule):
     """pamg_run skips what a step leaves that the next step overwrites unread (the step-start
     tnew_nonlin copy, the last cycle's residual / tnew_nonlin / coarse RHS and residual / halo
