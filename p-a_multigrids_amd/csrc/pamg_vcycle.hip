@@ -245,28 +245,44 @@ __device__ __forceinline__ void stencil(bool uni, const double *__restrict__ stc
     load_stc(stc + u * (uint32_t)kStcStride, S);
 }
 
+// n sweeps of one smoother call (n_smooth, :491-507): x the last iterate (tnew_nonlin), p the
+// one before it (tnew, :550 vs :693) -- copied once, before the last sweep (p unchanged if n = 0)
+template <class ST>
+__device__ __forceinline__ void sweeps1(const ST &S, double rdt, int n, const double b[3], double x[3], double p[3]) {
+    if (n <= 0) return;
+    for (int it = 1; it < n; ++it) sweep(S, rdt, b, x);
+    copy3(p, x);
+    sweep(S, rdt, b, x);
+}
+
 // two sub-elements of one un_ele, interleaved
 template <class ST>
 __device__ __forceinline__ void sweeps2(const ST &S, double rdt, int n, const double b0[3], const double b1[3],
                                         double x0[3], double x1[3], double p0[3], double p1[3]) {
-    for (int it = 0; it < n; ++it) {
-        copy3(p0, x0);
-        copy3(p1, x1);
+    if (n <= 0) return;
+    for (int it = 1; it < n; ++it) {
         sweep(S, rdt, b0, x0);
         sweep(S, rdt, b1, x1);
     }
+    copy3(p0, x0);
+    copy3(p1, x1);
+    sweep(S, rdt, b0, x0);
+    sweep(S, rdt, b1, x1);
 }
 
 // N sub-elements of one un_ele, interleaved
 template <int N, class ST>
 __device__ __forceinline__ void sweepsN(const ST &S, double rdt, int n, const double b[N][3], double x[N][3],
                                         double p[N][3]) {
-    for (int it = 0; it < n; ++it) {
-#pragma unroll
-        for (int q = 0; q < N; ++q) copy3(p[q], x[q]);
+    if (n <= 0) return;
+    for (int it = 1; it < n; ++it) {
 #pragma unroll
         for (int q = 0; q < N; ++q) sweep(S, rdt, b[q], x[q]);
     }
+#pragma unroll
+    for (int q = 0; q < N; ++q) copy3(p[q], x[q]);
+#pragma unroll
+    for (int q = 0; q < N; ++q) sweep(S, rdt, b[q], x[q]);
 }
 
 template <class ST>
@@ -622,19 +638,13 @@ __device__ __forceinline__ void coarsest_chain(const VArgs &A, const double *__r
     constexpr int prio = std::is_same<ST, StcF>::value ? PAMG_CHAIN_PRIO : 0;
     if (prio) __builtin_amdgcn_s_setprio(prio);
     double p[3];
-    for (int it = 0; it < ns; ++it) {
-        copy3(p, x);
-        sweep(St, rdt, b, x);
-    }
+    sweeps1(St, rdt, ns, b, x, p);
     double r[3];
     residual(St, rdt, p, b, r);
     if (v && keep) store3(V.RES(), V.pitch, gx, r);
     copy3(x, p);   // tnew_nonlin := tnew (:348)
     const int nB = ns * A.n_coarse;
-    for (int it = 0; it < nB; ++it) {
-        copy3(p, x);
-        sweep(St, rdt, b, x);
-    }
+    sweeps1(St, rdt, nB, b, x, p);
     if (prio) __builtin_amdgcn_s_setprio(0);
     if (v) store3(V.T(), V.pitch, gx, p);
 #pragma unroll
@@ -673,10 +683,7 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
         const bool keep = A.keep & kKeepCoarse;
         if (v && keep) store3(V.RHS(), V.pitch, gx, b);
         stencil(G::uni(l), SP[l], gx >> G::lg(l), St);
-        for (int it = 0; it < ns; ++it) {
-            copy3(p, x);
-            sweep(St, rdt, b, x);
-        }
+        sweeps1(St, rdt, ns, b, x, p);
         double r[3];
         residual(St, rdt, p, b, r);
         if (v && keep) store3(V.RES(), V.pitch, gx, r);
@@ -709,10 +716,7 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
             for (int c = 0; c < 3; ++c) p[c] = lds[P::PC() + c * P::nt(C) + i];
         } else {
             const int nB = l == C ? ns * A.n_coarse : ns;
-            for (int it = 0; it < nB; ++it) {
-                copy3(p, x);
-                sweep(St, rdt, b, x);
-            }
+            sweeps1(St, rdt, nB, b, x, p);
         }
         if (v) {
             if constexpr (!(HOIST && l == C)) store3(V.T(), V.pitch, gx, p);
@@ -914,6 +918,10 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 #ifndef PAMG_RES_WAVES
 #define PAMG_RES_WAVES 4
 #endif
+// n_split >= 5, L >= 3: the balanced-role instance k_vc_resb (A/B builds: 0 keeps k_vc_res)
+#ifndef PAMG_RES_BALANCED
+#define PAMG_RES_BALANCED 1
+#endif
 template <int S, int L>
 struct RGeo {
     using P = PGeo<S, L>;
@@ -1011,19 +1019,13 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             if (last && keepc && vc) store3(V.RHS(), V.pitch, gxc, bs);
             double x[3], p[3];
             copy3(x, xs);
-            for (int it = 0; it < ns; ++it) {
-                copy3(p, x);
-                sweep(St, rdt, bs, x);
-            }
+            sweeps1(St, rdt, ns, bs, x, p);
             double r[3];
             residual(St, rdt, p, bs, r);
             if (last && keepc && vc) store3(V.RES(), V.pitch, gxc, r);
             copy3(x, p);   // tnew_nonlin := tnew (:348)
             const int nB = ns * A.n_coarse;
-            for (int it = 0; it < nB; ++it) {
-                copy3(p, x);
-                sweep(St, rdt, bs, x);
-            }
+            sweeps1(St, rdt, nB, bs, x, p);
             copy3(xs, p);
             if (prio) __builtin_amdgcn_s_setprio(0);
             if (last && vc) store3(V.T(), V.pitch, gxc, xs);
@@ -1068,10 +1070,7 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             if (last && keepc && vc) store3(V.RHS(), V.pitch, gxc, bs);
             double x[3], p[3];
             copy3(x, xs);
-            for (int it = 0; it < ns; ++it) {
-                copy3(p, x);
-                sweep(St, rdt, bs, x);
-            }
+            sweeps1(St, rdt, ns, bs, x, p);
             double r[3];
             residual(St, rdt, p, bs, r);
             if (last && keepc && vc) store3(V.RES(), V.pitch, gxc, r);
@@ -1081,10 +1080,7 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
                 CI[P::M(l) + ic] = (r[0] + r[1] + r[2]) / 3.;
             }
             copy3(x, p);   // tnew_nonlin := tnew (:367)
-            for (int it = 0; it < ns; ++it) {
-                copy3(p, x);
-                sweep(St, rdt, bs, x);
-            }
+            sweeps1(St, rdt, ns, bs, x, p);
             copy3(xs, p);
             if (last && vc) store3(V.T(), V.pitch, gxc, xs);
         });
@@ -1110,6 +1106,295 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
     cycle(m - 1, std::true_type{});
 }
 
+// ---- balanced roles (n_split >= 5, three levels or more). In k_vc_res the coarsest level's
+// 1 + n_coarse calls (64 dependent sweeps at the defaults: a quarter of a tile's fp64 issue,
+// on ONE wave -- an instruction stream does not get shorter with fewer active lanes) sit on
+// wave 4 beside its level-1 pair, and wave 4 shares its SIMD with wave 0 (the hardware places
+// waves w and w+4 of a 512-thread workgroup on one SIMD, scripts/micro/wave_simd.hip), which
+// also carries level-2 work: that SIMD had ~2.3x the issue of the others and set the pace.
+// Here a tile's issue is split evenly over its four SIMDs:
+//   wave 4      the coarsest level alone (its SIMD partner, wave 0, has the levels 3..L-1);
+//   waves 1,2,3,5  level 1: an adjacent pair and a single sub-element per thread (768);
+//   waves 6,7   level 1: an adjacent pair per thread (256), and level 2: two sub-elements each.
+// Per tile-cycle (n_split 5, L 3): SIMD(0,4) 64 sweeps on one wave; SIMD(1,5) 6, SIMD(2,6) and
+// SIMD(3,7) 7 sub-element units of 2 smoother calls each. Every sub-element's operations are
+// the same as in every other form (bitwise, the same tests). A tile is one un_ele or a part of
+// one (n_split >= 5), so every operator record is wave-uniform and every tile full.
+template <int S, int L, class ST, bool RHSF>
+__global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const double *__restrict__ sp0,
+                                                                const double *__restrict__ sp1,
+                                                                const double *__restrict__ sp2,
+                                                                const double *__restrict__ sp3,
+                                                                const double *__restrict__ sp4) {
+    using G = Geo<S, L>;
+    using P = PGeo<S, L>;
+    using R = RGeo<S, L>;
+    constexpr int C = G::C, T = G::T;
+    static_assert(C >= 2 && C <= 4 && T == 1024 && G::MT == 512 && S >= 5, "balanced roles: n_split >= 5, L 3..5");
+    __shared__ __attribute__((aligned(16))) double F0[R::LDS()];
+    double *const M0 = F0 + 3 * T;
+    double *const CI = F0 + R::CI();
+    const int t = threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const double rdt = A.rdt;
+    const int ns = A.n_smooth, m = A.cycles;
+    const int64_t tb = (int64_t)blockIdx.x + A.tile0;
+    const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo, keepc = A.keep & kKeepCoarse;
+    // Each role runs its own cycle loop with its own state (the loop is unswitched by role, so
+    // the registers of one role's loop-carried state are not reserved in the others); every
+    // role passes the same two barriers per cycle.
+    if (wv == 4) {
+        // ---- the coarsest level: its restriction-leg call, get_residual, 1 + n_coarse calls
+        const VLevel &V = A.lv[C];
+        bool vc;
+        const uint32_t gc = tile_index<S>(A, tb, P::nt(C), C, lane, vc);
+        double xs[3], bs[3];
+        load3(V.T(), V.pitch, gc, xs);
+        load3(V.RHSN(), V.pitch, gc, bs);
+        auto cycle = [&](auto lastc) {
+            constexpr bool last = decltype(lastc)::value;
+            ST St;
+            stencil(true, C == 2 ? sp2 : C == 3 ? sp3 : sp4, opaque(gc >> G::lg(C)), St);
+            constexpr int prio = std::is_same<ST, StcF>::value ? PAMG_CHAIN_PRIO : 0;
+            if (prio) __builtin_amdgcn_s_setprio(prio);
+            if (last && keepc && vc) store3(V.RHS(), V.pitch, gc, bs);
+            double x[3], p[3];
+            copy3(x, xs);
+            sweeps1(St, rdt, ns, bs, x, p);
+            double r[3];
+            residual(St, rdt, p, bs, r);
+            if (last && keepc && vc) store3(V.RES(), V.pitch, gc, r);
+            copy3(x, p);   // tnew_nonlin := tnew (:348)
+            sweeps1(St, rdt, ns * A.n_coarse, bs, x, p);
+            copy3(xs, p);
+            if (prio) __builtin_amdgcn_s_setprio(0);
+            if (last && vc) store3(V.T(), V.pitch, gc, xs);
+            __syncthreads();
+            if (vc) {   // restrictor (:336) of level C-1's residual; prolongator cascade (:370, dead)
+                const double *Mf = CI + P::M(C - 1);
+                bs[0] = Mf[4 * lane + 2];
+                bs[1] = Mf[4 * lane + 3];
+                bs[2] = Mf[4 * lane];
+                if (last) store3(V.RHSN(), V.pitch, gc, bs);
+                const int fi[4] = {4 * lane, 4 * lane + 1, 4 * lane + 2, 4 * lane + 3};
+                prolong_cascade(CI + P::F(C - 1), P::nt(C - 1), fi, xs);
+            }
+            __syncthreads();
+        };
+        for (int c = 0; c + 1 < m; ++c) cycle(std::false_type{});
+        cycle(std::true_type{});
+    } else if (wv == 0) {
+        // ---- levels 3 .. L-1 (1-based), one sub-element of each per lane (none with L = 3)
+        double xs[2][3] = {}, bs[2][3] = {};
+        uint32_t gc[2] = {0, 0};
+        bool vc[2] = {false, false};
+        static_for<2, C>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            const VLevel &V = A.lv[l];
+            gc[l - 2] = tile_index<S>(A, tb, P::nt(l), l, lane, vc[l - 2]);
+            load3(V.T(), V.pitch, gc[l - 2], xs[l - 2]);
+            load3(V.RHSN(), V.pitch, gc[l - 2], bs[l - 2]);
+        });
+        const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
+        auto cycle = [&](auto lastc) {
+            constexpr bool last = decltype(lastc)::value;
+            static_for<2, C>([&](auto lc) {
+                constexpr int l = decltype(lc)::value, k = l - 2;
+                const VLevel &V = A.lv[l];
+                ST St;
+                stencil(true, SP[l], opaque(gc[k] >> G::lg(l)), St);
+                if (last && keepc && vc[k]) store3(V.RHS(), V.pitch, gc[k], bs[k]);
+                double x[3], p[3];
+                copy3(x, xs[k]);
+                sweeps1(St, rdt, ns, bs[k], x, p);
+                double r[3];
+                residual(St, rdt, p, bs[k], r);
+                if (last && keepc && vc[k]) store3(V.RES(), V.pitch, gc[k], r);
+                if (vc[k]) {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) CI[P::F(l) + q * P::nt(l) + lane] = p[q];
+                    CI[P::M(l) + lane] = (r[0] + r[1] + r[2]) / 3.;
+                }
+                copy3(x, p);   // tnew_nonlin := tnew (:367)
+                sweeps1(St, rdt, ns, bs[k], x, p);
+                copy3(xs[k], p);
+                if (last && vc[k]) store3(V.T(), V.pitch, gc[k], xs[k]);
+            });
+            __syncthreads();
+            static_for<2, C>([&](auto lc) {
+                constexpr int l = decltype(lc)::value, k = l - 2;
+                if (!vc[k]) return;
+                const double *Mf = CI + P::M(l - 1);
+                bs[k][0] = Mf[4 * lane + 2];
+                bs[k][1] = Mf[4 * lane + 3];
+                bs[k][2] = Mf[4 * lane];
+                if (last) store3(A.lv[l].RHSN(), A.lv[l].pitch, gc[k], bs[k]);
+                const int fi[4] = {4 * lane, 4 * lane + 1, 4 * lane + 2, 4 * lane + 3};
+                prolong_cascade(CI + P::F(l - 1), P::nt(l - 1), fi, xs[k]);
+            });
+            __syncthreads();
+        };
+        for (int c = 0; c + 1 < m; ++c) cycle(std::false_type{});
+        cycle(std::true_type{});
+    } else {
+        // ---- level 1 (the reference's): waves 1,2,3,5 an adjacent pair + a single sub-element
+        //      per thread (N = 3), waves 6,7 a pair (N = 2) and two sub-elements of level 2
+        const bool grpB = wv >= 6;
+        const VLevel &V0 = A.lv[0];
+        constexpr int hmask = (1 << G::lg(0)) - 1;
+        auto level1 = [&](auto nc) {
+            constexpr int N = decltype(nc)::value;   // level-1 sub-elements of the thread
+            const int ga = (wv == 5 ? 3 : wv - 1) * 64 + lane, gb = (wv - 6) * 64 + lane;
+            const int jp = N == 3 ? 2 * ga : 768 + 2 * gb, js = 512 + ga;
+            bool vp, vq = false;
+            const uint32_t sp = tile_index<S>(A, tb, T, 0, jp, vp);
+            const uint32_t sq = N == 3 ? tile_index<S>(A, tb, T, 0, js, vq) : 0u;
+            const uint32_t w0 = sp >> G::lg(0);   // the tile's un_ele
+            double X0[N][3], B0[N][3], P0[N][3];
+            if constexpr (RHSF) {   // the start of a time step (:316-317, get_RHS :452-464)
+                double q[N][3];
+                load3p<PAMG_NT_TL>(V0.T(), V0.pitch, sp, X0[0], X0[1]);
+                load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, sp, q[0], q[1]);
+                if constexpr (N == 3) {
+                    load3(V0.T(), V0.pitch, sq, X0[2]);
+                    load3(V0.SRC(), V0.pitch, sq, q[2]);
+                }
+                const double c = sp0[(size_t)__builtin_amdgcn_readfirstlane(w0) * kStcStride + kStcC];
+#pragma unroll
+                for (int k = 0; k < N; ++k) rhs_from_source(c, rdt, X0[k], q[k], B0[k]);
+                if (vp) {
+                    if (A.keep & kKeepTold) {
+                        store3p(V0.TOLD(), V0.pitch, sp, X0[0], X0[1]);
+#pragma unroll
+                        for (int k = 0; k < 2; ++k)
+                            hs_write_static(V0.H, A.send_b, w0, hs_pack(V0.H.hsub[(sp + k) & hmask]), X0[k]);
+                    }
+                    if (keep1) store3p(V0.RHS(), V0.pitch, sp, B0[0], B0[1]);
+                }
+                if constexpr (N == 3)
+                    if (vq) {
+                        if (A.keep & kKeepTold) {
+                            store3(V0.TOLD(), V0.pitch, sq, X0[2]);
+                            hs_write_static(V0.H, A.send_b, w0, hs_pack(V0.H.hsub[sq & hmask]), X0[2]);
+                        }
+                        if (keep1) store3(V0.RHS(), V0.pitch, sq, B0[2]);
+                    }
+            } else {
+                load3p<PAMG_NT_TL>(V0.T(), V0.pitch, sp, X0[0], X0[1]);
+                load3p<PAMG_NT_RL>(V0.RHS(), V0.pitch, sp, B0[0], B0[1]);
+                if constexpr (N == 3) {
+                    load3(V0.T(), V0.pitch, sq, X0[2]);
+                    load3(V0.RHS(), V0.pitch, sq, B0[2]);
+                }
+            }
+            // level 2 (0-based 1), group B: sub-elements 2 gb, 2 gb + 1 (RHS: RHSN)
+            double xs[2][3], bs[2][3];
+            bool vc = false;
+            uint32_t gc = 0;
+            if constexpr (N == 2) {
+                const VLevel &V = A.lv[1];
+                gc = tile_index<S>(A, tb, P::nt(1), 1, 2 * gb, vc);
+                load3p(V.T(), V.pitch, gc, xs[0], xs[1]);
+                load3p(A.rhsn2, V.pitch, gc, bs[0], bs[1]);
+            }
+            auto cycle = [&](int c, auto lastc) {
+                constexpr bool last = decltype(lastc)::value;
+                ST St0;
+                stencil(true, sp0, opaque(w0), St0);
+                if (c > 0) {
+#pragma unroll
+                    for (int k = 0; k < N; ++k) copy3(X0[k], P0[k]);   // tnew_nonlin := tnew (:327)
+                }
+                sweepsN<N>(St0, rdt, ns, B0, X0, P0);   // restriction-leg call (:331)
+                double r[N][3];
+#pragma unroll
+                for (int k = 0; k < N; ++k) residual(St0, rdt, P0[k], B0[k], r[k]);   // :338
+                if (vp) {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        *reinterpret_cast<double2 *>(F0 + q * T + jp) = make_double2(P0[0][q], P0[1][q]);
+                    *reinterpret_cast<double2 *>(M0 + jp) =
+                        make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
+                    if (last && keep1) store3p(V0.RES(), V0.pitch, sp, r[0], r[1]);
+                }
+                if constexpr (N == 3)
+                    if (vq) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) F0[q * T + js] = P0[2][q];
+                        M0[js] = (r[2][0] + r[2][1] + r[2][2]) / 3.;
+                        if (last && keep1) store3(V0.RES(), V0.pitch, sq, r[2]);
+                    }
+#pragma unroll
+                for (int k = 0; k < N; ++k) copy3(X0[k], P0[k]);
+                sweepsN<N>(St0, rdt, ns, B0, X0, P0);   // prolongation-leg call (:376)
+                if constexpr (last) {
+                    if (vp) {
+#pragma unroll
+                        for (int k = 0; k < 2; ++k)
+                            if (keeph) hs_write(true, V0.H, w0, hs_pack(V0.H.hsub[(sp + k) & hmask]), P0[k]);
+                        store3p<PAMG_NT_TS>(V0.T(), V0.pitch, sp, P0[0], P0[1]);
+                        if (keep1) store3p(V0.TNN(), V0.pitch, sp, X0[0], X0[1]);
+                    }
+                    if constexpr (N == 3)
+                        if (vq) {
+                            if (keeph) hs_write(true, V0.H, w0, hs_pack(V0.H.hsub[sq & hmask]), P0[2]);
+                            store3(V0.T(), V0.pitch, sq, P0[2]);
+                            if (keep1) store3(V0.TNN(), V0.pitch, sq, X0[2]);
+                        }
+                }
+                if constexpr (N == 2) {   // level 2: both smoother calls and get_residual
+                    const VLevel &V = A.lv[1];
+                    ST St;
+                    stencil(true, sp1, opaque(gc >> G::lg(1)), St);
+                    if (last && keepc && vc) store3p(V.RHS(), V.pitch, gc, bs[0], bs[1]);
+                    double x[2][3], p[2][3];
+                    copy3(x[0], xs[0]);
+                    copy3(x[1], xs[1]);
+                    sweeps2(St, rdt, ns, bs[0], bs[1], x[0], x[1], p[0], p[1]);
+                    double rr[2][3];
+                    residual(St, rdt, p[0], bs[0], rr[0]);
+                    residual(St, rdt, p[1], bs[1], rr[1]);
+                    if (last && keepc && vc) store3p(V.RES(), V.pitch, gc, rr[0], rr[1]);
+                    if (vc) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q)
+                            *reinterpret_cast<double2 *>(CI + P::F(1) + q * P::nt(1) + 2 * gb) =
+                                make_double2(p[0][q], p[1][q]);
+                        *reinterpret_cast<double2 *>(CI + P::M(1) + 2 * gb) =
+                            make_double2((rr[0][0] + rr[0][1] + rr[0][2]) / 3., (rr[1][0] + rr[1][1] + rr[1][2]) / 3.);
+                    }
+                    copy3(x[0], p[0]);   // tnew_nonlin := tnew (:367)
+                    copy3(x[1], p[1]);
+                    sweeps2(St, rdt, ns, bs[0], bs[1], x[0], x[1], p[0], p[1]);
+                    copy3(xs[0], p[0]);
+                    copy3(xs[1], p[1]);
+                    if (last && vc) store3p(V.T(), V.pitch, gc, xs[0], xs[1]);
+                }
+                __syncthreads();
+                if constexpr (N == 2) {   // level 2's restrictor (:336) and prolongator cascade (:370, dead)
+                    if (vc) {
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) {
+                            const int i = 2 * gb + k;
+                            bs[k][0] = M0[4 * i + 2];
+                            bs[k][1] = M0[4 * i + 3];
+                            bs[k][2] = M0[4 * i];
+                            const int fi[4] = {4 * i, 4 * i + 1, 4 * i + 2, 4 * i + 3};
+                            prolong_cascade(F0, T, fi, xs[k]);
+                        }
+                        if (last) store3p(A.rhsn2, A.lv[1].pitch, gc, bs[0], bs[1]);
+                    }
+                }
+                __syncthreads();
+            };
+            for (int c = 0; c + 1 < m; ++c) cycle(c, std::false_type{});
+            cycle(m - 1, std::true_type{});
+        };
+        if (grpB) level1(std::integral_constant<int, 2>{});
+        else level1(std::integral_constant<int, 3>{});
+    }
+}
+
 // part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
 template <int S, int L, class ST, bool W8>
 hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
@@ -1132,7 +1417,14 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
         else
             return hipErrorInvalidValue;
     } else if (part == 4 || part == 5) {   // the resident call (5: starting a time step)
-        if constexpr (L >= 2 && fine_np(S) == 2) {
+        if constexpr (PAMG_RES_BALANCED && S >= 5 && L >= 3) {
+            if (part == 5)
+                hipLaunchKernelGGL((k_vc_resb<S, L, ST, true>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
+                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+            else
+                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
+                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+        } else if constexpr (L >= 2 && fine_np(S) == 2) {
             if (part == 5)
                 hipLaunchKernelGGL((k_vc_res<S, L, ST, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
                                    A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
