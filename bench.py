@@ -10,14 +10,18 @@ omega = 0.8). One step = one V-cycle of transport_tri_semi.F90:319-379
 (restriction leg, 15 coarse smoother calls, prolongation leg, halo after
 every smoother call) over the whole mesh.
 
-Defaults: the pipelined fused schedule (fused = 3: a call of K cycles is one
-coarse-level launch, K - 1 launches of [level 1 of cycle c + levels 2..L of
-cycle c+1] and one level-1 launch; state identical to the per-step kernel
-sequence, bit for bit) and the contracted operator arithmetic (arith = 1: fma
-rows of A_e = M/dt + Kd; ~1e-15 relative to the reference on the solution, the
-north star's bar being 1e-10). The other schedules and the reference's own
-operation order (arith = 0, bitwise equal to the reference) are timed on the
-same workload and reported under "extra".
+Defaults: the fused V-cycle (fused = 3) in its resident call schedule -- the K
+cycles of a pamg_vcycle(K) call in ONE launch, every tile's state (all levels)
+on-chip between cycles, loaded once and stored once (pamg_vcycle.hip k_vc_resb);
+every sweep, residual, restriction and prolongation of every cycle runs, and the
+state after the call is the per-step kernel sequence's, bit for bit -- and the
+contracted operator arithmetic (arith = 1: fma rows of A_e = M/dt + Kd; ~1e-15
+relative to the reference on the solution, the north star's bar being 1e-10).
+The cycle is then fp64-issue-bound: the roofline is the launch's fp64 operations
+(pamg_vcycle_flops x cycles) over its duration against the 78.6 TFLOP/s fp64
+peak. The other schedules (one HBM-bound launch per cycle: the round-1 form, with
+its HBM roofline), the reference's own operation order (arith = 0, bitwise equal
+to the reference) and the other workloads are timed and reported under "extra".
 
 N > 1 (python -m torch.distributed.run ... bench.py --gpus N): strong scaling
 of the same mesh, x-strip domain decomposition by unstructured element, one
@@ -45,8 +49,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "p-a_multigrids_amd"))
 MESH = os.path.join(ROOT, "tests", "meshes", "untitled8192.msh")
-HBM_PEAK_GBS = 8000.0
-EVENT_STRIDE = 10   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# fp64 peak: MI355X spec FP64 vector 78.6 TFLOP/s (= the FP64 matrix peak; half the guide's 157.3
+# TFLOP/s FP32 vector peak: a wave64 v_fma_f64 issues in 4 cycles per SIMD, 256 CUs x 4 SIMDs x 16
+# lanes x 2 flops x 2.4 GHz)
+FP64_PEAK_TFLOPS = 78.6
+EVENT_STRIDE = 10
+ALL_CLASSES = 0x3F7F   # every timing class (PAMG_K_*) but sweep_bench
 
 
 def parse():
@@ -163,7 +172,9 @@ def pmc_traffic(kernel, nsplit, levels):
     return None
 
 
-RK_DESC = {"vcycle_pipe": "k_vc_fine<.., true> (pipelined fused V-cycle: level 1 of cycle c -- both smoother "
+RK_DESC = {"vcycle_res": "k_vc_resb (resident V-cycle call: all cycles of the call in one launch, every level of a "
+                         "tile on-chip between cycles; fp64-issue-bound)",
+           "vcycle_pipe": "k_vc_fine<.., true> (pipelined fused V-cycle: level 1 of cycle c -- both smoother "
                           "calls, residual, restrictor, prolongator -- and levels 2..L of cycle c+1, per tile)",
            "vcycle": "k_vc_fine (fused V-cycle, level-1 launch: both smoother calls, residual, prolongator; "
                      "the coarse levels run in k_vc_coarse just before it)",
@@ -186,7 +197,7 @@ def measure_time_loop(s):
     s.run(TIME_LOOP_STEPS, 2)
     s.synchronize()
     el = time.perf_counter() - t0
-    s.timing_enable(0xF7F)
+    s.timing_enable(ALL_CLASSES)
     s.timing_stride(1)
     s.timing_reset()
     s.run(TIME_LOOP_STEPS, 2)
@@ -196,11 +207,15 @@ def measure_time_loop(s):
     by = sum(v["bytes"] / v["launches"] * v["issued"] for v in tm.values() if v["launches"]) / TIME_LOOP_STEPS
     kms = sum(v["ms"] for v in tm.values() if v["launches"]) / TIME_LOOP_STEPS
     ms_step = 1e3 * el / TIME_LOOP_STEPS
+    fl = 2 * s.vcycle_flops()
+    # a step moves the state in and out once (HBM) and runs 2 cycles of fp64 work: both rooflines
     out = {"workload": f"pamg_run(ntime={TIME_LOOP_STEPS}, n_multigrid=2): each step begin_timestep + 2 V-cycles "
-                       "(the reference's n_multigrid loop inside its time loop)",
+                       "(the reference's n_multigrid loop inside its time loop), one resident launch per step",
            "vcycles_per_s": round(2 * TIME_LOOP_STEPS / el, 1), "ms_per_step": round(ms_step, 4),
            "alg_bytes_per_step": by, "achieved": round(by / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(by / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "fp64_flops_per_step": fl, "fp64_tflops": round(fl / (ms_step * 1e-3) / 1e12, 2),
+           "fp64_frac": round(fl / (ms_step * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
            "kernel_ms_per_step_evented": round(kms, 4),
            "launches": {k: dict(per_step=round(v["issued"] / TIME_LOOP_STEPS, 2),
                                 ms=round(v["ms"] / v["launches"], 4),
@@ -212,7 +227,7 @@ def measure_time_loop(s):
 
 def measure_workload(pamg, m, S, L, ns, arith, device, cycles=100):
     """V-cycles/s of one pamg_vcycle(cycles) call on mesh m at n_split S (after a warm-up call),
-    and the pipelined launch's roofline from a sampled-event pass"""
+    and its launch's fp64 roofline from an evented pass"""
     s = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=3, device=device, arith=arith, fused=3)
     s.begin_timestep()
     s.vcycle(cycles)
@@ -221,17 +236,19 @@ def measure_workload(pamg, m, S, L, ns, arith, device, cycles=100):
     s.vcycle(cycles)
     s.synchronize()
     v = cycles / (time.perf_counter() - t0)
-    s.timing_enable(0xF7F)
+    s.timing_enable(ALL_CLASSES)
     s.timing_stride(EVENT_STRIDE)
     s.timing_reset()
     s.vcycle(cycles)
     s.synchronize()
-    k = s.timing()["vcycle_pipe"]
+    tm = s.timing()
     out = dict(U=m.U, n_split=S, fine_sub_elements=m.U * 4 ** S, vcycles_per_s=round(v, 1))
+    k = tm["vcycle_res"]
     if k["launches"]:
         ms = k["ms"] / k["launches"]
-        out.update(pipe_ms=round(ms, 4), pipe_alg_bytes=k["bytes"] / k["launches"],
-                   pipe_frac=round(k["bytes"] / k["launches"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+        fl = s.vcycle_flops() * cycles
+        out.update(launch_ms=round(ms, 4), fp64_tflops=round(fl / (ms * 1e-3) / 1e12, 2),
+                   fp64_frac=round(fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4))
     s.close()
     return out
 
@@ -288,7 +305,7 @@ def main():
     # each rank's share of a cycle is ~1/N as long and the events would be a visible part of
     # it, so there they are recorded in a short pass after the timed region
     live_events = world == 1
-    s.timing_enable(0xF7F if live_events else 0)  # every class but sweep_bench
+    s.timing_enable(ALL_CLASSES if live_events else 0)
     # an event pair between back-to-back launches costs ~10 us (~5 % of a cycle): time the
     # first launch of each class and then one in EVENT_STRIDE
     s.timing_stride(EVENT_STRIDE)
@@ -316,22 +333,29 @@ def main():
         # per-launch events time each launch on its own: the post-pass runs the pipelined
         # calls as one launch per cycle (the timed region ran the partition's automatic
         # schedule, two tile streams)
-        s.set_call_schedule(1)
-        s.timing_enable(0xF7F)
+        post = max(1, min(a.steps, 20))
+        resident = a.fused == 3 and a.halo_exchange == 0 and a.levels >= 2
+        if not resident:
+            s.set_call_schedule(1)
+        s.timing_enable(ALL_CLASSES)
         s.timing_reset()
-        s.vcycle(max(1, min(a.steps, 20)))
+        s.vcycle(post)
         s.synchronize()
     tm = s.timing()
     value = a.steps / elapsed
     # dominant kernel by total time inside the timed region
     dom = max((k for k in tm if tm[k]["launches"] > 0 and k != "sweep_bench"), key=lambda k: tm[k]["ms"])
-    # roofline kernel: the fused V-cycle when it ran, else the level-1 smoother
-    rk = next(k for k in ("vcycle_pipe", "vcycle", "smooth_L1") if tm[k]["launches"])
+    # roofline kernel: the resident call when it ran (fp64-bound), else the fused V-cycle's
+    # pipelined launch or the level-1 smoother (HBM-bound)
+    rk = next(k for k in ("vcycle_res", "vcycle_pipe", "vcycle", "smooth_L1") if tm[k]["launches"])
     kinfo = tm[rk]
     ms_per_launch = kinfo["ms"] / max(1, kinfo["launches"])
     bytes_per_launch = kinfo["bytes"] / max(1, kinfo["launches"])
     achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
     traffic = pmc_traffic(rk, a.nsplit, a.levels) if world == 1 else None
+    cycles_per_launch = (a.steps if live_events else post) if rk == "vcycle_res" else 1
+    flops_per_launch = s.vcycle_flops() * cycles_per_launch
+    tflops = flops_per_launch / (ms_per_launch * 1e-3) / 1e12 if ms_per_launch > 0 else 0.0
     extra = {"kernels": {k: dict(ms_total=round(v["ms"], 4), launches=v["launches"], issued=v["issued"],
                                  gbs=round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None)
                          for k, v in tm.items() if v["launches"]},
@@ -343,6 +367,32 @@ def main():
     extra["cycle_alg_gbs"] = round(tot_bytes / elapsed / 1e9, 1)
     extra["comm"] = comm_report(s, world, dist)
     if rank == 0 and world == 1 and not a.no_extra:
+        # the round-1 form on the same workload: one HBM-bound launch per cycle (call schedule 1),
+        # its pipelined launch against the HBM roofline
+        s1 = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
+                                        fused=a.fused, arith=a.arith)
+        s1.set_call_schedule(1)
+        s1.begin_timestep()
+        s1.vcycle(a.warmup)
+        s1.synchronize()
+        t0 = time.perf_counter()
+        s1.vcycle(a.steps)
+        s1.synchronize()
+        v1 = a.steps / (time.perf_counter() - t0)
+        s1.timing_enable(ALL_CLASSES)
+        s1.timing_stride(EVENT_STRIDE)
+        s1.timing_reset()
+        s1.vcycle(a.steps)
+        s1.synchronize()
+        kp = s1.timing()["vcycle_pipe"]
+        if kp["launches"]:
+            msp = kp["ms"] / kp["launches"]
+            bp = kp["bytes"] / kp["launches"]
+            extra["one_launch_per_cycle"] = dict(
+                vcycles_per_s=round(v1, 1), pipe_ms=round(msp, 4), pipe_alg_bytes=bp,
+                pipe_gbs=round(bp / (msp * 1e-3) / 1e9, 1), pipe_frac=round(bp / (msp * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                pipe_traffic=pmc_traffic("vcycle_pipe", a.nsplit, a.levels))
+        s1.close()
         for asm in (False, True):
             ms, by = s.sweep_bench(20, asm)
             extra["sweep_assembled" if asm else "sweep_stencil"] = dict(
@@ -451,13 +501,23 @@ def main():
                        "arith": "contracted (fma, 1e-15 of the reference)" if a.arith else "reference order (bitwise)",
                        "fused": a.fused, "halo_exchange": "per call" if a.halo_exchange == 0 else "per cycle",
                        "comm": a.comm if world > 1 else None,
-                       "call_schedule": "two tile streams" if world > 1 else "one launch per cycle"},
-            "roofline": {"bound": "hbm", "kernel": RK_DESC[rk],
-                         "events": (f"timed region, the first and then 1 in {EVENT_STRIDE} launches" if live_events
-                                    else "post-pass of min(steps, 20) cycles, one launch per cycle"),
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "alg_bytes_per_launch": bytes_per_launch, "ms_per_launch": round(ms_per_launch, 4)},
+                       "call_schedule": ("resident (the call's cycles in one launch)" if rk == "vcycle_res" else
+                                         "two tile streams" if world > 1 else "one launch per cycle")},
+            "roofline": ({"bound": "fp64-valu", "kernel": RK_DESC[rk],
+                          "events": (f"timed region (the call is one launch)" if live_events
+                                     else f"post-pass of one call of {post} cycles"),
+                          "achieved": round(tflops, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(tflops / FP64_PEAK_TFLOPS, 4), "traffic": traffic,
+                          "fp64_flops_per_launch": flops_per_launch, "cycles_per_launch": cycles_per_launch,
+                          "alg_bytes_per_launch": bytes_per_launch, "hbm_gbs": round(achieved, 1),
+                          "ms_per_launch": round(ms_per_launch, 4)}
+                         if rk == "vcycle_res" else
+                         {"bound": "hbm", "kernel": RK_DESC[rk],
+                          "events": (f"timed region, the first and then 1 in {EVENT_STRIDE} launches" if live_events
+                                     else "post-pass of min(steps, 20) cycles, one launch per cycle"),
+                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                          "alg_bytes_per_launch": bytes_per_launch, "ms_per_launch": round(ms_per_launch, 4)}),
             "cpu_baseline": ({k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")} if cpu else None),
             "time_loop": time_loop,
             "extra": extra,
