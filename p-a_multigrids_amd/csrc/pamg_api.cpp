@@ -679,11 +679,12 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
     // 0.0128 -> 0.0114, full mesh 0.1319 -> 0.1290. Automatic on partitions only: on one GPU
     // the bench's per-launch events time launches, which schedule 2 overlaps.
     //
-    // pamg_set_call_schedule(h, s): 0 automatic (2 on a partition of a multi-rank run, 1 on
-    // one GPU), 1 one launch per cycle, 2 two tile streams; PAMG_CALL_SCHEDULE=<s> overrides
-    // for A/B runs. (A persistent form -- one launch whose workgroups loop over their tile's
-    // cycles -- was tried: the loop pushed the launch from 62 to 128 VGPRs with spills, and
-    // it is not kept.)
+    // pamg_set_call_schedule(h, s): 0 automatic (3 where it applies, else 2 on a partition of
+    // a multi-rank run, 1 on one GPU), 1 one launch per cycle, 2 two tile streams, 3 resident
+    // (below); PAMG_CALL_SCHEDULE=<s> overrides for A/B runs. (Round 1 tried a persistent
+    // form of the pipelined launch and dropped it at 128 VGPRs with spills; the resident form
+    // fits -- its final-cycle stores are peeled out of the cycle loop and its loop is
+    // unswitched by wave role, pamg_vcycle.hip k_vc_res / k_vc_resb.)
     const int tile = vcycle_tile_un_eles(h->p.n_split);
     const int ntiles = (h->U + tile - 1) / tile;
     const int sched = call_schedule(h);

@@ -30,6 +30,10 @@
 //   restrictor of its residual into level 2's RHSN, and the prolongator cascade
 //   from the final level-2 tnew; a streaming kernel (tnew, RHS in; residual,
 //   tnew, tnew_nonlin out).
+// The pipelined form runs level 1 of cycle c and the coarse levels of cycle c+1 in
+// one launch (k_vc_fine<.., PIPE>); the resident form (k_vc_res, k_vc_resb, the
+// default) runs every cycle of a pamg_vcycle call in one launch with the tiles'
+// state on-chip between cycles.
 // Levels are 0-based inside this file: level 0 = the reference's level 1.
 #include <hip/hip_runtime.h>
 
