@@ -41,6 +41,25 @@ __device__ __forceinline__ void st2(double *p, double2 v) {
 // M = c [[2,1,1],[1,2,1],[1,1,2]] with c = detwei / 4 (every product N_gi w_g N_gj is
 // 0 or 0.25 detwei, detwei equal at the three points of an affine element); the host
 // checks this bit for bit (level_stencil). The kernels therefore keep c, not M.
+// RN(x / 3) without a division -- the restrictor's mean of three residual components
+// (splitting.F90:146-151): q0 = RN(x t) with t = RN(1/3) is within 1 ulp of x / 3, the remainder
+// x - 3 q0 is exact in one fma, and one fma correction q0 + r t gives the correctly rounded
+// quotient (Markstein's theorem). Outside 2^-1000 <= |x| <= 2^1000 (zeros, subnormals, huge
+// values, inf, NaN) it divides. Bitwise x / 3 (scripts/micro/div3_check.c, profiles/r02_div3_check.txt: 2.0e10 values of
+// every exponent, 0 differences), in 5 instructions instead of the division's ~10.
+#ifndef PAMG_DIV3
+#define PAMG_DIV3 1
+#endif
+__device__ __forceinline__ double div3(double x) {
+    if (!PAMG_DIV3) return x / 3.0;   // A/B builds
+    const double a = __builtin_fabs(x);
+    if (__builtin_expect(!(a >= 0x1p-1000 && a <= 0x1p+1000), 0)) return x / 3.0;
+    const double t = 1.0 / 3.0;
+    const double q0 = x * t;
+    const double r = __builtin_fma(-3.0, q0, x);
+    return __builtin_fma(r, t, q0);
+}
+
 struct Stc {
     double c, K[9], w[3];
 };

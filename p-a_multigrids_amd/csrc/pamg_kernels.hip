@@ -329,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void k_restrict_tile(const double *__restri
         const int pick[3] = {4 * cc + 2, 4 * cc + 3, 4 * cc};   // children 3, 4, 1 (splitting.F90:26-28)
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-            RHSc[i * pitch_c + c0 + cc] = (lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]) / 3.;
+            RHSc[i * pitch_c + c0 + cc] = div3(lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]);
     }
 }
 
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void k_restrict_residual(const double *__re
         const int pick[3] = {4 * cc + 2, 4 * cc + 3, 4 * cc};
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-            RHSc[i * pitch_c + c0 + cc] = (lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]) / 3.;
+            RHSc[i * pitch_c + c0 + cc] = div3(lds[pick[i]] + lds[TF + pick[i]] + lds[2 * TF + pick[i]]);
     }
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {

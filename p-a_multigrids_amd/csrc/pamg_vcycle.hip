@@ -482,7 +482,7 @@ __global__ __launch_bounds__(kMTc, 3) void k_vc_coarse(VArgs A, const double *__
                 const int i = t + 64 * Q::kk(j);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) lds[Q::F(l) + c * Q::nt(l) + i] = p[j][c];
-                lds[Q::M(l) + i] = (r[0] + r[1] + r[2]) / 3.;
+                lds[Q::M(l) + i] = div3(r[0] + r[1] + r[2]);
             }
         }
         copy3(x[j], p[j]);   // tnew_nonlin := tnew (:348 coarsest, :367 the others)
@@ -695,7 +695,7 @@ __device__ __forceinline__ void coarse_next(const VArgs &A, const double *__rest
             if (v) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c) lds[P::F(l) + c * P::nt(l) + i] = p[c];
-                lds[P::M(l) + i] = (r[0] + r[1] + r[2]) / 3.;
+                lds[P::M(l) + i] = div3(r[0] + r[1] + r[2]);
             }
         }
         copy3(x, p);   // tnew_nonlin := tnew (:348 coarsest, :367 the others)
@@ -822,13 +822,13 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
             if (keep1) store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
             if constexpr (C > 0)   // restrictor input: mean of the residual components (splitting.F90:146-151)
                 *reinterpret_cast<double2 *>(M0 + 2 * t) =
-                    make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
+                    make_double2(div3(r[0][0] + r[0][1] + r[0][2]), div3(r[1][0] + r[1][1] + r[1][2]));
         } else {
             if constexpr (C > 0)
 #pragma unroll
                 for (int c = 0; c < 3; ++c) F0[c * T + t] = p0[0][c];
             if (keep1) store3(V0.RES(), V0.pitch, s0, r[0]);
-            if constexpr (C > 0) M0[t] = (r[0][0] + r[0][1] + r[0][2]) / 3.;
+            if constexpr (C > 0) M0[t] = div3(r[0][0] + r[0][1] + r[0][2]);
         }
     }
     stamp<MT>(A, 2);
@@ -925,6 +925,12 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 // n_split >= 5, L >= 3: the balanced-role instance k_vc_resb (A/B builds: 0 keeps k_vc_res)
 #ifndef PAMG_RES_BALANCED
 #define PAMG_RES_BALANCED 1
+#endif
+// k_vc_resb A/B: level 2 all on waves 6,7 (0) or half of it on wave 0 (1, fewer VGPRs at the same
+// occupancy: measured equal, profiles/r02_res_ab_variants.txt). (A prolongator cascade sequenced
+// by scheduling barriers to cut the VGPR peak further measured 15 % slower and is not kept.)
+#ifndef PAMG_RES_L2W0
+#define PAMG_RES_L2W0 0
 #endif
 template <int S, int L>
 struct RGeo {
@@ -1052,7 +1058,7 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
                 *reinterpret_cast<double2 *>(F0 + q * T + 2 * t) = make_double2(p0[0][q], p0[1][q]);
             if (last && keep1) store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
             *reinterpret_cast<double2 *>(M0 + 2 * t) =
-                make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
+                make_double2(div3(r[0][0] + r[0][1] + r[0][2]), div3(r[1][0] + r[1][1] + r[1][2]));
         }
 #pragma unroll
         for (int k = 0; k < NP; ++k) copy3(x0[k], p0[k]);
@@ -1081,7 +1087,7 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             if (vc) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) CI[P::F(l) + q * P::nt(l) + ic] = p[q];
-                CI[P::M(l) + ic] = (r[0] + r[1] + r[2]) / 3.;
+                CI[P::M(l) + ic] = div3(r[0] + r[1] + r[2]);
             }
             copy3(x, p);   // tnew_nonlin := tnew (:367)
             sweeps1(St, rdt, ns, bs, x, p);
@@ -1117,11 +1123,13 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
 // waves w and w+4 of a 512-thread workgroup on one SIMD, scripts/micro/wave_simd.hip), which
 // also carries level-2 work: that SIMD had ~2.3x the issue of the others and set the pace.
 // Here a tile's issue is split evenly over its four SIMDs:
-//   wave 4      the coarsest level alone (its SIMD partner, wave 0, has the levels 3..L-1);
+//   wave 4      the coarsest level alone;
+//   wave 0      level 2: sub-elements 128..255, two per thread; the levels 3..L-1;
 //   waves 1,2,3,5  level 1: an adjacent pair and a single sub-element per thread (768);
-//   waves 6,7   level 1: an adjacent pair per thread (256), and level 2: two sub-elements each.
-// Per tile-cycle (n_split 5, L 3): SIMD(0,4) 64 sweeps on one wave; SIMD(1,5) 6, SIMD(2,6) and
-// SIMD(3,7) 7 sub-element units of 2 smoother calls each. Every sub-element's operations are
+//   waves 6,7   level 1: an adjacent pair per thread (256), and level 2: sub-elements 0..127.
+// Per tile-cycle (n_split 5, L 3), in units of 64 sub-elements x 2 smoother calls: SIMD(0,4)
+// 64 sweeps on one wave (~5.4) + 2; SIMD(1,5) 6; SIMD(2,6), SIMD(3,7) 3 + 2 + 1. No thread holds
+// two level-2 sub-elements beside its level-1 state (118 -> fewer VGPRs). Every sub-element's operations are
 // the same as in every other form (bitwise, the same tests). A tile is one un_ele or a part of
 // one (n_split >= 5), so every operator record is wave-uniform and every tile full.
 template <int S, int L, class ST, bool RHSF>
@@ -1147,6 +1155,87 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
     // Each role runs its own cycle loop with its own state (the loop is unswitched by role, so
     // the registers of one role's loop-carried state are not reserved in the others); every
     // role passes the same two barriers per cycle.
+    //
+    // level 2 (0-based 1), K = 1 or 2 adjacent sub-elements i0 .. i0+K-1 of the tile: load (tnew,
+    // and the RHS: RHSN), both smoother calls + get_residual + LDS images (before the cycle's
+    // barrier), restrictor + prolongator cascade (after it)
+    auto l2_load = [&](auto kc, int i0, double (&xs)[2][3], double (&bs)[2][3], uint32_t &gc, bool &vc) {
+        constexpr int K = decltype(kc)::value;
+        const VLevel &V = A.lv[1];
+        gc = tile_index<S>(A, tb, P::nt(1), 1, i0, vc);
+        if constexpr (K == 2) {
+            load3p(V.T(), V.pitch, gc, xs[0], xs[1]);
+            load3p(A.rhsn2, V.pitch, gc, bs[0], bs[1]);
+        } else {
+            load3(V.T(), V.pitch, gc, xs[0]);
+            load3(A.rhsn2, V.pitch, gc, bs[0]);
+        }
+    };
+    auto l2_legs = [&](auto kc, auto lastc, int i0, double (&xs)[2][3], const double (&bs)[2][3], uint32_t gc,
+                       bool vc) {
+        constexpr int K = decltype(kc)::value;
+        constexpr bool last = decltype(lastc)::value;
+        const VLevel &V = A.lv[1];
+        ST St;
+        stencil(true, sp1, opaque(gc >> G::lg(1)), St);
+        double x[2][3], p[2][3], rr[2][3];
+        if constexpr (K == 2) {
+            if (last && keepc && vc) store3p(V.RHS(), V.pitch, gc, bs[0], bs[1]);
+            copy3(x[0], xs[0]);
+            copy3(x[1], xs[1]);
+            sweeps2(St, rdt, ns, bs[0], bs[1], x[0], x[1], p[0], p[1]);
+        } else {
+            if (last && keepc && vc) store3(V.RHS(), V.pitch, gc, bs[0]);
+            copy3(x[0], xs[0]);
+            sweeps1(St, rdt, ns, bs[0], x[0], p[0]);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) residual(St, rdt, p[k], bs[k], rr[k]);
+        if (vc) {
+            if constexpr (K == 2) {
+                if (last && keepc) store3p(V.RES(), V.pitch, gc, rr[0], rr[1]);
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    *reinterpret_cast<double2 *>(CI + P::F(1) + q * P::nt(1) + i0) = make_double2(p[0][q], p[1][q]);
+                *reinterpret_cast<double2 *>(CI + P::M(1) + i0) =
+                    make_double2(div3(rr[0][0] + rr[0][1] + rr[0][2]), div3(rr[1][0] + rr[1][1] + rr[1][2]));
+            } else {
+                if (last && keepc) store3(V.RES(), V.pitch, gc, rr[0]);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) CI[P::F(1) + q * P::nt(1) + i0] = p[0][q];
+                CI[P::M(1) + i0] = div3(rr[0][0] + rr[0][1] + rr[0][2]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) copy3(x[k], p[k]);   // tnew_nonlin := tnew (:367)
+        if constexpr (K == 2) sweeps2(St, rdt, ns, bs[0], bs[1], x[0], x[1], p[0], p[1]);
+        else sweeps1(St, rdt, ns, bs[0], x[0], p[0]);
+#pragma unroll
+        for (int k = 0; k < K; ++k) copy3(xs[k], p[k]);
+        if (last && vc) {
+            if constexpr (K == 2) store3p(V.T(), V.pitch, gc, xs[0], xs[1]);
+            else store3(V.T(), V.pitch, gc, xs[0]);
+        }
+    };
+    auto l2_restrict = [&](auto kc, auto lastc, int i0, const double (&xs)[2][3], double (&bs)[2][3], uint32_t gc,
+                           bool vc) {
+        constexpr int K = decltype(kc)::value;
+        constexpr bool last = decltype(lastc)::value;
+        if (!vc) return;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {   // level 2's restrictor (:336) and prolongator cascade (:370, dead)
+            const int i = i0 + k;
+            bs[k][0] = M0[4 * i + 2];
+            bs[k][1] = M0[4 * i + 3];
+            bs[k][2] = M0[4 * i];
+            const int fi[4] = {4 * i, 4 * i + 1, 4 * i + 2, 4 * i + 3};
+            prolong_cascade(F0, T, fi, xs[k]);
+        }
+        if (last) {
+            if constexpr (K == 2) store3p(A.rhsn2, A.lv[1].pitch, gc, bs[0], bs[1]);
+            else store3(A.rhsn2, A.lv[1].pitch, gc, bs[0]);
+        }
+    };
     if (wv == 4) {
         // ---- the coarsest level: its restriction-leg call, get_residual, 1 + n_coarse calls
         const VLevel &V = A.lv[C];
@@ -1188,7 +1277,13 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
         for (int c = 0; c + 1 < m; ++c) cycle(std::false_type{});
         cycle(std::true_type{});
     } else if (wv == 0) {
-        // ---- levels 3 .. L-1 (1-based), one sub-element of each per lane (none with L = 3)
+        // ---- level 2: sub-elements 128 + 2 lane, +1; levels 3 .. L-1 (1-based), one sub-element
+        //      of each per lane (none with L = 3)
+        const int i2 = 128 + 2 * lane;
+        double x2[2][3], b2[2][3];
+        uint32_t g2 = 0;
+        bool v2 = false;
+        if (PAMG_RES_L2W0) l2_load(std::integral_constant<int, 2>{}, i2, x2, b2, g2, v2);
         double xs[2][3] = {}, bs[2][3] = {};
         uint32_t gc[2] = {0, 0};
         bool vc[2] = {false, false};
@@ -1202,6 +1297,7 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
         const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
         auto cycle = [&](auto lastc) {
             constexpr bool last = decltype(lastc)::value;
+            if (PAMG_RES_L2W0) l2_legs(std::integral_constant<int, 2>{}, lastc, i2, x2, b2, g2, v2);
             static_for<2, C>([&](auto lc) {
                 constexpr int l = decltype(lc)::value, k = l - 2;
                 const VLevel &V = A.lv[l];
@@ -1217,7 +1313,7 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                 if (vc[k]) {
 #pragma unroll
                     for (int q = 0; q < 3; ++q) CI[P::F(l) + q * P::nt(l) + lane] = p[q];
-                    CI[P::M(l) + lane] = (r[0] + r[1] + r[2]) / 3.;
+                    CI[P::M(l) + lane] = div3(r[0] + r[1] + r[2]);
                 }
                 copy3(x, p);   // tnew_nonlin := tnew (:367)
                 sweeps1(St, rdt, ns, bs[k], x, p);
@@ -1225,6 +1321,7 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                 if (last && vc[k]) store3(V.T(), V.pitch, gc[k], xs[k]);
             });
             __syncthreads();
+            if (PAMG_RES_L2W0) l2_restrict(std::integral_constant<int, 2>{}, lastc, i2, x2, b2, g2, v2);
             static_for<2, C>([&](auto lc) {
                 constexpr int l = decltype(lc)::value, k = l - 2;
                 if (!vc[k]) return;
@@ -1242,7 +1339,7 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
         cycle(std::true_type{});
     } else {
         // ---- level 1 (the reference's): waves 1,2,3,5 an adjacent pair + a single sub-element
-        //      per thread (N = 3), waves 6,7 a pair (N = 2) and two sub-elements of level 2
+        //      per thread (N = 3), waves 6,7 a pair (N = 2) and one sub-element of level 2
         const bool grpB = wv >= 6;
         const VLevel &V0 = A.lv[0];
         constexpr int hmask = (1 << G::lg(0)) - 1;
@@ -1291,16 +1388,13 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                     load3(V0.RHS(), V0.pitch, sq, B0[2]);
                 }
             }
-            // level 2 (0-based 1), group B: sub-elements 2 gb, 2 gb + 1 (RHS: RHSN)
+            // level 2 (0-based 1), group B: sub-element gb (wave 0 has 128 .. 255)
             double xs[2][3], bs[2][3];
             bool vc = false;
             uint32_t gc = 0;
-            if constexpr (N == 2) {
-                const VLevel &V = A.lv[1];
-                gc = tile_index<S>(A, tb, P::nt(1), 1, 2 * gb, vc);
-                load3p(V.T(), V.pitch, gc, xs[0], xs[1]);
-                load3p(A.rhsn2, V.pitch, gc, bs[0], bs[1]);
-            }
+            constexpr int K2 = PAMG_RES_L2W0 ? 1 : 2;   // level-2 sub-elements of the thread
+            const int i2 = PAMG_RES_L2W0 ? gb : 2 * gb;
+            if constexpr (N == 2) l2_load(std::integral_constant<int, K2>{}, i2, xs, bs, gc, vc);
             auto cycle = [&](int c, auto lastc) {
                 constexpr bool last = decltype(lastc)::value;
                 ST St0;
@@ -1318,14 +1412,14 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                     for (int q = 0; q < 3; ++q)
                         *reinterpret_cast<double2 *>(F0 + q * T + jp) = make_double2(P0[0][q], P0[1][q]);
                     *reinterpret_cast<double2 *>(M0 + jp) =
-                        make_double2((r[0][0] + r[0][1] + r[0][2]) / 3., (r[1][0] + r[1][1] + r[1][2]) / 3.);
+                        make_double2(div3(r[0][0] + r[0][1] + r[0][2]), div3(r[1][0] + r[1][1] + r[1][2]));
                     if (last && keep1) store3p(V0.RES(), V0.pitch, sp, r[0], r[1]);
                 }
                 if constexpr (N == 3)
                     if (vq) {
 #pragma unroll
                         for (int q = 0; q < 3; ++q) F0[q * T + js] = P0[2][q];
-                        M0[js] = (r[2][0] + r[2][1] + r[2][2]) / 3.;
+                        M0[js] = div3(r[2][0] + r[2][1] + r[2][2]);
                         if (last && keep1) store3(V0.RES(), V0.pitch, sq, r[2]);
                     }
 #pragma unroll
@@ -1346,49 +1440,9 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                             if (keep1) store3(V0.TNN(), V0.pitch, sq, X0[2]);
                         }
                 }
-                if constexpr (N == 2) {   // level 2: both smoother calls and get_residual
-                    const VLevel &V = A.lv[1];
-                    ST St;
-                    stencil(true, sp1, opaque(gc >> G::lg(1)), St);
-                    if (last && keepc && vc) store3p(V.RHS(), V.pitch, gc, bs[0], bs[1]);
-                    double x[2][3], p[2][3];
-                    copy3(x[0], xs[0]);
-                    copy3(x[1], xs[1]);
-                    sweeps2(St, rdt, ns, bs[0], bs[1], x[0], x[1], p[0], p[1]);
-                    double rr[2][3];
-                    residual(St, rdt, p[0], bs[0], rr[0]);
-                    residual(St, rdt, p[1], bs[1], rr[1]);
-                    if (last && keepc && vc) store3p(V.RES(), V.pitch, gc, rr[0], rr[1]);
-                    if (vc) {
-#pragma unroll
-                        for (int q = 0; q < 3; ++q)
-                            *reinterpret_cast<double2 *>(CI + P::F(1) + q * P::nt(1) + 2 * gb) =
-                                make_double2(p[0][q], p[1][q]);
-                        *reinterpret_cast<double2 *>(CI + P::M(1) + 2 * gb) =
-                            make_double2((rr[0][0] + rr[0][1] + rr[0][2]) / 3., (rr[1][0] + rr[1][1] + rr[1][2]) / 3.);
-                    }
-                    copy3(x[0], p[0]);   // tnew_nonlin := tnew (:367)
-                    copy3(x[1], p[1]);
-                    sweeps2(St, rdt, ns, bs[0], bs[1], x[0], x[1], p[0], p[1]);
-                    copy3(xs[0], p[0]);
-                    copy3(xs[1], p[1]);
-                    if (last && vc) store3p(V.T(), V.pitch, gc, xs[0], xs[1]);
-                }
+                if constexpr (N == 2) l2_legs(std::integral_constant<int, K2>{}, lastc, i2, xs, bs, gc, vc);
                 __syncthreads();
-                if constexpr (N == 2) {   // level 2's restrictor (:336) and prolongator cascade (:370, dead)
-                    if (vc) {
-#pragma unroll
-                        for (int k = 0; k < 2; ++k) {
-                            const int i = 2 * gb + k;
-                            bs[k][0] = M0[4 * i + 2];
-                            bs[k][1] = M0[4 * i + 3];
-                            bs[k][2] = M0[4 * i];
-                            const int fi[4] = {4 * i, 4 * i + 1, 4 * i + 2, 4 * i + 3};
-                            prolong_cascade(F0, T, fi, xs[k]);
-                        }
-                        if (last) store3p(A.rhsn2, A.lv[1].pitch, gc, bs[0], bs[1]);
-                    }
-                }
+                if constexpr (N == 2) l2_restrict(std::integral_constant<int, K2>{}, lastc, i2, xs, bs, gc, vc);
                 __syncthreads();
             };
             for (int c = 0; c + 1 < m; ++c) cycle(c, std::false_type{});

@@ -7,7 +7,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 name=$1
 shift
 tmp=$(mktemp -d /tmp/pamg_ab_XXXX)
-cp -r "$ROOT/p-a_multigrids_amd" "$ROOT/include" "$ROOT/examples" "$tmp/"
+cp -r "$ROOT/p-a_multigrids_amd" "$ROOT/include" "$tmp/"
 cd "$tmp/p-a_multigrids_amd"
 rm -rf build pamg/libpamg.so
 make -j8 pamg/libpamg.so HIPCC="/opt/rocm/bin/hipcc $*" > "$tmp/build.log" 2>&1
