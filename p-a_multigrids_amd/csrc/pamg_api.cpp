@@ -633,7 +633,9 @@ int call_schedule(pamg_handle *h) {
 // residual, the halo words -- before any read (nothing reads t_overlap, the next step's first
 // restrictor reads level 2's RHSN, which is stored), so the pipelined schedule skips them
 // and the exchange of the halo words too
-int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
+// steps > 1: the resident schedule runs `steps` time steps of n cycles in one launch (pamg_run;
+// the call starts the first step, rhs_pending)
+int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     const double rdt = 1 / h->p.dt;
     HaloPlan &P1 = h->lv[1].halo;
@@ -691,6 +693,11 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
     // schedule 3, resident: the call's n cycles in one launch (pamg_vcycle.hip k_vc_res), every
     // tile's state on-chip between them; the final-cycle stores as the pipelined schedule makes
     // them (the call's last launch stores all, or inside pamg_run the fields the next step reads)
+    if (steps > 1 && !(pipe && n >= 1 && sched == 3 && h->p.halo_exchange == 0 && !h->coarse_ahead && rhs_first &&
+                       vcycle_resident_run_supported(h->p.n_split, L))) {
+        h->err = "internal: a resident run outside the resident schedule";
+        return PAMG_ERR_STATE;
+    }
     if (pipe && n >= 1 && sched == 3 && h->p.halo_exchange == 0 && !h->coarse_ahead &&
         vcycle_resident_supported(h->p.n_split, L)) {
         const int buf = two ? 1 - P1.send_cur : 0;
@@ -706,7 +713,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after) {
             Span sp(h, rhsf ? PAMG_K_VCYCLE_RES_RHSF : PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, rhsf));
             HIPCHK(h, launch_vcycle_resident(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
                                              h->tovo, P1.send_buf(buf), L2.RHSN, keep, rhsf,
-                                             two ? P1.send_buf(1 - buf) : nullptr, n));
+                                             two ? P1.send_buf(1 - buf) : nullptr, n, steps));
         }
         if (rhsf) {
             h->overlap_static_l1 = kt != 0;
@@ -1310,6 +1317,26 @@ int pamg_block_inverse(pamg_handle *h, int n, long nb, const double *A, double *
 
 int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
     if (!h || ntime < 0 || n_multigrid < 0) return PAMG_ERR_ARG;
+    {
+        // the resident schedule runs the whole loop as one launch: a step touches only its own
+        // tiles (told := tnew, the RHS from it and s', n_multigrid cycles), so every tile goes
+        // through all ntime steps on-chip and only the run's final state is stored
+        const int L = h->p.multi_levels;
+        if (ntime >= 2 && n_multigrid >= 1 && h->p.cycle == 0 && h->p.fused == 3 && h->p.coarse_solver == 0 &&
+            h->p.op == 0 && h->p.halo_exchange == 0 && !h->coarse_ahead && call_schedule(h) == 3 &&
+            vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth) &&
+            vcycle_resident_run_supported(h->p.n_split, L) && vcycle_rhsf_supported(h->p.n_split) &&
+            !PAMG_RHS_TOLD_HALO && getenv("PAMG_NO_RHS_FUSION") == nullptr && getenv("PAMG_NO_RESIDENT_RUN") == nullptr) {
+            int rc = begin_timestep(h, true, true, true);
+            if (rc == PAMG_OK) rc = vcycle_fused(h, n_multigrid, false, ntime);
+            if (rc != PAMG_OK) {
+                h->coarse_ahead = false;
+                h->rhs_pending = false;
+                return rc;
+            }
+            return comm_error(h);
+        }
+    }
     for (int t = 0; t < ntime; ++t) {
         const int L = h->p.multi_levels;
         const bool fused_next = n_multigrid > 0 && h->p.cycle == 0 && h->p.fused && h->p.coarse_solver == 0 && h->p.op == 0 &&

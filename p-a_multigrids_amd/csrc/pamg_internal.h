@@ -248,10 +248,13 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
 // the resident form: all `cycles` cycles of a call in one launch, every level's state on-chip
 // between them (first coarse cycle included: level 2's RHS from rhsn2); the final-cycle
 // stores as keep says; rhsf: the launch starts the time step (as launch_vcycle_fine's)
+// steps > 1 (rhsf): a whole pamg_run -- `steps` time steps of `cycles` cycles, each step starting
+// with told := tnew and its RHS -- in one launch (vcycle_resident_run_supported)
 hipError_t launch_vcycle_resident(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                   int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                                  int keep, bool rhsf, double *send_b, int cycles);
+                                  int keep, bool rhsf, double *send_b, int cycles, int steps = 1);
 bool vcycle_resident_supported(int n_split, int L);
+bool vcycle_resident_run_supported(int n_split, int L);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const Level &L, const double *aos, double *soa);
 // FINDInv (matrix_inversion.F90:50-148) batched, n <= 8, column-major (n, n, nb)

@@ -128,7 +128,9 @@ struct VArgs {
     // RHSF launches (the first of a pamg_run step, told := tnew and level 1's RHS from it) with
     // kKeepTold: the second send buffer, whose told halves it writes too
     double *send_b;
-    int cycles;             // the resident launch: cycles of the call
+    int cycles;             // the resident launch: cycles of the call (of each time step)
+    int steps;              // the resident launch starting time steps (RHSF): steps of the run, each
+                            // told := tnew and its RHS, then `cycles` cycles; 1 otherwise
 };
 
 // Stores of a pipelined launch whose values the rest of the call overwrites before any read
@@ -1274,7 +1276,7 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             }
             __syncthreads();
         };
-        for (int c = 0; c + 1 < m; ++c) cycle(std::false_type{});
+        for (int c = 0; c + 1 < A.steps * m; ++c) cycle(std::false_type{});
         cycle(std::true_type{});
     } else if (wv == 0) {
         // ---- level 2: sub-elements 128 + 2 lane, +1; levels 3 .. L-1 (1-based), one sub-element
@@ -1335,7 +1337,7 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             });
             __syncthreads();
         };
-        for (int c = 0; c + 1 < m; ++c) cycle(std::false_type{});
+        for (int c = 0; c + 1 < A.steps * m; ++c) cycle(std::false_type{});
         cycle(std::true_type{});
     } else {
         // ---- level 1 (the reference's): waves 1,2,3,5 an adjacent pair + a single sub-element
@@ -1352,34 +1354,43 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             const uint32_t sq = N == 3 ? tile_index<S>(A, tb, T, 0, js, vq) : 0u;
             const uint32_t w0 = sp >> G::lg(0);   // the tile's un_ele
             double X0[N][3], B0[N][3], P0[N][3];
-            if constexpr (RHSF) {   // the start of a time step (:316-317, get_RHS :452-464)
-                double q[N][3];
+            double Q[RHSF ? N : 1][3];   // RHSF: the source s' of every step's RHS
+            // the start of a time step (:316-317, get_RHS :452-464): told := tnew (X0 holds it) and
+            // the RHS from it and s'; the run's last step stores told, the step's constant halo
+            // words (kKeepTold) and the RHS it formed (kKeepL1) -- earlier steps' are overwritten
+            auto start_step = [&](bool last_step) {
+                if constexpr (RHSF) {
+                    const double c = sp0[(size_t)__builtin_amdgcn_readfirstlane(w0) * kStcStride + kStcC];
+#pragma unroll
+                    for (int k = 0; k < N; ++k) rhs_from_source(c, rdt, X0[k], Q[k], B0[k]);
+                    if (!last_step) return;
+                    if (vp) {
+                        if (A.keep & kKeepTold) {
+                            store3p(V0.TOLD(), V0.pitch, sp, X0[0], X0[1]);
+#pragma unroll
+                            for (int k = 0; k < 2; ++k)
+                                hs_write_static(V0.H, A.send_b, w0, hs_pack(V0.H.hsub[(sp + k) & hmask]), X0[k]);
+                        }
+                        if (keep1) store3p(V0.RHS(), V0.pitch, sp, B0[0], B0[1]);
+                    }
+                    if constexpr (N == 3)
+                        if (vq) {
+                            if (A.keep & kKeepTold) {
+                                store3(V0.TOLD(), V0.pitch, sq, X0[2]);
+                                hs_write_static(V0.H, A.send_b, w0, hs_pack(V0.H.hsub[sq & hmask]), X0[2]);
+                            }
+                            if (keep1) store3(V0.RHS(), V0.pitch, sq, B0[2]);
+                        }
+                }
+            };
+            if constexpr (RHSF) {
                 load3p<PAMG_NT_TL>(V0.T(), V0.pitch, sp, X0[0], X0[1]);
-                load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, sp, q[0], q[1]);
+                load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, sp, Q[0], Q[1]);
                 if constexpr (N == 3) {
                     load3(V0.T(), V0.pitch, sq, X0[2]);
-                    load3(V0.SRC(), V0.pitch, sq, q[2]);
+                    load3(V0.SRC(), V0.pitch, sq, Q[2]);
                 }
-                const double c = sp0[(size_t)__builtin_amdgcn_readfirstlane(w0) * kStcStride + kStcC];
-#pragma unroll
-                for (int k = 0; k < N; ++k) rhs_from_source(c, rdt, X0[k], q[k], B0[k]);
-                if (vp) {
-                    if (A.keep & kKeepTold) {
-                        store3p(V0.TOLD(), V0.pitch, sp, X0[0], X0[1]);
-#pragma unroll
-                        for (int k = 0; k < 2; ++k)
-                            hs_write_static(V0.H, A.send_b, w0, hs_pack(V0.H.hsub[(sp + k) & hmask]), X0[k]);
-                    }
-                    if (keep1) store3p(V0.RHS(), V0.pitch, sp, B0[0], B0[1]);
-                }
-                if constexpr (N == 3)
-                    if (vq) {
-                        if (A.keep & kKeepTold) {
-                            store3(V0.TOLD(), V0.pitch, sq, X0[2]);
-                            hs_write_static(V0.H, A.send_b, w0, hs_pack(V0.H.hsub[sq & hmask]), X0[2]);
-                        }
-                        if (keep1) store3(V0.RHS(), V0.pitch, sq, B0[2]);
-                    }
+                start_step(A.steps == 1);
             } else {
                 load3p<PAMG_NT_TL>(V0.T(), V0.pitch, sp, X0[0], X0[1]);
                 load3p<PAMG_NT_RL>(V0.RHS(), V0.pitch, sp, B0[0], B0[1]);
@@ -1445,8 +1456,22 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                 if constexpr (N == 2) l2_restrict(std::integral_constant<int, K2>{}, lastc, i2, xs, bs, gc, vc);
                 __syncthreads();
             };
-            for (int c = 0; c + 1 < m; ++c) cycle(c, std::false_type{});
-            cycle(m - 1, std::true_type{});
+            // RHSF: A.steps time steps of m cycles; each later step starts from the tnew the
+            // previous one left (told := tnew, tnew_nonlin := tnew, :316-317)
+            const int total = A.steps * m;
+            auto next_step = [&](int c) {
+                if (RHSF && c > 0 && c % m == 0) {
+#pragma unroll
+                    for (int k = 0; k < N; ++k) copy3(X0[k], P0[k]);
+                    start_step(c / m == A.steps - 1);
+                }
+            };
+            for (int c = 0; c + 1 < total; ++c) {
+                next_step(c);
+                cycle(c, std::false_type{});
+            }
+            next_step(total - 1);
+            cycle(total - 1, std::true_type{});
         };
         if (grpB) level1(std::integral_constant<int, 2>{});
         else level1(std::integral_constant<int, 3>{});
@@ -1556,10 +1581,11 @@ hipError_t launch_s(hipStream_t s, const VArgs &A, unsigned grid, int L, int par
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
                        double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part, int keep,
-                       int ua, int ub, double *send_b = nullptr, int cycles = 1) {
+                       int ua, int ub, double *send_b = nullptr, int cycles = 1, int steps = 1) {
     const bool coarse = part == 1;
     if (part >= 2 && L < 2) return hipErrorInvalidValue;
     if (part >= 4 && cycles < 1) return hipErrorInvalidValue;
+    if (steps != 1 && !(part == 5 && steps > 1 && vcycle_resident_run_supported(n_split, L))) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
     VArgs A{};
     for (int l = 0; l < L; ++l) {
@@ -1586,6 +1612,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.keep = keep;
     A.send_b = send_b;
     A.cycles = cycles;
+    A.steps = steps;
     // tile: 2**TL level-1 sub-elements, TL = fine_tl (level-1 launch) or CGeo's (coarse launch)
     const int TL = coarse ? (2 * n_split > 8 ? std::min(2 * n_split, kFineTLMax) : 8) : fine_tl(n_split);
     // un_eles [ua, ub) (ub < 0: all); ua on a tile boundary, ub too unless it is U
@@ -1656,9 +1683,14 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
 
 hipError_t launch_vcycle_resident(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                   int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                                  int keep, bool rhsf, double *send_b, int cycles) {
+                                  int keep, bool rhsf, double *send_b, int cycles, int steps) {
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, rhsn2, rhsf ? 5 : 4, keep, 0, -1,
-                       send_b, cycles);
+                       send_b, cycles, steps);
+}
+
+// several time steps in one resident launch: the balanced-role instance
+bool vcycle_resident_run_supported(int n_split, int L) {
+    return PAMG_RES_BALANCED && n_split >= 5 && n_split <= kMaxFusedSplit && L >= 3 && L <= kMaxFusedLevels;
 }
 
 // the resident form: two levels or more, adjacent pairs (fine_np == 2)

@@ -253,6 +253,21 @@ def test_resident_vcycle_launches():
     assert t["vcycle_res_rhsf"]["bytes"] > 0
 
 
+def test_resident_run_is_one_launch():
+    """n_split >= 5, L >= 3: a whole pamg_run (every time step: told := tnew, the RHS, n_multigrid
+    cycles) is one resident launch; its state equals the step-by-step public calls bit for bit
+    (test_time_loop_equals_public_steps, schedule 3)."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled2048.msh"))
+    s = pamg.SemiImplicitIterative(m, 5, 3, arith=1, fused=3)
+    s.timing_enable(0x3F7F)
+    s.timing_reset()
+    s.run(4, 2)
+    t = s.timing()
+    assert t["vcycle_res_rhsf"]["launches"] == 1 and t["vcycle_res"]["launches"] == 0
+    assert t["rhs"]["launches"] == 0 and t["vcycle_pipe"]["launches"] == 0
+    s.close()
+
+
 @pytest.mark.parametrize("mesh,S,L,solver,ns", [
     ("untitled8.msh", 1, 1, 3, 1), ("untitled8.msh", 2, 2, 3, 2), ("untitled8.msh", 3, 3, 1, 1),
     ("irregular.msh", 3, 3, 3, 1), ("900_ele.msh", 2, 2, 3, 3), ("900_ele.msh", 4, 4, 1, 1),
