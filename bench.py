@@ -210,7 +210,8 @@ def measure_time_loop(s):
     fl = 2 * s.vcycle_flops()
     # a step moves the state in and out once (HBM) and runs 2 cycles of fp64 work: both rooflines
     out = {"workload": f"pamg_run(ntime={TIME_LOOP_STEPS}, n_multigrid=2): each step begin_timestep + 2 V-cycles "
-                       "(the reference's n_multigrid loop inside its time loop), one resident launch per step",
+                       "(the reference's n_multigrid loop inside its time loop); with the resident schedule the whole run is "
+                       "one launch (n_split >= 5, L >= 3; a launch per step otherwise)",
            "vcycles_per_s": round(2 * TIME_LOOP_STEPS / el, 1), "ms_per_step": round(ms_step, 4),
            "alg_bytes_per_step": by, "achieved": round(by / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(by / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
