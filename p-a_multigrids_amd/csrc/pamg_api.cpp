@@ -607,8 +607,10 @@ int vcycle_corrected(pamg_handle *h) {
         CHK(smooth_to_tnew(h, L, ns * h->p.n_coarse));
     }
     for (int l = L - 1; l >= 1; --l) {
-        Span sp(h, PAMG_K_PROLONG, 216.0 * (double)h->lv[l + 1].N);
-        HIPCHK(h, launch_interp_add(h->stream, h->lv[l], h->lv[l + 1]));
+        {
+            Span sp(h, PAMG_K_PROLONG, 216.0 * (double)h->lv[l + 1].N);
+            HIPCHK(h, launch_interp_add(h->stream, h->lv[l], h->lv[l + 1]));
+        }
         CHK(smooth_to_tnew(h, l, ns));
     }
     if (L > 1) CHK(residual_corrected(h, 1));   // the fine residual after the cycle

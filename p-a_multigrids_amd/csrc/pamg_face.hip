@@ -45,8 +45,10 @@ __global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *_
 }
 
 // MODE 0 / 1: one colour of a red-black sweep (up / down sub-elements), X = OUT = tnew_nonlin;
-// MODE 2: a Jacobi sweep, X = tnew, OUT = tnew_nonlin; MODE 3 / 4: residual A X - RHS / RHS - A X
-template <int MODE>
+// MODE 2: a Jacobi sweep, X = tnew, OUT = tnew_nonlin; MODE 3 / 4: residual A X - RHS / RHS - A X.
+// UNI: every wave lies inside one un_ele (nsub >= 64): its operator and face records come through
+// the scalar unit (one fetch per wave instead of one per lane)
+template <int MODE, bool UNI>
 __global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, const double *__restrict__ RHS,
                                                  const double *__restrict__ stc, const int4 *__restrict__ fnb,
                                                  const double *__restrict__ fface, const int *__restrict__ fsx,
@@ -54,7 +56,9 @@ __global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, c
                                                  int nsub_log2, int slots, int level1, double rdt, double omega) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= N) return;
-    const int64_t u = s >> nsub_log2, base = u << nsub_log2;
+    int64_t u = s >> nsub_log2;
+    if (UNI) u = __builtin_amdgcn_readfirstlane((int)u);
+    const int64_t base = u << nsub_log2;
     const int4 nb = fnb[s & ((1ll << nsub_log2) - 1)];
     if ((MODE == 0 && !nb.w) || (MODE == 1 && nb.w)) return;
     double x[3], b[3];
@@ -128,13 +132,16 @@ hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, i
     if (!L.fnb || !L.fface || !L.fsx) return hipErrorInvalidValue;
     const dim3 g(grid_for(L.N)), b(kBlock);
     const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0;
+    const bool uni = L.nsub >= 64;
+#define PAMG_FACE(M, X_, O_)                                                                                        \
+    if (uni) hipLaunchKernelGGL((k_face<M, true>), g, b, 0, s, X_, O_, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov,     \
+                                L.pitch, L.N, lg, slots, l1, rdt, omega);                                           \
+    else hipLaunchKernelGGL((k_face<M, false>), g, b, 0, s, X_, O_, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov,       \
+                            L.pitch, L.N, lg, slots, l1, rdt, omega)
     switch (mode) {
-        case 0: hipLaunchKernelGGL(k_face<0>, g, b, 0, s, L.TNN, L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch,
-                                   L.N, lg, slots, l1, rdt, omega); break;
-        case 1: hipLaunchKernelGGL(k_face<1>, g, b, 0, s, L.TNN, L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch,
-                                   L.N, lg, slots, l1, rdt, omega); break;
-        case 2: hipLaunchKernelGGL(k_face<2>, g, b, 0, s, L.T, L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch,
-                                   L.N, lg, slots, l1, rdt, omega); break;
+        case 0: PAMG_FACE(0, L.TNN, L.TNN); break;
+        case 1: PAMG_FACE(1, L.TNN, L.TNN); break;
+        case 2: PAMG_FACE(2, L.T, L.TNN); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -146,12 +153,14 @@ hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov
     if (!L.fnb || !L.fface || !L.fsx) return hipErrorInvalidValue;
     const dim3 g(grid_for(L.N)), b(kBlock);
     const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0;
-    if (neg)
-        hipLaunchKernelGGL(k_face<4>, g, b, 0, s, L.T, L.RES, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch, L.N, lg,
-                           slots, l1, rdt, 0.0);
-    else
-        hipLaunchKernelGGL(k_face<3>, g, b, 0, s, L.T, L.RES, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tov, L.pitch, L.N, lg,
-                           slots, l1, rdt, 0.0);
+    const bool uni = L.nsub >= 64;
+    const double omega = 0.0;
+    if (neg) {
+        PAMG_FACE(4, L.T, L.RES);
+    } else {
+        PAMG_FACE(3, L.T, L.RES);
+    }
+#undef PAMG_FACE
     return hipGetLastError();
 }
 
