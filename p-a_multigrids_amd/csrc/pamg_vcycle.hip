@@ -1659,9 +1659,13 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
 
 }  // namespace
 
+// halo_mode 1 (the reference's schedule: the halo rewritten at every sweep, :555) fuses too: the
+// words of a smoother call's last sweep are the only observable ones either way (nothing reads
+// t_overlap inside a cycle), so the fused forms write them once with the same values (bitwise,
+// test_fused_vcycle_halo_mode1_bitwise)
 bool vcycle_fusable(const Level *lv, int L, int n_split, int solver, int halo_mode, int n_smooth) {
     (void)lv;
-    return solver != 2 && halo_mode == 0 && n_smooth > 0 && L >= 1 && L <= kMaxFusedLevels && n_split <= kMaxFusedSplit &&
+    return solver != 2 && (halo_mode == 0 || halo_mode == 1) && n_smooth > 0 && L >= 1 && L <= kMaxFusedLevels && n_split <= kMaxFusedSplit &&
            n_split >= L;
 }
 

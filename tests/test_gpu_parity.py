@@ -100,9 +100,11 @@ def test_driver_equals_fine_grained_calls_bitwise():
 
 
 def test_per_sweep_halo_mode_is_state_identical():
+    """the per-step kernels: the halo written once per smoother call (halo_mode 0) or before
+    every sweep (1, one launch per sweep) leave the same state"""
     meta, _ = goldens.load("irregular_s3_l3")
-    a = gpu_solver(meta, halo_mode=0)
-    b = gpu_solver(meta, halo_mode=1)
+    a = gpu_solver(meta, halo_mode=0, fused=0)
+    b = gpu_solver(meta, halo_mode=1, fused=0)
     a.run(2, 2)
     b.run(2, 2)
     for k, v in a.state().items():
@@ -289,6 +291,26 @@ def test_fused_vcycle_equals_kernel_sequence_bitwise(mesh, S, L, solver, ns, fus
     b = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, fused=0)
     a.run(2, 3)
     b.run(2, 3)
+    sa, sb = a.state(), b.state()
+    for k in sb:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    for x, y in zip(a.overlap(), b.overlap()):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("mesh,S,L", [("untitled2048.msh", 5, 3), ("irregular.msh", 6, 3), ("900_ele.msh", 3, 2)])
+@pytest.mark.parametrize("fused", [1, 3])
+def test_fused_vcycle_halo_mode1_bitwise(mesh, S, L, fused):
+    """halo_mode = 1 (the reference's schedule: the halo rewritten before every sweep) runs the
+    fused forms too, and leaves the state of the per-step kernels with halo_mode = 1 -- every
+    field and t_overlap / t_overlap_old -- bit for bit (a time loop of 2 steps x 3 cycles)."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    a = pamg.SemiImplicitIterative(m, S, L, fused=fused, halo_mode=1, arith=1)
+    b = pamg.SemiImplicitIterative(m, S, L, fused=0, halo_mode=1, arith=1)
+    a.timing_enable(0x3F7F)
+    a.run(2, 3)
+    b.run(2, 3)
+    assert a.timing()["smooth_L1"]["launches"] == 0   # the fused path ran
     sa, sb = a.state(), b.state()
     for k in sb:
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)

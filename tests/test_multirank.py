@@ -94,13 +94,13 @@ def test_local_group_matches_single_domain(mesh, S, L, nparts, kind, fused, exch
 
 
 def test_local_group_halo_mode_per_sweep():
-    """halo_mode = 1: one launch per sweep and an exchange after every sweep (the reference's
-    halo schedule, :555), on 2 ranks."""
+    """halo_mode = 1 with the per-step kernels: one launch per sweep and an exchange after every
+    sweep (the reference's halo schedule, :555), on 2 ranks."""
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
     full = pamg.SemiImplicitIterative(m, 3, 3, fused=0)
     full.run(2, 2)
     owner = m.x_strip_owner(2)
-    parts = [pamg.SemiImplicitIterative(m, 3, 3, comm=(2, r, None, owner), halo_mode=1) for r in range(2)]
+    parts = [pamg.SemiImplicitIterative(m, 3, 3, comm=(2, r, None, owner), halo_mode=1, fused=0) for r in range(2)]
     local_group(parts)
     run_ranks(parts, lambda p: p.run(2, 2))
     check_parts(full, parts, owner)
