@@ -928,11 +928,11 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 #ifndef PAMG_RES_BALANCED
 #define PAMG_RES_BALANCED 1
 #endif
-// k_vc_resb A/B: level 2 all on waves 6,7 (0) or half of it on wave 0 (1, fewer VGPRs at the same
-// occupancy: measured equal, profiles/r02_res_ab_variants.txt). (A prolongator cascade sequenced
+// k_vc_resb: level 2 half on wave 0 (1: 110 VGPRs, no scratch) or all on waves 6,7 (0: 128 with
+// 12 B of scratch per lane; measured equal, profiles/r02_res_ab_variants.txt). (A prolongator cascade sequenced
 // by scheduling barriers to cut the VGPR peak further measured 15 % slower and is not kept.)
 #ifndef PAMG_RES_L2W0
-#define PAMG_RES_L2W0 0
+#define PAMG_RES_L2W0 1
 #endif
 template <int S, int L>
 struct RGeo {
@@ -1145,7 +1145,10 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
     using R = RGeo<S, L>;
     constexpr int C = G::C, T = G::T;
     static_assert(C >= 2 && C <= 4 && T == 1024 && G::MT == 512 && S >= 5, "balanced roles: n_split >= 5, L 3..5");
-    __shared__ __attribute__((aligned(16))) double F0[R::LDS()];
+    // RHSF: the tile's source s' (3 T doubles) behind the images -- every step's RHS reads it; in
+    // registers it pushed the launch past 128 VGPRs
+    __shared__ __attribute__((aligned(16))) double F0[R::LDS() + (RHSF ? 3 * T : 0)];
+    double *const SQ = F0 + R::LDS();
     double *const M0 = F0 + 3 * T;
     double *const CI = F0 + R::CI();
     const int t = threadIdx.x, lane = t & 63;
@@ -1354,13 +1357,20 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             const uint32_t sq = N == 3 ? tile_index<S>(A, tb, T, 0, js, vq) : 0u;
             const uint32_t w0 = sp >> G::lg(0);   // the tile's un_ele
             double X0[N][3], B0[N][3], P0[N][3];
-            double Q[RHSF ? N : 1][3];   // RHSF: the source s' of every step's RHS
             // the start of a time step (:316-317, get_RHS :452-464): told := tnew (X0 holds it) and
             // the RHS from it and s'; the run's last step stores told, the step's constant halo
             // words (kKeepTold) and the RHS it formed (kKeepL1) -- earlier steps' are overwritten
             auto start_step = [&](bool last_step) {
                 if constexpr (RHSF) {
                     const double c = sp0[(size_t)__builtin_amdgcn_readfirstlane(w0) * kStcStride + kStcC];
+                    double Q[N][3];   // the thread's own s' words (written by it, no barrier)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const double2 v = *reinterpret_cast<const double2 *>(SQ + q * T + jp);
+                        Q[0][q] = v.x;
+                        Q[1][q] = v.y;
+                        if constexpr (N == 3) Q[2][q] = SQ[q * T + js];
+                    }
 #pragma unroll
                     for (int k = 0; k < N; ++k) rhs_from_source(c, rdt, X0[k], Q[k], B0[k]);
                     if (!last_step) return;
@@ -1384,11 +1394,17 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                 }
             };
             if constexpr (RHSF) {
+                double Q[N][3];
                 load3p<PAMG_NT_TL>(V0.T(), V0.pitch, sp, X0[0], X0[1]);
                 load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, sp, Q[0], Q[1]);
                 if constexpr (N == 3) {
                     load3(V0.T(), V0.pitch, sq, X0[2]);
                     load3(V0.SRC(), V0.pitch, sq, Q[2]);
+                }
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    *reinterpret_cast<double2 *>(SQ + q * T + jp) = make_double2(Q[0][q], Q[1][q]);
+                    if constexpr (N == 3) SQ[q * T + js] = Q[2][q];
                 }
                 start_step(A.steps == 1);
             } else {
