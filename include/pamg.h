@@ -192,8 +192,10 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid);
  * cycles; 0 automatic (3 where supported: two levels or more; else one GPU: 1, a partition
  * of a multi-rank run: 2). The state after the call is bitwise the same in all. */
 int pamg_set_call_schedule(pamg_handle *h, int schedule);
-/* fp64 operations of one V-cycle of the handle's configuration (the resident launch's
- * roofline: every sweep, residual, restriction and prolongation cascade) */
+/* fp64 operations one fused V-cycle of the handle's configuration executes (the resident
+ * launch's roofline): its sweeps, residuals, restrictions and prolongation cascades, less each
+ * smoother call's last sweep, whose only output (tnew_nonlin) the cycle overwrites unread
+ *  */
 int pamg_vcycle_flops(pamg_handle *h, double *flops_per_cycle);
 int pamg_synchronize(pamg_handle *h);
 

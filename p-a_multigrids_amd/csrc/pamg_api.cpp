@@ -503,19 +503,25 @@ double vcycle_res_bytes(pamg_handle *h, int keep, bool rhsf) {
     for (int l = 2; l <= L; ++l) b += (96.0 + (keep & PAMG_KEEP_COARSE ? 48.0 : 0.0)) * h->lv[l].N;
     return b + 104.0 * h->U * L;
 }
-// fp64 operations of one V-cycle (fma = 2): a sweep is 12 fma (contracted) or 42 operations
-// (the reference's order, apply_A + update), get_residual 9 fma or 36; the restrictor's input
-// mean 3 per sub-element of the levels < L; the prolongator cascade 21 per coarse
-// sub-element (splitting.F90:59-88, executed although dead)
+// fp64 operations one V-cycle of the fused forms executes (fma = 2): a sweep is 12 fma (24 flop,
+// contracted) or 42 operations (the reference's order, apply_A + update), get_residual 9 fma or
+// 36; the restrictor's input mean 3 per sub-element of the levels < L; the prolongator cascade 21
+// per coarse sub-element (splitting.F90:59-88, executed on LDS images although its output is dead).
+// A smoother call's last sweep only produces tnew_nonlin; inside a fused cycle that value is
+// overwritten before any read (:367 after the restriction leg, :327 of the next cycle after the
+// prolongation leg, :348 on the coarsest level), so it is never computed (the compiler drops it:
+// its result never leaves registers) -- per cycle a level l < L runs 2 (n_smooth - 1) sweeps and
+// the coarsest n_smooth (1 + n_coarse) - 2; only a call's last cycle also runs level 1's final
+// sweep, whose tnew_nonlin it stores (not counted here)
 double vcycle_flops(pamg_handle *h) {
-    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    const int L = h->p.multi_levels, ns = h->p.n_smooth, nc = h->p.n_coarse;
     const bool f = h->p.arith == 1;
     const double sw = f ? 24.0 : 42.0, rs = f ? 18.0 : 36.0;
     double fl = 0.0;
     for (int l = 1; l <= L; ++l) {
         const double n = (double)h->lv[l].N;
-        if (l < L) fl += n * (2.0 * ns * sw + rs + 3.0);
-        else fl += n * ((ns + (double)ns * h->p.n_coarse) * sw + rs);
+        if (l < L) fl += n * (2.0 * std::max(ns - 1, 0) * sw + rs + 3.0);
+        else fl += n * ((nc > 0 ? (double)ns * (1 + nc) - 2 : (double)ns - 1) * sw + rs);
         if (l >= 2) fl += n * 21.0;
     }
     return fl;
