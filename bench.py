@@ -13,13 +13,14 @@ every smoother call) over the whole mesh.
 Defaults: the fused V-cycle (fused = 3) in its resident call schedule -- the K
 cycles of a pamg_vcycle(K) call in ONE launch, every tile's state (all levels)
 on-chip between cycles, loaded once and stored once (pamg_vcycle.hip k_vc_resb);
-every sweep, residual, restriction and prolongation of every cycle runs, and the
-state after the call is the per-step kernel sequence's, bit for bit -- and the
+the state after the call is the per-step kernel sequence's, bit for bit (values
+overwritten unread inside the call -- stores, and a smoother call's last sweep --
+are not produced) -- and the
 contracted operator arithmetic (arith = 1: fma rows of A_e = M/dt + Kd; ~1e-15
 relative to the reference on the solution, the north star's bar being 1e-10).
-The cycle is then fp64-issue-bound: the roofline is the launch's fp64 operations
-(pamg_vcycle_flops x cycles) over its duration against the 78.6 TFLOP/s fp64
-peak. The other schedules (one HBM-bound launch per cycle: the round-1 form, with
+The cycle is then fp64-issue-bound: the roofline is the fp64 operations the launch
+executes (pamg_vcycle_flops x cycles) over its duration against the 78.6 TFLOP/s
+fp64 peak. The other schedules (one HBM-bound launch per cycle: the round-1 form, with
 its HBM roofline), the reference's own operation order (arith = 0, bitwise equal
 to the reference) and the other workloads are timed and reported under "extra".
 

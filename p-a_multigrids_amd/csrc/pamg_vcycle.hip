@@ -917,10 +917,11 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 // HBM sees the tile's state twice per call: loaded at the start (tnew and RHS or, starting
 // a time step (RHSF), tnew and the source s' of level 1; tnew and RHSN of the coarse
 // levels) and stored at the end, with the same final-cycle store policy as the pipelined
-// launches (VArgs::keep). Every sweep, residual, restriction and prolongation of every cycle
-// runs, in the same order on the same values: the state after the call is bitwise the
-// per-step kernel sequence's (tests/test_gpu_parity.py). The cycle is fp64-issue-bound here,
-// no longer HBM-bound.
+// launches (VArgs::keep). Every sweep, residual, restriction and prolongation whose result is
+// read runs, in the same order on the same values (a smoother call's last sweep, which only
+// feeds a tnew_nonlin the cycle overwrites unread, is left to the compiler to drop): the state
+// after the call is bitwise the per-step kernel sequence's (tests/test_gpu_parity.py). The
+// cycle is fp64-issue-bound here, no longer HBM-bound.
 #ifndef PAMG_RES_WAVES
 #define PAMG_RES_WAVES 4
 #endif
