@@ -261,6 +261,17 @@ __device__ __forceinline__ void sweeps1(const ST &S, double rdt, int n, const do
     sweep(S, rdt, b, x);
 }
 
+// one smoother call inside a fused cycle when only its tnew is read: the iterate before the last
+// sweep (:550 vs :693); the last sweep feeds only a tnew_nonlin the cycle overwrites unread
+// (dead computation), so the call is n - 1 sweeps in place (N sub-elements, interleaved)
+template <int N, class ST>
+__device__ __forceinline__ void sweeps_tnew(const ST &S, double rdt, int n, const double b[N][3], double x[N][3]) {
+    for (int it = 1; it < n; ++it) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) sweep(S, rdt, b[q], x[q]);
+    }
+}
+
 // two sub-elements of one un_ele, interleaved
 template <class ST>
 __device__ __forceinline__ void sweeps2(const ST &S, double rdt, int n, const double b0[3], const double b1[3],
@@ -1184,40 +1195,30 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
         const VLevel &V = A.lv[1];
         ST St;
         stencil(true, sp1, opaque(gc >> G::lg(1)), St);
-        double x[2][3], p[2][3], rr[2][3];
-        if constexpr (K == 2) {
-            if (last && keepc && vc) store3p(V.RHS(), V.pitch, gc, bs[0], bs[1]);
-            copy3(x[0], xs[0]);
-            copy3(x[1], xs[1]);
-            sweeps2(St, rdt, ns, bs[0], bs[1], x[0], x[1], p[0], p[1]);
-        } else {
-            if (last && keepc && vc) store3(V.RHS(), V.pitch, gc, bs[0]);
-            copy3(x[0], xs[0]);
-            sweeps1(St, rdt, ns, bs[0], x[0], p[0]);
+        if (last && keepc && vc) {
+            if constexpr (K == 2) store3p(V.RHS(), V.pitch, gc, bs[0], bs[1]);
+            else store3(V.RHS(), V.pitch, gc, bs[0]);
         }
+        sweeps_tnew<K>(St, rdt, ns, bs, xs);   // restriction-leg call (:331): its tnew, in place
+        double rr[2][3];
 #pragma unroll
-        for (int k = 0; k < K; ++k) residual(St, rdt, p[k], bs[k], rr[k]);
+        for (int k = 0; k < K; ++k) residual(St, rdt, xs[k], bs[k], rr[k]);   // :338
         if (vc) {
             if constexpr (K == 2) {
                 if (last && keepc) store3p(V.RES(), V.pitch, gc, rr[0], rr[1]);
 #pragma unroll
                 for (int q = 0; q < 3; ++q)
-                    *reinterpret_cast<double2 *>(CI + P::F(1) + q * P::nt(1) + i0) = make_double2(p[0][q], p[1][q]);
+                    *reinterpret_cast<double2 *>(CI + P::F(1) + q * P::nt(1) + i0) = make_double2(xs[0][q], xs[1][q]);
                 *reinterpret_cast<double2 *>(CI + P::M(1) + i0) =
                     make_double2(div3(rr[0][0] + rr[0][1] + rr[0][2]), div3(rr[1][0] + rr[1][1] + rr[1][2]));
             } else {
                 if (last && keepc) store3(V.RES(), V.pitch, gc, rr[0]);
 #pragma unroll
-                for (int q = 0; q < 3; ++q) CI[P::F(1) + q * P::nt(1) + i0] = p[0][q];
+                for (int q = 0; q < 3; ++q) CI[P::F(1) + q * P::nt(1) + i0] = xs[0][q];
                 CI[P::M(1) + i0] = div3(rr[0][0] + rr[0][1] + rr[0][2]);
             }
         }
-#pragma unroll
-        for (int k = 0; k < K; ++k) copy3(x[k], p[k]);   // tnew_nonlin := tnew (:367)
-        if constexpr (K == 2) sweeps2(St, rdt, ns, bs[0], bs[1], x[0], x[1], p[0], p[1]);
-        else sweeps1(St, rdt, ns, bs[0], x[0], p[0]);
-#pragma unroll
-        for (int k = 0; k < K; ++k) copy3(xs[k], p[k]);
+        sweeps_tnew<K>(St, rdt, ns, bs, xs);   // prolongation-leg call (:367-376), from that tnew
         if (last && vc) {
             if constexpr (K == 2) store3p(V.T(), V.pitch, gc, xs[0], xs[1]);
             else store3(V.T(), V.pitch, gc, xs[0]);
@@ -1257,15 +1258,15 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             constexpr int prio = std::is_same<ST, StcF>::value ? PAMG_CHAIN_PRIO : 0;
             if (prio) __builtin_amdgcn_s_setprio(prio);
             if (last && keepc && vc) store3(V.RHS(), V.pitch, gc, bs);
-            double x[3], p[3];
-            copy3(x, xs);
-            sweeps1(St, rdt, ns, bs, x, p);
+            double(*x1)[3] = reinterpret_cast<double(*)[3]>(xs);
+            const double(*b1)[3] = reinterpret_cast<const double(*)[3]>(bs);
+            sweeps_tnew<1>(St, rdt, ns, b1, x1);   // restriction-leg call: its tnew, in place
             double r[3];
-            residual(St, rdt, p, bs, r);
+            residual(St, rdt, xs, bs, r);
             if (last && keepc && vc) store3(V.RES(), V.pitch, gc, r);
-            copy3(x, p);   // tnew_nonlin := tnew (:348)
-            sweeps1(St, rdt, ns * A.n_coarse, bs, x, p);
-            copy3(xs, p);
+            // the 1 + n_coarse calls (:351-353): one chain of n_smooth n_coarse sweeps from that tnew
+            // (tnew_nonlin := tnew, :348); its final tnew
+            sweeps_tnew<1>(St, rdt, ns * A.n_coarse, b1, x1);
             if (prio) __builtin_amdgcn_s_setprio(0);
             if (last && vc) store3(V.T(), V.pitch, gc, xs);
             __syncthreads();
@@ -1310,20 +1311,18 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                 ST St;
                 stencil(true, SP[l], opaque(gc[k] >> G::lg(l)), St);
                 if (last && keepc && vc[k]) store3(V.RHS(), V.pitch, gc[k], bs[k]);
-                double x[3], p[3];
-                copy3(x, xs[k]);
-                sweeps1(St, rdt, ns, bs[k], x, p);
+                double(*x1)[3] = reinterpret_cast<double(*)[3]>(xs[k]);
+                const double(*b1)[3] = reinterpret_cast<const double(*)[3]>(bs[k]);
+                sweeps_tnew<1>(St, rdt, ns, b1, x1);   // restriction-leg call: its tnew, in place
                 double r[3];
-                residual(St, rdt, p, bs[k], r);
+                residual(St, rdt, xs[k], bs[k], r);
                 if (last && keepc && vc[k]) store3(V.RES(), V.pitch, gc[k], r);
                 if (vc[k]) {
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) CI[P::F(l) + q * P::nt(l) + lane] = p[q];
+                    for (int q = 0; q < 3; ++q) CI[P::F(l) + q * P::nt(l) + lane] = xs[k][q];
                     CI[P::M(l) + lane] = div3(r[0] + r[1] + r[2]);
                 }
-                copy3(x, p);   // tnew_nonlin := tnew (:367)
-                sweeps1(St, rdt, ns, bs[k], x, p);
-                copy3(xs[k], p);
+                sweeps_tnew<1>(St, rdt, ns, b1, x1);   // prolongation-leg call (:367-376), from that tnew
                 if (last && vc[k]) store3(V.T(), V.pitch, gc[k], xs[k]);
             });
             __syncthreads();
@@ -1357,7 +1356,7 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             const uint32_t sp = tile_index<S>(A, tb, T, 0, jp, vp);
             const uint32_t sq = N == 3 ? tile_index<S>(A, tb, T, 0, js, vq) : 0u;
             const uint32_t w0 = sp >> G::lg(0);   // the tile's un_ele
-            double X0[N][3], B0[N][3], P0[N][3];
+            double X0[N][3], B0[N][3];   // tnew (told := tnew, tnew_nonlin := tnew at a cycle's start) and RHS
             // the start of a time step (:316-317, get_RHS :452-464): told := tnew (X0 holds it) and
             // the RHS from it and s'; the run's last step stores told, the step's constant halo
             // words (kKeepTold) and the RHS it formed (kKeepL1) -- earlier steps' are overwritten
@@ -1427,18 +1426,16 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                 constexpr bool last = decltype(lastc)::value;
                 ST St0;
                 stencil(true, sp0, opaque(w0), St0);
-                if (c > 0) {
-#pragma unroll
-                    for (int k = 0; k < N; ++k) copy3(X0[k], P0[k]);   // tnew_nonlin := tnew (:327)
-                }
-                sweepsN<N>(St0, rdt, ns, B0, X0, P0);   // restriction-leg call (:331)
+                (void)c;
+                // restriction-leg call (:331) from tnew (tnew_nonlin := tnew, :327): its tnew, in place
+                sweeps_tnew<N>(St0, rdt, ns, B0, X0);
                 double r[N][3];
 #pragma unroll
-                for (int k = 0; k < N; ++k) residual(St0, rdt, P0[k], B0[k], r[k]);   // :338
+                for (int k = 0; k < N; ++k) residual(St0, rdt, X0[k], B0[k], r[k]);   // :338
                 if (vp) {
 #pragma unroll
                     for (int q = 0; q < 3; ++q)
-                        *reinterpret_cast<double2 *>(F0 + q * T + jp) = make_double2(P0[0][q], P0[1][q]);
+                        *reinterpret_cast<double2 *>(F0 + q * T + jp) = make_double2(X0[0][q], X0[1][q]);
                     *reinterpret_cast<double2 *>(M0 + jp) =
                         make_double2(div3(r[0][0] + r[0][1] + r[0][2]), div3(r[1][0] + r[1][1] + r[1][2]));
                     if (last && keep1) store3p(V0.RES(), V0.pitch, sp, r[0], r[1]);
@@ -1446,26 +1443,31 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                 if constexpr (N == 3)
                     if (vq) {
 #pragma unroll
-                        for (int q = 0; q < 3; ++q) F0[q * T + js] = P0[2][q];
+                        for (int q = 0; q < 3; ++q) F0[q * T + js] = X0[2][q];
                         M0[js] = div3(r[2][0] + r[2][1] + r[2][2]);
                         if (last && keep1) store3(V0.RES(), V0.pitch, sq, r[2]);
                     }
-#pragma unroll
-                for (int k = 0; k < N; ++k) copy3(X0[k], P0[k]);
-                sweepsN<N>(St0, rdt, ns, B0, X0, P0);   // prolongation-leg call (:376)
+                sweeps_tnew<N>(St0, rdt, ns, B0, X0);   // prolongation-leg call (:367-376): the cycle's tnew
                 if constexpr (last) {
+                    // the call's last cycle: tnew_nonlin is observable, so its last sweep runs
+                    double Y0[N][3];
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        copy3(Y0[k], X0[k]);
+                        if (ns > 0) sweep(St0, rdt, B0[k], Y0[k]);
+                    }
                     if (vp) {
 #pragma unroll
                         for (int k = 0; k < 2; ++k)
-                            if (keeph) hs_write(true, V0.H, w0, hs_pack(V0.H.hsub[(sp + k) & hmask]), P0[k]);
-                        store3p<PAMG_NT_TS>(V0.T(), V0.pitch, sp, P0[0], P0[1]);
-                        if (keep1) store3p(V0.TNN(), V0.pitch, sp, X0[0], X0[1]);
+                            if (keeph) hs_write(true, V0.H, w0, hs_pack(V0.H.hsub[(sp + k) & hmask]), X0[k]);
+                        store3p<PAMG_NT_TS>(V0.T(), V0.pitch, sp, X0[0], X0[1]);
+                        if (keep1) store3p(V0.TNN(), V0.pitch, sp, Y0[0], Y0[1]);
                     }
                     if constexpr (N == 3)
                         if (vq) {
-                            if (keeph) hs_write(true, V0.H, w0, hs_pack(V0.H.hsub[sq & hmask]), P0[2]);
-                            store3(V0.T(), V0.pitch, sq, P0[2]);
-                            if (keep1) store3(V0.TNN(), V0.pitch, sq, X0[2]);
+                            if (keeph) hs_write(true, V0.H, w0, hs_pack(V0.H.hsub[sq & hmask]), X0[2]);
+                            store3(V0.T(), V0.pitch, sq, X0[2]);
+                            if (keep1) store3(V0.TNN(), V0.pitch, sq, Y0[2]);
                         }
                 }
                 if constexpr (N == 2) l2_legs(std::integral_constant<int, K2>{}, lastc, i2, xs, bs, gc, vc);
@@ -1476,12 +1478,8 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             // RHSF: A.steps time steps of m cycles; each later step starts from the tnew the
             // previous one left (told := tnew, tnew_nonlin := tnew, :316-317)
             const int total = A.steps * m;
-            auto next_step = [&](int c) {
-                if (RHSF && c > 0 && c % m == 0) {
-#pragma unroll
-                    for (int k = 0; k < N; ++k) copy3(X0[k], P0[k]);
-                    start_step(c / m == A.steps - 1);
-                }
+            auto next_step = [&](int c) {   // X0 holds tnew: told := tnew
+                if (RHSF && c > 0 && c % m == 0) start_step(c / m == A.steps - 1);
             };
             for (int c = 0; c + 1 < total; ++c) {
                 next_step(c);
