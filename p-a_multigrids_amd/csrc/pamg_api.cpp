@@ -354,6 +354,23 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
     const double bytes = 96.0 * (double)L.N + 168.0 * h->U;
     if (h->p.op == 1) {   // face-coupled operator: the halo is read, so it is refreshed (and exchanged) every sweep
         if (src_is_T) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
+        // single domain: one launch per sweep (k_face_sweep), the halo snapshots alternating
+        // between two t_overlap buffers so that a sweep's halo words for the next sweep never
+        // overwrite the ones it reads; the call's last sweep reads h->tov, which therefore holds
+        // the words of its start, as after the per-colour sequence (PAMG_FACE_FUSED=0: that sequence)
+        static const bool fuse_env = !getenv("PAMG_FACE_FUSED") || atoi(getenv("PAMG_FACE_FUSED")) != 0;
+        if (fuse_env && h->nranks == 1 && !h->comm && face_sweep_fusable(L)) {
+            if (!h->tov_b) CHK(dev_alloc(h, &h->tov_b, (size_t)h->slots * 3 * std::max(h->U, 1)));
+            double *buf[2] = {h->tov, h->tov_b};
+            HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
+            for (int s = 0; s < sweeps; ++s) {
+                Span sp(h, kid, bytes);   // read tnew_nonlin, RHS; write tnew, tnew_nonlin (+ halo words)
+                HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
+                                                  s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
+                                                  h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots));
+            }
+            return PAMG_OK;
+        }
         for (int s = 0; s < sweeps; ++s) {
             HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, true));   // tnew := tnew_nonlin (:550), :555
             CHK(halo(h, l));
@@ -513,16 +530,20 @@ double vcycle_res_bytes(pamg_handle *h, int keep, bool rhsf) {
 // its result never leaves registers) -- per cycle a level l < L runs 2 (n_smooth - 1) sweeps and
 // the coarsest n_smooth (1 + n_coarse) - 2; only a call's last cycle also runs level 1's final
 // sweep, whose tnew_nonlin it stores (not counted here)
+int call_schedule(pamg_handle *h);
 double vcycle_flops(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth, nc = h->p.n_coarse;
     const bool f = h->p.arith == 1;
     const double sw = f ? 24.0 : 42.0, rs = f ? 18.0 : 36.0;
+    // the balanced resident kernel (call schedule 3, n_split >= 5, L >= 3) does not compute the
+    // dead prolongator (pamg_vcycle.hip k_vc_resb); every other fused form executes its cascade
+    const bool prolong = !(call_schedule(h) == 3 && vcycle_resident_run_supported(h->p.n_split, L));
     double fl = 0.0;
     for (int l = 1; l <= L; ++l) {
         const double n = (double)h->lv[l].N;
         if (l < L) fl += n * (2.0 * std::max(ns - 1, 0) * sw + rs + 3.0);
         else fl += n * ((nc > 0 ? (double)ns * (1 + nc) - 2 : (double)ns - 1) * sw + rs);
-        if (l >= 2) fl += n * 21.0;
+        if (l >= 2 && prolong) fl += n * 21.0;
     }
     return fl;
 }
@@ -871,7 +892,7 @@ void free_levels(pamg_handle *h) {
         dev_free(L.halo.d_surf); dev_free(L.halo.d_told_halo);
         L = Level();
     }
-    dev_free(h->geo1); dev_free(h->tov); dev_free(h->tovo);
+    dev_free(h->geo1); dev_free(h->tov); dev_free(h->tovo); dev_free(h->tov_b);
     h->geo1 = h->tov = h->tovo = nullptr;
     h->mesh_ready = false;
 }

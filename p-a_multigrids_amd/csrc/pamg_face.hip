@@ -44,29 +44,15 @@ __global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *_
     halo_write(H, hp, p0, p1);
 }
 
-// MODE 0 / 1: one colour of a red-black sweep (up / down sub-elements), X = OUT = tnew_nonlin;
-// MODE 2: a Jacobi sweep, X = tnew, OUT = tnew_nonlin; MODE 3 / 4: residual A X - RHS / RHS - A X.
-// UNI: every wave lies inside one un_ele (nsub >= 64): its operator and face records come through
-// the scalar unit (one fetch per wave instead of one per lane)
-template <int MODE, bool UNI>
-__global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, const double *__restrict__ RHS,
-                                                 const double *__restrict__ stc, const int4 *__restrict__ fnb,
-                                                 const double *__restrict__ fface, const int *__restrict__ fsx,
-                                                 const double *__restrict__ tov, int64_t pitch, int64_t N,
-                                                 int nsub_log2, int slots, int level1, double rdt, double omega) {
-    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (s >= N) return;
-    int64_t u = s >> nsub_log2;
-    if (UNI) u = __builtin_amdgcn_readfirstlane((int)u);
-    const int64_t base = u << nsub_log2;
-    const int4 nb = fnb[s & ((1ll << nsub_log2) - 1)];
-    if ((MODE == 0 && !nb.w) || (MODE == 1 && nb.w)) return;
-    double x[3], b[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        x[c] = X[c * pitch + s];
-        b[c] = RHS[c * pitch + s];
-    }
+// One sub-element of the face-coupled operator (the oracle's face_terms / face_sweep order):
+// MODE <= 2 the smoother update x_i + omega / D_i (b_i - (A x)_i), MODE 3 / 4 the residual
+// A x - b / b - A x. x: the sub-element's values; xin(c, q): component c of the inner neighbour
+// at un_ele position q; tov: the halo snapshot (t_overlap) the sweep reads.
+template <int MODE, class XIN>
+__device__ __forceinline__ void face_point(const XIN &xin, const double x[3], const double b[3], int4 nb, int64_t u,
+                                           const double *__restrict__ stc, const double *__restrict__ fface,
+                                           const int *__restrict__ fsx, const double *__restrict__ tov, int slots,
+                                           int level1, double rdt, double omega, double out[3]) {
     Stc S;
     load_stc(stc + u * kStcStride, S);
     double A[3];
@@ -79,9 +65,8 @@ __global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, c
         const int a = cFNode[fi][0], bb = cFNode[fi][1];
         double ya, yb, wf;
         if (nbf[fi] >= 0) {   // inner neighbour: its nodes at my face nodes a, b are its b, a
-            const int64_t o = base + nbf[fi];
-            ya = X[bb * pitch + o];
-            yb = X[a * pitch + o];
+            ya = xin(bb, nbf[fi]);
+            yb = xin(a, nbf[fi]);
             wf = w[fi];
         } else {              // across the un_ele face: the halo (t_overlap slot sp)
             const int mface = cFMface[fi], sx = fsx[4 * u + mface - 1];
@@ -103,11 +88,143 @@ __global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, c
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const double ai = A[i] + ds[i];
-        double r;
-        if (MODE <= 2) r = x[i] + omega / D[i] * (b[i] - ai);
-        else if (MODE == 3) r = ai - b[i];
-        else r = b[i] - ai;
-        OUT[i * pitch + s] = r;
+        if (MODE <= 2) out[i] = x[i] + omega / D[i] * (b[i] - ai);
+        else if (MODE == 3) out[i] = ai - b[i];
+        else out[i] = b[i] - ai;
+    }
+}
+
+// MODE 0 / 1: one colour of a red-black sweep (up / down sub-elements), X = OUT = tnew_nonlin;
+// MODE 2: a Jacobi sweep, X = tnew, OUT = tnew_nonlin; MODE 3 / 4: residual A X - RHS / RHS - A X.
+// UNI: every wave lies inside one un_ele (nsub >= 64): its operator and face records come through
+// the scalar unit (one fetch per wave instead of one per lane)
+template <int MODE, bool UNI>
+__global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, const double *__restrict__ RHS,
+                                                 const double *__restrict__ stc, const int4 *__restrict__ fnb,
+                                                 const double *__restrict__ fface, const int *__restrict__ fsx,
+                                                 const double *__restrict__ tov, int64_t pitch, int64_t N,
+                                                 int nsub_log2, int slots, int level1, double rdt, double omega) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= N) return;
+    int64_t u = s >> nsub_log2;
+    if (UNI) u = __builtin_amdgcn_readfirstlane((int)u);
+    const int64_t base = u << nsub_log2;
+    const int4 nb = fnb[s & ((1ll << nsub_log2) - 1)];
+    if ((MODE == 0 && !nb.w) || (MODE == 1 && nb.w)) return;
+    double x[3], b[3], r[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        x[c] = X[c * pitch + s];
+        b[c] = RHS[c * pitch + s];
+    }
+    auto xin = [&](int c, int q) { return X[c * pitch + base + q]; };
+    face_point<MODE>(xin, x, b, nb, u, stc, fface, fsx, tov, slots, level1, rdt, omega, r);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) OUT[i * pitch + s] = r[i];
+}
+
+// One whole smoother sweep on a tile of TS sub-elements (whole un_eles; NT threads, TS / NT
+// sub-elements each), one launch instead of the halo refresh and two colour launches: the leg
+// copy tnew := tnew_nonlin (:550), the sweep itself -- red-black (RB: up sub-elements, then down
+// ones, the iterate in LDS) or Jacobi -- from the halo snapshot `tin`, tnew_nonlin stored, and,
+// unless this is the call's last sweep, the halo words the NEXT sweep reads (update_overlaps,
+// :555, from the new tnew_nonlin that its :550 copies into tnew) written through `Hn` into the
+// other t_overlap buffer. Single domain only (a partition's halo crosses ranks between sweeps).
+// Every sub-element's operations are face_point's, so the result is bitwise the per-colour
+// kernels' (and the oracle's).
+// (waves per SIMD: 6 for the wave-uniform 1024-tiles, 72-76 VGPRs; the others spill there)
+#ifndef PAMG_FACE_WAVES
+#define PAMG_FACE_WAVES 6
+#endif
+template <int TS, int NT, bool UNI, bool RB>
+__global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_sweep(double *T, double *TNN, const double *__restrict__ RHS,
+                                                   const double *__restrict__ stc, const int4 *__restrict__ fnb,
+                                                   const double *__restrict__ fface, const int *__restrict__ fsx,
+                                                   const double *__restrict__ tin, HaloArgs Hn, int next_halo,
+                                                   int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
+                                                   double rdt, double omega) {
+    constexpr int PER = TS / NT;
+    __shared__ double X[3][TS];
+    const int t = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * TS;
+    const int64_t nsm = (1ll << nsub_log2) - 1;
+    double b[PER][3];   // the RHS and neighbour records of the thread's sub-elements, read once
+    int4 nbr[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {   // tnew := tnew_nonlin (:550); the iterate into LDS
+        const int j = t + NT * k;
+        const int64_t s = s0 + j < N ? s0 + j : s0;
+        nbr[k] = fnb[s & nsm];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double v = TNN[c * pitch + s];
+            b[k][c] = RHS[c * pitch + s];
+            X[c][j] = v;
+            if (s0 + j < N) T[c * pitch + s] = v;
+        }
+    }
+    __syncthreads();
+    // one colour (0 up, 1 down) or the Jacobi sweep (2) of the thread's sub-elements
+    auto pass = [&](auto mc) {
+        constexpr int MODE = decltype(mc)::value;
+        double r[PER][3];
+        bool on[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = t + NT * k;
+            const int64_t s = s0 + j;
+            on[k] = false;
+            if (s >= N) continue;
+            int64_t u = s >> nsub_log2;
+            if (UNI) u = __builtin_amdgcn_readfirstlane((int)u);
+            const int4 nb = nbr[k];
+            if ((MODE == 0 && !nb.w) || (MODE == 1 && nb.w)) continue;
+            on[k] = true;
+            const int jb = (int)((u << nsub_log2) - s0);   // the un_ele's first tile position
+            double x[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[c] = X[c][j];
+            auto xin = [&](int c, int q) { return X[c][jb + q]; };
+            face_point<MODE>(xin, x, b[k], nb, u, stc, fface, fsx, tin, slots, level1, rdt, omega, r[k]);
+            // a colour's values are read only by the other colour: in place (red-black)
+            if (MODE != 2)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) X[c][j] = r[k][c];
+        }
+        if (MODE == 2) {   // Jacobi: every read of the old iterate before any write
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PER; ++k)
+                if (on[k])
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][t + NT * k] = r[k][c];
+        }
+        __syncthreads();
+    };
+    if constexpr (RB) {
+        pass(std::integral_constant<int, 0>{});
+        pass(std::integral_constant<int, 1>{});
+    } else {
+        pass(std::integral_constant<int, 2>{});
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {   // tnew_nonlin
+        const int j = t + NT * k;
+        const int64_t s = s0 + j;
+        if (s < N)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) TNN[c * pitch + s] = X[c][j];
+    }
+    if (!next_halo) return;
+#pragma unroll
+    for (int k = 0; k < PER / 2; ++k) {   // the next sweep's halo words, an adjacent pair per thread
+        const int j = 2 * (t + NT * k);
+        const int64_t s = s0 + j;
+        if (s >= N) continue;
+        HaloPre hp;
+        halo_prefetch(Hn, s, s >> nsub_log2, nsub_log2, hp);
+        const double p0[3] = {X[0][j], X[1][j], X[2][j]}, p1[3] = {X[0][j + 1], X[1][j + 1], X[2][j + 1]};
+        halo_write(Hn, hp, p0, p1);
     }
 }
 
@@ -144,6 +261,35 @@ hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, i
         case 2: PAMG_FACE(2, L.T, L.TNN); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// one fused sweep (k_face_sweep): reads the halo snapshot tin, writes the next sweep's halo words
+// into tout unless tout is null; single domain, un_eles of at most 4096 sub-elements
+bool face_sweep_fusable(const Level &L) { return L.nsub <= 4096; }
+
+hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
+                                   bool rb, bool level1, double rdt, double omega, int slots) {
+    if (L.N == 0) return hipSuccess;
+    if (!L.fnb || !L.fface || !L.fsx || !face_sweep_fusable(L)) return hipErrorInvalidValue;
+    const HaloPlan &P = L.halo;
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tout, tovo, P.d_send, 1 << L.isplit};
+    const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0, nh = tout ? 1 : 0;
+    const bool uni = L.nsub >= 64;
+#define PAMG_FSW(TS, NT, U, R)                                                                                      \
+    hipLaunchKernelGGL((k_face_sweep<TS, NT, U, R>), dim3((unsigned)((L.N + TS - 1) / TS)), dim3(NT), 0, s, L.T,   \
+                       L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tin, H, nh, L.pitch, L.N, lg, slots, l1, rdt, omega)
+    if (L.nsub > 1024) {
+        if (rb) PAMG_FSW(4096, 1024, true, true);
+        else PAMG_FSW(4096, 1024, true, false);
+    } else if (uni) {
+        if (rb) PAMG_FSW(1024, 512, true, true);
+        else PAMG_FSW(1024, 512, true, false);
+    } else {
+        if (rb) PAMG_FSW(1024, 512, false, true);
+        else PAMG_FSW(1024, 512, false, false);
+    }
+#undef PAMG_FSW
     return hipGetLastError();
 }
 

@@ -139,6 +139,7 @@ struct pamg_handle {
     pamg::Level lv[pamg::kMaxLevels + 1];   // 1-based
     double *geo1 = nullptr;    // U * kGeoStride
     double *tov = nullptr, *tovo = nullptr; // (slots, 3, U) t_overlap / t_overlap_old
+    double *tov_b = nullptr;   // the second t_overlap buffer of the fused face-operator sweeps (on first use)
     int slots = 0;
     int tnn_level = 1;
     // t_overlap_old and the boundary words hold what level 1's smoother writes in this
@@ -274,6 +275,11 @@ hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, i
                              double omega, int slots);
 hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov, bool neg, bool level1, double rdt,
                                 int slots);
+// one whole face-operator sweep in one launch (copy, both colours or Jacobi, the next sweep's halo
+// words into tout; single domain, un_eles of at most 4096 sub-elements)
+bool face_sweep_fusable(const Level &L);
+hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
+                                   bool rb, bool level1, double rdt, double omega, int slots);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg

@@ -1143,39 +1143,73 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
 //   waves 6,7   level 1: an adjacent pair per thread (256), and level 2: sub-elements 0..127.
 // Per tile-cycle (n_split 5, L 3), in units of 64 sub-elements x 2 smoother calls: SIMD(0,4)
 // 64 sweeps on one wave (~5.4) + 2; SIMD(1,5) 6; SIMD(2,6), SIMD(3,7) 3 + 2 + 1. No thread holds
-// two level-2 sub-elements beside its level-1 state (118 -> fewer VGPRs). Every sub-element's operations are
-// the same as in every other form (bitwise, the same tests). A tile is one un_ele or a part of
-// one (n_split >= 5), so every operator record is wave-uniform and every tile full.
+// two level-2 sub-elements beside its level-1 state (118 -> fewer VGPRs). A tile is one un_ele
+// or a part of one (n_split >= 5), so every operator record is wave-uniform and every tile full.
+//
+// One barrier per cycle. The only values that cross threads inside a cycle are the residual
+// means the restrictor (:336) reads: level l writes its means of cycle c, level l+1 reads them
+// as the RHS of cycle c+1. They sit in two LDS buffers by cycle parity, so a level-(l+1) owner
+// reads buffer (c-1) & 1 at the start of cycle c while level l fills buffer c & 1, and the
+// barrier that closes cycle c is the only one needed (the next writer of a buffer, two cycles
+// on, runs behind the barrier its readers passed). The prolongator (:370) is not computed here:
+// its output, tracer(l)%tnew, is overwritten by the smoother's first statement
+// (tnew = tnew_nonlin, :550) before anything reads it (SURVEY.md A3 iv), so within a resident
+// call -- where no observer can run between :370 and :550 -- it is dead computation like a
+// smoother call's last sweep; the per-call API and the per-step kernels execute
+// and store it. Every operation whose result is read runs, in the same order on the same values:
+// the state after the call is bitwise the per-step kernel sequence's (the same tests).
+template <int S, int L>
+struct BGeo {
+    using G = Geo<S, L>;
+    static constexpr int C = G::C;
+    // level l's residual means (0 <= l < C) in one parity buffer: level 1's T, then nt(1) ..
+    static constexpr int MO(int l) { int o = 0; for (int i = 0; i < l; ++i) o += G::nt(i); return o; }
+    static constexpr int MS = MO(C);
+    static constexpr int LDS(bool rhsf) { return 2 * MS + (rhsf ? 3 * G::T : 0); }
+};
+
+// three workgroups per CU (80 VGPRs; a few spilled words): 21,500 vs 20,330 V-cycles/s at two
+// (scripts/ab_res.sh, profiles/r02_resm_ab.txt); L = 5 keeps two (it would spill 132 B per lane)
+#ifndef PAMG_RESB_WAVES
+#define PAMG_RESB_WAVES 6
+#endif
 template <int S, int L, class ST, bool RHSF>
-__global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const double *__restrict__ sp0,
+__global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) void k_vc_resb(VArgs A, const double *__restrict__ sp0,
                                                                 const double *__restrict__ sp1,
                                                                 const double *__restrict__ sp2,
                                                                 const double *__restrict__ sp3,
                                                                 const double *__restrict__ sp4) {
     using G = Geo<S, L>;
     using P = PGeo<S, L>;
-    using R = RGeo<S, L>;
+    using B = BGeo<S, L>;
     constexpr int C = G::C, T = G::T;
     static_assert(C >= 2 && C <= 4 && T == 1024 && G::MT == 512 && S >= 5, "balanced roles: n_split >= 5, L 3..5");
-    // RHSF: the tile's source s' (3 T doubles) behind the images -- every step's RHS reads it; in
-    // registers it pushed the launch past 128 VGPRs
-    __shared__ __attribute__((aligned(16))) double F0[R::LDS() + (RHSF ? 3 * T : 0)];
-    double *const SQ = F0 + R::LDS();
-    double *const M0 = F0 + 3 * T;
-    double *const CI = F0 + R::CI();
+    // two parity buffers of residual means; RHSF: the tile's source s' (3 T doubles) behind them
+    // -- every step's RHS reads it; in registers it pushed the launch past 128 VGPRs
+    __shared__ __attribute__((aligned(16))) double MB[B::LDS(RHSF)];
+    double *const SQ = MB + 2 * B::MS;
+    auto means = [&](int c, int l) { return MB + (c & 1) * B::MS + B::MO(l); };
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const double rdt = A.rdt;
     const int ns = A.n_smooth, m = A.cycles;
     const int64_t tb = (int64_t)blockIdx.x + A.tile0;
     const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo, keepc = A.keep & kKeepCoarse;
+    const int total = A.steps * m;
+    // the restrictor (:336): the RHS of coarse sub-element i of level l from the means of its
+    // children 4i .. 4i+3 (element_conversion's fin order) on level l-1, cycle c
+    auto restrict_rhs = [&](int c, int l, int i, double b[3]) {
+        const double *Mf = means(c, l - 1);
+        b[0] = Mf[4 * i + 2];
+        b[1] = Mf[4 * i + 3];
+        b[2] = Mf[4 * i];
+    };
     // Each role runs its own cycle loop with its own state (the loop is unswitched by role, so
     // the registers of one role's loop-carried state are not reserved in the others); every
-    // role passes the same two barriers per cycle.
+    // role passes the same barrier once per cycle.
     //
     // level 2 (0-based 1), K = 1 or 2 adjacent sub-elements i0 .. i0+K-1 of the tile: load (tnew,
-    // and the RHS: RHSN), both smoother calls + get_residual + LDS images (before the cycle's
-    // barrier), restrictor + prolongator cascade (after it)
+    // and the RHS: RHSN), the cycle's RHS (restrictor), both smoother calls + get_residual + means
     auto l2_load = [&](auto kc, int i0, double (&xs)[2][3], double (&bs)[2][3], uint32_t &gc, bool &vc) {
         constexpr int K = decltype(kc)::value;
         const VLevel &V = A.lv[1];
@@ -1188,11 +1222,15 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             load3(A.rhsn2, V.pitch, gc, bs[0]);
         }
     };
-    auto l2_legs = [&](auto kc, auto lastc, int i0, double (&xs)[2][3], const double (&bs)[2][3], uint32_t gc,
+    auto l2_legs = [&](auto kc, auto lastc, int c, int i0, double (&xs)[2][3], double (&bs)[2][3], uint32_t gc,
                        bool vc) {
         constexpr int K = decltype(kc)::value;
         constexpr bool last = decltype(lastc)::value;
         const VLevel &V = A.lv[1];
+        if (c > 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) restrict_rhs(c - 1, 1, i0 + k, bs[k]);
+        }
         ST St;
         stencil(true, sp1, opaque(gc >> G::lg(1)), St);
         if (last && keepc && vc) {
@@ -1204,18 +1242,14 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
 #pragma unroll
         for (int k = 0; k < K; ++k) residual(St, rdt, xs[k], bs[k], rr[k]);   // :338
         if (vc) {
+            double *M = means(c, 1);
             if constexpr (K == 2) {
                 if (last && keepc) store3p(V.RES(), V.pitch, gc, rr[0], rr[1]);
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    *reinterpret_cast<double2 *>(CI + P::F(1) + q * P::nt(1) + i0) = make_double2(xs[0][q], xs[1][q]);
-                *reinterpret_cast<double2 *>(CI + P::M(1) + i0) =
+                *reinterpret_cast<double2 *>(M + i0) =
                     make_double2(div3(rr[0][0] + rr[0][1] + rr[0][2]), div3(rr[1][0] + rr[1][1] + rr[1][2]));
             } else {
                 if (last && keepc) store3(V.RES(), V.pitch, gc, rr[0]);
-#pragma unroll
-                for (int q = 0; q < 3; ++q) CI[P::F(1) + q * P::nt(1) + i0] = xs[0][q];
-                CI[P::M(1) + i0] = div3(rr[0][0] + rr[0][1] + rr[0][2]);
+                M[i0] = div3(rr[0][0] + rr[0][1] + rr[0][2]);
             }
         }
         sweeps_tnew<K>(St, rdt, ns, bs, xs);   // prolongation-leg call (:367-376), from that tnew
@@ -1224,24 +1258,15 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             else store3(V.T(), V.pitch, gc, xs[0]);
         }
     };
-    auto l2_restrict = [&](auto kc, auto lastc, int i0, const double (&xs)[2][3], double (&bs)[2][3], uint32_t gc,
-                           bool vc) {
+    // after the call's last cycle: level 2's RHSN, the restriction of that cycle's level-1 means
+    auto l2_rhsn = [&](auto kc, int c, int i0, uint32_t gc, bool vc) {
         constexpr int K = decltype(kc)::value;
-        constexpr bool last = decltype(lastc)::value;
         if (!vc) return;
+        double bn[2][3];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {   // level 2's restrictor (:336) and prolongator cascade (:370, dead)
-            const int i = i0 + k;
-            bs[k][0] = M0[4 * i + 2];
-            bs[k][1] = M0[4 * i + 3];
-            bs[k][2] = M0[4 * i];
-            const int fi[4] = {4 * i, 4 * i + 1, 4 * i + 2, 4 * i + 3};
-            prolong_cascade(F0, T, fi, xs[k]);
-        }
-        if (last) {
-            if constexpr (K == 2) store3p(A.rhsn2, A.lv[1].pitch, gc, bs[0], bs[1]);
-            else store3(A.rhsn2, A.lv[1].pitch, gc, bs[0]);
-        }
+        for (int k = 0; k < K; ++k) restrict_rhs(c, 1, i0 + k, bn[k]);
+        if constexpr (K == 2) store3p(A.rhsn2, A.lv[1].pitch, gc, bn[0], bn[1]);
+        else store3(A.rhsn2, A.lv[1].pitch, gc, bn[0]);
     };
     if (wv == 4) {
         // ---- the coarsest level: its restriction-leg call, get_residual, 1 + n_coarse calls
@@ -1251,8 +1276,9 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
         double xs[3], bs[3];
         load3(V.T(), V.pitch, gc, xs);
         load3(V.RHSN(), V.pitch, gc, bs);
-        auto cycle = [&](auto lastc) {
+        auto cycle = [&](int c, auto lastc) {
             constexpr bool last = decltype(lastc)::value;
+            if (c > 0) restrict_rhs(c - 1, C, lane, bs);   // (:336) of level C-1's residual of cycle c-1
             ST St;
             stencil(true, C == 2 ? sp2 : C == 3 ? sp3 : sp4, opaque(gc >> G::lg(C)), St);
             constexpr int prio = std::is_same<ST, StcF>::value ? PAMG_CHAIN_PRIO : 0;
@@ -1270,19 +1296,14 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             if (prio) __builtin_amdgcn_s_setprio(0);
             if (last && vc) store3(V.T(), V.pitch, gc, xs);
             __syncthreads();
-            if (vc) {   // restrictor (:336) of level C-1's residual; prolongator cascade (:370, dead)
-                const double *Mf = CI + P::M(C - 1);
-                bs[0] = Mf[4 * lane + 2];
-                bs[1] = Mf[4 * lane + 3];
-                bs[2] = Mf[4 * lane];
-                if (last) store3(V.RHSN(), V.pitch, gc, bs);
-                const int fi[4] = {4 * lane, 4 * lane + 1, 4 * lane + 2, 4 * lane + 3};
-                prolong_cascade(CI + P::F(C - 1), P::nt(C - 1), fi, xs);
+            if (last && vc) {   // RHSN: the restriction of level C-1's residual of the last cycle
+                double bn[3];
+                restrict_rhs(c, C, lane, bn);
+                store3(V.RHSN(), V.pitch, gc, bn);
             }
-            __syncthreads();
         };
-        for (int c = 0; c + 1 < A.steps * m; ++c) cycle(std::false_type{});
-        cycle(std::true_type{});
+        for (int c = 0; c + 1 < total; ++c) cycle(c, std::false_type{});
+        cycle(total - 1, std::true_type{});
     } else if (wv == 0) {
         // ---- level 2: sub-elements 128 + 2 lane, +1; levels 3 .. L-1 (1-based), one sub-element
         //      of each per lane (none with L = 3)
@@ -1290,7 +1311,7 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
         double x2[2][3], b2[2][3];
         uint32_t g2 = 0;
         bool v2 = false;
-        if (PAMG_RES_L2W0) l2_load(std::integral_constant<int, 2>{}, i2, x2, b2, g2, v2);
+        l2_load(std::integral_constant<int, 2>{}, i2, x2, b2, g2, v2);
         double xs[2][3] = {}, bs[2][3] = {};
         uint32_t gc[2] = {0, 0};
         bool vc[2] = {false, false};
@@ -1302,12 +1323,13 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             load3(V.RHSN(), V.pitch, gc[l - 2], bs[l - 2]);
         });
         const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
-        auto cycle = [&](auto lastc) {
+        auto cycle = [&](int c, auto lastc) {
             constexpr bool last = decltype(lastc)::value;
-            if (PAMG_RES_L2W0) l2_legs(std::integral_constant<int, 2>{}, lastc, i2, x2, b2, g2, v2);
+            l2_legs(std::integral_constant<int, 2>{}, lastc, c, i2, x2, b2, g2, v2);
             static_for<2, C>([&](auto lc) {
                 constexpr int l = decltype(lc)::value, k = l - 2;
                 const VLevel &V = A.lv[l];
+                if (c > 0) restrict_rhs(c - 1, l, lane, bs[k]);
                 ST St;
                 stencil(true, SP[l], opaque(gc[k] >> G::lg(l)), St);
                 if (last && keepc && vc[k]) store3(V.RHS(), V.pitch, gc[k], bs[k]);
@@ -1317,31 +1339,24 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                 double r[3];
                 residual(St, rdt, xs[k], bs[k], r);
                 if (last && keepc && vc[k]) store3(V.RES(), V.pitch, gc[k], r);
-                if (vc[k]) {
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) CI[P::F(l) + q * P::nt(l) + lane] = xs[k][q];
-                    CI[P::M(l) + lane] = div3(r[0] + r[1] + r[2]);
-                }
+                if (vc[k]) means(c, l)[lane] = div3(r[0] + r[1] + r[2]);
                 sweeps_tnew<1>(St, rdt, ns, b1, x1);   // prolongation-leg call (:367-376), from that tnew
                 if (last && vc[k]) store3(V.T(), V.pitch, gc[k], xs[k]);
             });
             __syncthreads();
-            if (PAMG_RES_L2W0) l2_restrict(std::integral_constant<int, 2>{}, lastc, i2, x2, b2, g2, v2);
-            static_for<2, C>([&](auto lc) {
-                constexpr int l = decltype(lc)::value, k = l - 2;
-                if (!vc[k]) return;
-                const double *Mf = CI + P::M(l - 1);
-                bs[k][0] = Mf[4 * lane + 2];
-                bs[k][1] = Mf[4 * lane + 3];
-                bs[k][2] = Mf[4 * lane];
-                if (last) store3(A.lv[l].RHSN(), A.lv[l].pitch, gc[k], bs[k]);
-                const int fi[4] = {4 * lane, 4 * lane + 1, 4 * lane + 2, 4 * lane + 3};
-                prolong_cascade(CI + P::F(l - 1), P::nt(l - 1), fi, xs[k]);
-            });
-            __syncthreads();
+            if (last) {
+                l2_rhsn(std::integral_constant<int, 2>{}, c, i2, g2, v2);
+                static_for<2, C>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value, k = l - 2;
+                    if (!vc[k]) return;
+                    double bn[3];
+                    restrict_rhs(c, l, lane, bn);
+                    store3(A.lv[l].RHSN(), A.lv[l].pitch, gc[k], bn);
+                });
+            }
         };
-        for (int c = 0; c + 1 < A.steps * m; ++c) cycle(std::false_type{});
-        cycle(std::true_type{});
+        for (int c = 0; c + 1 < total; ++c) cycle(c, std::false_type{});
+        cycle(total - 1, std::true_type{});
     } else {
         // ---- level 1 (the reference's): waves 1,2,3,5 an adjacent pair + a single sub-element
         //      per thread (N = 3), waves 6,7 a pair (N = 2) and one sub-element of level 2
@@ -1363,16 +1378,12 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             auto start_step = [&](bool last_step) {
                 if constexpr (RHSF) {
                     const double c = sp0[(size_t)__builtin_amdgcn_readfirstlane(w0) * kStcStride + kStcC];
-                    double Q[N][3];   // the thread's own s' words (written by it, no barrier)
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        const double2 v = *reinterpret_cast<const double2 *>(SQ + q * T + jp);
-                        Q[0][q] = v.x;
-                        Q[1][q] = v.y;
-                        if constexpr (N == 3) Q[2][q] = SQ[q * T + js];
+                    for (int k = 0; k < N; ++k) {   // the thread's own s' words (written by it, no barrier)
+                        const int j = k < 2 ? jp + k : js;
+                        const double q3[3] = {SQ[j], SQ[T + j], SQ[2 * T + j]};
+                        rhs_from_source(c, rdt, X0[k], q3, B0[k]);
                     }
-#pragma unroll
-                    for (int k = 0; k < N; ++k) rhs_from_source(c, rdt, X0[k], Q[k], B0[k]);
                     if (!last_step) return;
                     if (vp) {
                         if (A.keep & kKeepTold) {
@@ -1419,31 +1430,24 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
             double xs[2][3], bs[2][3];
             bool vc = false;
             uint32_t gc = 0;
-            constexpr int K2 = PAMG_RES_L2W0 ? 1 : 2;   // level-2 sub-elements of the thread
-            const int i2 = PAMG_RES_L2W0 ? gb : 2 * gb;
-            if constexpr (N == 2) l2_load(std::integral_constant<int, K2>{}, i2, xs, bs, gc, vc);
+            if constexpr (N == 2) l2_load(std::integral_constant<int, 1>{}, gb, xs, bs, gc, vc);
             auto cycle = [&](int c, auto lastc) {
                 constexpr bool last = decltype(lastc)::value;
                 ST St0;
                 stencil(true, sp0, opaque(w0), St0);
-                (void)c;
                 // restriction-leg call (:331) from tnew (tnew_nonlin := tnew, :327): its tnew, in place
                 sweeps_tnew<N>(St0, rdt, ns, B0, X0);
                 double r[N][3];
 #pragma unroll
                 for (int k = 0; k < N; ++k) residual(St0, rdt, X0[k], B0[k], r[k]);   // :338
+                double *M0 = means(c, 0);
                 if (vp) {
-#pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        *reinterpret_cast<double2 *>(F0 + q * T + jp) = make_double2(X0[0][q], X0[1][q]);
                     *reinterpret_cast<double2 *>(M0 + jp) =
                         make_double2(div3(r[0][0] + r[0][1] + r[0][2]), div3(r[1][0] + r[1][1] + r[1][2]));
                     if (last && keep1) store3p(V0.RES(), V0.pitch, sp, r[0], r[1]);
                 }
                 if constexpr (N == 3)
                     if (vq) {
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) F0[q * T + js] = X0[2][q];
                         M0[js] = div3(r[2][0] + r[2][1] + r[2][2]);
                         if (last && keep1) store3(V0.RES(), V0.pitch, sq, r[2]);
                     }
@@ -1470,22 +1474,23 @@ __global__ __launch_bounds__(512, PAMG_RES_WAVES) void k_vc_resb(VArgs A, const 
                             if (keep1) store3(V0.TNN(), V0.pitch, sq, Y0[2]);
                         }
                 }
-                if constexpr (N == 2) l2_legs(std::integral_constant<int, K2>{}, lastc, i2, xs, bs, gc, vc);
+                if constexpr (N == 2) l2_legs(std::integral_constant<int, 1>{}, lastc, c, gb, xs, bs, gc, vc);
                 __syncthreads();
-                if constexpr (N == 2) l2_restrict(std::integral_constant<int, K2>{}, lastc, i2, xs, bs, gc, vc);
-                __syncthreads();
+                if constexpr (N == 2 && last) l2_rhsn(std::integral_constant<int, 1>{}, c, gb, gc, vc);
             };
             // RHSF: A.steps time steps of m cycles; each later step starts from the tnew the
-            // previous one left (told := tnew, tnew_nonlin := tnew, :316-317)
-            const int total = A.steps * m;
-            auto next_step = [&](int c) {   // X0 holds tnew: told := tnew
-                if (RHSF && c > 0 && c % m == 0) start_step(c / m == A.steps - 1);
-            };
-            for (int c = 0; c + 1 < total; ++c) {
-                next_step(c);
-                cycle(c, std::false_type{});
+            // previous one left (told := tnew, tnew_nonlin := tnew, :316-317). The last step, whose
+            // start stores told, the RHS and the constant halo words, is peeled (so that none of its
+            // store addresses stays live across the loop).
+            int c = 0;
+            if constexpr (RHSF) {
+                for (int st = 0; st + 1 < A.steps; ++st) {
+                    if (st > 0) start_step(false);
+                    for (int k = 0; k < m; ++k, ++c) cycle(c, std::false_type{});
+                }
+                if (A.steps > 1) start_step(true);
             }
-            next_step(total - 1);
+            for (; c + 1 < total; ++c) cycle(c, std::false_type{});
             cycle(total - 1, std::true_type{});
         };
         if (grpB) level1(std::integral_constant<int, 2>{});

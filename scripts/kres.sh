@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/../p-a_multigrids_amd"
 pat=$1; shift
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -DPAMG_STAMPS=0 -DPAMG_NT=3 "$@" \
-  -Rpass-analysis=kernel-resource-usage -c csrc/pamg_vcycle.hip -o /tmp/kres_$$.o 2>&1 | python3 -c '
+  -Rpass-analysis=kernel-resource-usage -c csrc/${KRES_SRC:-pamg_vcycle.hip} -o /tmp/kres_$$.o 2>&1 | python3 -c '
 import re, sys
 pat = re.compile(sys.argv[1]); cur = None; rows = {}
 for line in sys.stdin:
