@@ -921,18 +921,22 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 // so in cycle c every level runs its calls at once, from registers: level 1 on every thread
 // (the adjacent pair, as k_vc_fine), level l >= 2 on the threads PGeo assigns it (one coarse
 // sub-element each, as the pipelined tail), the coarsest level's 1 + n_coarse calls at raised
-// priority. One barrier per cycle publishes the residual means and restriction-leg images
-// in LDS; behind it every coarse owner forms its RHS of the next cycle (the restrictor, :336)
-// and runs the prolongator cascade (:370) from its final tnew (dead, :550, executed as in
-// the other forms). A second barrier closes the cycle before those LDS images are reused.
+// priority. The only values that cross threads inside a cycle are the residual means the
+// restrictor (:336) reads: level l writes its means of cycle c into one of two LDS buffers
+// (by cycle parity), and at the start of cycle c+1 every coarse owner forms its RHS from the
+// finer level's means -- one barrier per cycle (a buffer's next writer runs two cycles on,
+// behind the barrier its readers passed). The prolongator (:370) is not computed: its output,
+// tracer(l)%tnew, is overwritten by the smoother's first statement (tnew = tnew_nonlin, :550)
+// before anything reads it (SURVEY.md A3 iv), and inside one launch no observer can run in
+// between; the per-call API and the per-step kernels execute and store it.
 // HBM sees the tile's state twice per call: loaded at the start (tnew and RHS or, starting
 // a time step (RHSF), tnew and the source s' of level 1; tnew and RHSN of the coarse
 // levels) and stored at the end, with the same final-cycle store policy as the pipelined
-// launches (VArgs::keep). Every sweep, residual, restriction and prolongation whose result is
-// read runs, in the same order on the same values (a smoother call's last sweep, which only
-// feeds a tnew_nonlin the cycle overwrites unread, is left to the compiler to drop): the state
-// after the call is bitwise the per-step kernel sequence's (tests/test_gpu_parity.py). The
-// cycle is fp64-issue-bound here, no longer HBM-bound.
+// launches (VArgs::keep). Every sweep, residual and restriction whose result is read runs,
+// in the same order on the same values (a smoother call's last sweep, which only feeds a
+// tnew_nonlin the cycle overwrites unread, is left to the compiler to drop): the state after
+// the call is bitwise the per-step kernel sequence's (tests/test_gpu_parity.py). The cycle is
+// fp64-issue-bound here, no longer HBM-bound.
 #ifndef PAMG_RES_WAVES
 #define PAMG_RES_WAVES 4
 #endif
@@ -946,6 +950,16 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 #ifndef PAMG_RES_L2W0
 #define PAMG_RES_L2W0 1
 #endif
+template <int S, int L>
+struct BGeo {
+    using G = Geo<S, L>;
+    static constexpr int C = G::C;
+    // level l's residual means (0 <= l < C) in one parity buffer: level 1's T, then nt(1) ..
+    static constexpr int MO(int l) { int o = 0; for (int i = 0; i < l; ++i) o += G::nt(i); return o; }
+    static constexpr int MS = MO(C);
+    static constexpr int LDS(bool rhsf) { return 2 * MS + (rhsf ? 3 * G::T : 0); }
+};
+
 template <int S, int L>
 struct RGeo {
     using P = PGeo<S, L>;
@@ -970,13 +984,12 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
                                                                       const double *__restrict__ sp4) {
     using G = Geo<S, L>;
     using P = PGeo<S, L>;
-    using R = RGeo<S, L>;
+    using B = BGeo<S, L>;
     constexpr int C = G::C;
     static_assert(C > 0 && G::NP == 2, "the resident launch needs a coarse level and streams pairs");
     constexpr int T = G::T, NP = 2;
-    __shared__ __attribute__((aligned(16))) double F0[R::LDS()];
-    double *const M0 = F0 + 3 * T;
-    double *const CI = F0 + R::CI();
+    __shared__ __attribute__((aligned(16))) double MB[2 * B::MS];   // residual means, two parities
+    auto means = [&](int c, int l) { return MB + (c & 1) * B::MS + B::MO(l); };
     const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
     const int t = threadIdx.x;
     const double rdt = A.rdt;
@@ -1028,10 +1041,25 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
         load3(V.T(), V.pitch, gxc, xs);
         load3(l == 1 ? A.rhsn2 : V.RHSN(), V.pitch, gxc, bs);
     });
+    // the restrictor (:336): children 4 ic .. 4 ic + 3 on level l-1, cycle c (element_conversion order)
+    auto restrict_rhs = [&](int c, int l, double b[3]) {
+        const double *Mf = means(c, l - 1);
+        b[0] = Mf[4 * ic + 2];
+        b[1] = Mf[4 * ic + 3];
+        b[2] = Mf[4 * ic];
+    };
     // one cycle; LAST: the call's last, which makes the final-cycle stores (peeled, so that no
     // store address stays live across the loop)
     auto cycle = [&](int c, auto lastc) {
         constexpr bool last = decltype(lastc)::value;
+        // ---- every coarse owner: its RHS of this cycle, the restriction of the finer level's
+        //      residual of the previous cycle (the first cycle's is RHSN)
+        if (c > 0)
+            static_for<1, C + 1>([&](auto lc) {
+                constexpr int l = decltype(lc)::value;
+                if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l) || !vc) return;
+                restrict_rhs(c - 1, l, bs);
+            });
         // ---- the coarsest level: restriction-leg call (:331 via :351), get_residual (:338),
         //      the 1 + n_coarse calls (:351-353) -- the tile's longest dependent chain, first
         if (t >= P::T0(C) && t < P::T0(C) + P::NTH(C)) {
@@ -1067,11 +1095,8 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             double r[NP][3];
 #pragma unroll
             for (int k = 0; k < NP; ++k) residual(St0, rdt, p0[k], b0[k], r[k]);
-#pragma unroll
-            for (int q = 0; q < 3; ++q)
-                *reinterpret_cast<double2 *>(F0 + q * T + 2 * t) = make_double2(p0[0][q], p0[1][q]);
             if (last && keep1) store3p(V0.RES(), V0.pitch, s0, r[0], r[1]);
-            *reinterpret_cast<double2 *>(M0 + 2 * t) =
+            *reinterpret_cast<double2 *>(means(c, 0) + 2 * t) =
                 make_double2(div3(r[0][0] + r[0][1] + r[0][2]), div3(r[1][0] + r[1][1] + r[1][2]));
         }
 #pragma unroll
@@ -1098,33 +1123,23 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             double r[3];
             residual(St, rdt, p, bs, r);
             if (last && keepc && vc) store3(V.RES(), V.pitch, gxc, r);
-            if (vc) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q) CI[P::F(l) + q * P::nt(l) + ic] = p[q];
-                CI[P::M(l) + ic] = div3(r[0] + r[1] + r[2]);
-            }
+            if (vc) means(c, l)[ic] = div3(r[0] + r[1] + r[2]);
             copy3(x, p);   // tnew_nonlin := tnew (:367)
             sweeps1(St, rdt, ns, bs, x, p);
             copy3(xs, p);
             if (last && vc) store3(V.T(), V.pitch, gxc, xs);
         });
         __syncthreads();
-        // ---- every coarse owner: the restrictor (:336) of the finer level's residual of this
-        //      cycle -- its RHS of the next cycle (stored as RHSN after the call's last) -- and
-        //      the prolongator cascade (:370) from its final tnew into the finer level's
-        //      restriction-leg image (dead, :550); the children of i are 4i .. 4i+3 (Level::pos)
-        static_for<1, C + 1>([&](auto lc) {
-            constexpr int l = decltype(lc)::value;
-            if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l) || !vc) return;
-            const double *Mf = l == 1 ? M0 : CI + P::M(l - 1);
-            bs[0] = Mf[4 * ic + 2];
-            bs[1] = Mf[4 * ic + 3];
-            bs[2] = Mf[4 * ic];
-            if (last) store3(l == 1 ? A.rhsn2 : A.lv[l].RHSN(), A.lv[l].pitch, gxc, bs);
-            const int fi[4] = {4 * ic, 4 * ic + 1, 4 * ic + 2, 4 * ic + 3};
-            prolong_cascade(l == 1 ? F0 : CI + P::F(l - 1), G::nt(l - 1), fi, xs);
-        });
-        __syncthreads();
+        // ---- after the call's last cycle: every coarse owner's RHSN, the restriction of the
+        //      finer level's residual of that cycle (the next call's first RHS)
+        if (last)
+            static_for<1, C + 1>([&](auto lc) {
+                constexpr int l = decltype(lc)::value;
+                if (t < P::T0(l) || t >= P::T0(l) + P::NTH(l) || !vc) return;
+                double bn[3];
+                restrict_rhs(c, l, bn);
+                store3(l == 1 ? A.rhsn2 : A.lv[l].RHSN(), A.lv[l].pitch, gxc, bn);
+            });
     };
     for (int c = 0; c + 1 < m; ++c) cycle(c, std::false_type{});
     cycle(m - 1, std::true_type{});
@@ -1158,16 +1173,6 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
 // smoother call's last sweep; the per-call API and the per-step kernels execute
 // and store it. Every operation whose result is read runs, in the same order on the same values:
 // the state after the call is bitwise the per-step kernel sequence's (the same tests).
-template <int S, int L>
-struct BGeo {
-    using G = Geo<S, L>;
-    static constexpr int C = G::C;
-    // level l's residual means (0 <= l < C) in one parity buffer: level 1's T, then nt(1) ..
-    static constexpr int MO(int l) { int o = 0; for (int i = 0; i < l; ++i) o += G::nt(i); return o; }
-    static constexpr int MS = MO(C);
-    static constexpr int LDS(bool rhsf) { return 2 * MS + (rhsf ? 3 * G::T : 0); }
-};
-
 // three workgroups per CU (80 VGPRs; a few spilled words): 21,500 vs 20,330 V-cycles/s at two
 // (scripts/ab_res.sh, profiles/r02_resm_ab.txt); L = 5 keeps two (it would spill 132 B per lane)
 #ifndef PAMG_RESB_WAVES
