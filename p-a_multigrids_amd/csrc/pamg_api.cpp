@@ -535,9 +535,9 @@ double vcycle_flops(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth, nc = h->p.n_coarse;
     const bool f = h->p.arith == 1;
     const double sw = f ? 24.0 : 42.0, rs = f ? 18.0 : 36.0;
-    // the balanced resident kernel (call schedule 3, n_split >= 5, L >= 3) does not compute the
-    // dead prolongator (pamg_vcycle.hip k_vc_resb); every other fused form executes its cascade
-    const bool prolong = !(call_schedule(h) == 3 && vcycle_resident_run_supported(h->p.n_split, L));
+    // the resident kernels (call schedule 3) do not compute the dead prolongator (pamg_vcycle.hip
+    // k_vc_res, k_vc_resb); every other fused form executes its cascade
+    const bool prolong = !(call_schedule(h) == 3 && vcycle_resident_supported(h->p.n_split, L));
     double fl = 0.0;
     for (int l = 1; l <= L; ++l) {
         const double n = (double)h->lv[l].N;

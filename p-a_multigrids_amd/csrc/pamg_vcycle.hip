@@ -1004,24 +1004,32 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
 #pragma unroll
     for (int k = 0; k < NP; ++k) h0[k] = v0 ? hs_pack(V0.H.hsub[(s0 + k) & ((1 << G::lg(0)) - 1)]) : 0;
     double x0[NP][3], b0[NP][3], p0[NP][3];
+    double q[NP][3];   // RHSF: the source s' of the pair, every step's RHS reads it
+    // the start of a time step (:316-317, get_RHS :452-464): told := tnew (t holds it) and the
+    // RHS from it and s'; the run's last step stores told, the step's constant halo words
+    // (kKeepTold) and the RHS it formed (kKeepL1) -- earlier steps' are overwritten unread
+    auto start_step = [&](const double (&tn)[NP][3], bool last_step) {
+        if constexpr (RHSF) {
+            const uint32_t wu = G::uni(0) ? (uint32_t)__builtin_amdgcn_readfirstlane(w0) : w0;
+            const double c = sp0[(size_t)wu * kStcStride + kStcC];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) rhs_from_source(c, rdt, tn[k], q[k], b0[k]);
+            if (last_step && v0) {
+                if (A.keep & kKeepTold) {
+                    store3p(V0.TOLD(), V0.pitch, s0, tn[0], tn[1]);
+#pragma unroll
+                    for (int k = 0; k < NP; ++k) hs_write_static(V0.H, A.send_b, w0, h0[k], tn[k]);
+                }
+                // the RHS lives in registers for the call; stored for an observer (dead inside pamg_run)
+                if (keep1) store3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
+            }
+        }
+    };
     // ---- level 1: tnew (tnew_nonlin := tnew, :327) and the RHS
     if constexpr (RHSF) {   // the start of a time step (:316-317, get_RHS :452-464), as k_vc_fine
-        double q0[3], q1[3];
         load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
-        load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, s0, q0, q1);
-        const uint32_t wu = G::uni(0) ? (uint32_t)__builtin_amdgcn_readfirstlane(w0) : w0;
-        const double c = sp0[(size_t)wu * kStcStride + kStcC];
-        rhs_from_source(c, rdt, x0[0], q0, b0[0]);
-        rhs_from_source(c, rdt, x0[1], q1, b0[1]);
-        if (v0) {
-            if (A.keep & kKeepTold) {
-                store3p(V0.TOLD(), V0.pitch, s0, x0[0], x0[1]);
-#pragma unroll
-                for (int k = 0; k < NP; ++k) hs_write_static(V0.H, A.send_b, w0, h0[k], x0[k]);
-            }
-            // the RHS lives in registers for the call; stored for an observer (dead inside pamg_run)
-            if (keep1) store3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
-        }
+        load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, s0, q[0], q[1]);
+        start_step(x0, A.steps == 1);
     } else {
         load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
         load3p<PAMG_NT_RL>(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
@@ -1141,8 +1149,20 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
                 store3(l == 1 ? A.rhsn2 : A.lv[l].RHSN(), A.lv[l].pitch, gxc, bn);
             });
     };
-    for (int c = 0; c + 1 < m; ++c) cycle(c, std::false_type{});
-    cycle(m - 1, std::true_type{});
+    // RHSF: A.steps time steps of m cycles; each later step starts from the tnew the previous
+    // one left (p0: told := tnew, and tnew_nonlin := tnew at its first cycle, :316-317); the
+    // run's last step start, which stores, is peeled out of the loop
+    const int total = A.steps * m;
+    int c = 0;
+    if constexpr (RHSF) {
+        for (int st = 0; st + 1 < A.steps; ++st) {
+            if (st > 0) start_step(p0, false);
+            for (int k = 0; k < m; ++k, ++c) cycle(c, std::false_type{});
+        }
+        if (A.steps > 1) start_step(p0, true);
+    }
+    for (; c + 1 < total; ++c) cycle(c, std::false_type{});
+    cycle(total - 1, std::true_type{});
 }
 
 // ---- balanced roles (n_split >= 5, three levels or more). In k_vc_res the coarsest level's
@@ -1717,9 +1737,9 @@ hipError_t launch_vcycle_resident(hipStream_t s, const Level *lv, int L, int U, 
                        send_b, cycles, steps);
 }
 
-// several time steps in one resident launch: the balanced-role instance
+// several time steps in one resident launch (k_vc_resb, or k_vc_res below n_split 5 and at L = 2)
 bool vcycle_resident_run_supported(int n_split, int L) {
-    return PAMG_RES_BALANCED && n_split >= 5 && n_split <= kMaxFusedSplit && L >= 3 && L <= kMaxFusedLevels;
+    return L >= 2 && L <= kMaxFusedLevels && n_split <= kMaxFusedSplit && fine_np(n_split) == 2;
 }
 
 // the resident form: two levels or more, adjacent pairs (fine_np == 2)

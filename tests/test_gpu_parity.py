@@ -500,7 +500,8 @@ def test_call_schedules_equal_one_sequence(mesh, S, L, n, arith):
 
 @pytest.mark.parametrize("mesh,S,L,n", [("untitled8192.msh", 5, 3, 2), ("irregular.msh", 4, 4, 3),
                                         ("900_ele.msh", 3, 2, 1), ("untitled2048.msh", 5, 5, 2),
-                                        ("irregular.msh", 6, 3, 2), ("irregular.msh", 7, 3, 1)])
+                                        ("irregular.msh", 6, 3, 2), ("irregular.msh", 7, 3, 1),
+                                        ("untitled2048.msh", 5, 2, 2), ("untitled8192.msh", 3, 3, 2)])
 @pytest.mark.parametrize("schedule", [1, 2, 3])
 def test_time_loop_equals_public_steps(mesh, S, L, n, schedule):
     """pamg_run skips what a step leaves that the next step overwrites unread (the step-start
