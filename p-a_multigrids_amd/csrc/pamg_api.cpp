@@ -364,10 +364,12 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
             double *buf[2] = {h->tov, h->tov_b};
             HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
             for (int s = 0; s < sweeps; ++s) {
-                Span sp(h, kid, bytes);   // read tnew_nonlin, RHS; write tnew, tnew_nonlin (+ halo words)
+                // read tnew_nonlin, RHS; write tnew_nonlin (+ tnew in the last sweep, + halo words)
+                Span sp(h, kid, (s + 1 == sweeps ? 96.0 : 72.0) * (double)L.N + 168.0 * h->U);
                 HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
                                                   s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
-                                                  h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots));
+                                                  h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots,
+                                                  s + 1 == sweeps));
             }
             return PAMG_OK;
         }

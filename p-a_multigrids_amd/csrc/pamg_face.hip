@@ -130,6 +130,8 @@ __global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, c
 // unless this is the call's last sweep, the halo words the NEXT sweep reads (update_overlaps,
 // :555, from the new tnew_nonlin that its :550 copies into tnew) written through `Hn` into the
 // other t_overlap buffer. Single domain only (a partition's halo crosses ranks between sweeps).
+// tnew is rewritten by every sweep's :550 before anything reads it, so only the call's last
+// sweep stores it (store_t; the call's first copy comes from the halo refresh before it).
 // Every sub-element's operations are face_point's, so the result is bitwise the per-colour
 // kernels' (and the oracle's).
 // (waves per SIMD: 6 for the wave-uniform 1024-tiles, 72-76 VGPRs; the others spill there)
@@ -140,7 +142,7 @@ template <int TS, int NT, bool UNI, bool RB>
 __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_sweep(double *T, double *TNN, const double *__restrict__ RHS,
                                                    const double *__restrict__ stc, const int4 *__restrict__ fnb,
                                                    const double *__restrict__ fface, const int *__restrict__ fsx,
-                                                   const double *__restrict__ tin, HaloArgs Hn, int next_halo,
+                                                   const double *__restrict__ tin, HaloArgs Hn, int next_halo, int store_t,
                                                    int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                    double rdt, double omega) {
     constexpr int PER = TS / NT;
@@ -160,7 +162,7 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
             const double v = TNN[c * pitch + s];
             b[k][c] = RHS[c * pitch + s];
             X[c][j] = v;
-            if (s0 + j < N) T[c * pitch + s] = v;
+            if (store_t && s0 + j < N) T[c * pitch + s] = v;
         }
     }
     __syncthreads();
@@ -269,25 +271,30 @@ hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, i
 bool face_sweep_fusable(const Level &L) { return L.nsub <= 4096; }
 
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots) {
+                                   bool rb, bool level1, double rdt, double omega, int slots, bool store_t) {
     if (L.N == 0) return hipSuccess;
     if (!L.fnb || !L.fface || !L.fsx || !face_sweep_fusable(L)) return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
     HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tout, tovo, P.d_send, 1 << L.isplit};
-    const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0, nh = tout ? 1 : 0;
+    const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0, nh = tout ? 1 : 0, st = store_t ? 1 : 0;
     const bool uni = L.nsub >= 64;
 #define PAMG_FSW(TS, NT, U, R)                                                                                      \
     hipLaunchKernelGGL((k_face_sweep<TS, NT, U, R>), dim3((unsigned)((L.N + TS - 1) / TS)), dim3(NT), 0, s, L.T,   \
-                       L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tin, H, nh, L.pitch, L.N, lg, slots, l1, rdt, omega)
+                       L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tin, H, nh, st, L.pitch, L.N, lg, slots, l1, rdt, omega)
+    // tiles of one un_ele of 4,096 or 1,024 sub-elements; the coarse levels in tiles of 256 (more
+    // workgroups per CU for sweeps that are short and latency-bound)
     if (L.nsub > 1024) {
         if (rb) PAMG_FSW(4096, 1024, true, true);
         else PAMG_FSW(4096, 1024, true, false);
-    } else if (uni) {
+    } else if (L.nsub == 1024) {
         if (rb) PAMG_FSW(1024, 512, true, true);
         else PAMG_FSW(1024, 512, true, false);
+    } else if (uni) {
+        if (rb) PAMG_FSW(256, 128, true, true);
+        else PAMG_FSW(256, 128, true, false);
     } else {
-        if (rb) PAMG_FSW(1024, 512, false, true);
-        else PAMG_FSW(1024, 512, false, false);
+        if (rb) PAMG_FSW(256, 128, false, true);
+        else PAMG_FSW(256, 128, false, false);
     }
 #undef PAMG_FSW
     return hipGetLastError();

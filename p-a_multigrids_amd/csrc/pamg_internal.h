@@ -279,7 +279,7 @@ hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov
 // words into tout; single domain, un_eles of at most 4096 sub-elements)
 bool face_sweep_fusable(const Level &L);
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots);
+                                   bool rb, bool level1, double rdt, double omega, int slots, bool store_t);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg

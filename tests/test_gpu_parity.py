@@ -237,7 +237,8 @@ def test_pipelined_vcycle_launches():
 
 def test_resident_vcycle_launches():
     """fused = 3, schedule 3 (automatic where it applies): a call of n cycles is one launch; a
-    pamg_run step is one launch that also starts the step (told, RHS: vcycle_res_rhsf)."""
+    pamg_run of several steps is one launch that also starts every step (told, RHS:
+    vcycle_res_rhsf)."""
     meta, _ = goldens.load("u8_s3_l3_gs")
     s = gpu_solver(meta, fused=3)
     s.timing_enable(0x3F7F)
@@ -249,14 +250,14 @@ def test_resident_vcycle_launches():
     s.timing_reset()
     s.run(2, 3)
     t = s.timing()
-    assert t["vcycle_res_rhsf"]["launches"] == 2 and t["vcycle_res"]["launches"] == 0
+    assert t["vcycle_res_rhsf"]["launches"] == 1 and t["vcycle_res"]["launches"] == 0
     assert t["rhs"]["launches"] == 0 and t["vcycle_pipe"]["launches"] == 0 and t["smooth_L1"]["launches"] == 0
     # one launch moves every level's state in and out once, whatever the number of cycles
     assert t["vcycle_res_rhsf"]["bytes"] > 0
 
 
 def test_resident_run_is_one_launch():
-    """n_split >= 5, L >= 3: a whole pamg_run (every time step: told := tnew, the RHS, n_multigrid
+    """Every resident configuration: a whole pamg_run (every time step: told := tnew, the RHS, n_multigrid
     cycles) is one resident launch; its state equals the step-by-step public calls bit for bit
     (test_time_loop_equals_public_steps, schedule 3)."""
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled2048.msh"))
