@@ -944,12 +944,9 @@ __global__ __launch_bounds__(fine_mt(S), (S >= 3) ? ((W8 || fine_np(S) == 1) ? 8
 #ifndef PAMG_RES_BALANCED
 #define PAMG_RES_BALANCED 1
 #endif
-// k_vc_resb: level 2 half on wave 0 (1: 110 VGPRs, no scratch) or all on waves 6,7 (0: 128 with
-// 12 B of scratch per lane; measured equal, profiles/r02_res_ab_variants.txt). (A prolongator cascade sequenced
-// by scheduling barriers to cut the VGPR peak further measured 15 % slower and is not kept.)
-#ifndef PAMG_RES_L2W0
-#define PAMG_RES_L2W0 1
-#endif
+// (k_vc_resb keeps half of level 2 on wave 0: all of it on waves 6, 7 measured slower,
+// profiles/r02_res_ab_variants.txt; two tiles per 1,024-thread workgroup measured equal,
+// DESIGN.md 5)
 template <int S, int L>
 struct BGeo {
     using G = Geo<S, L>;
@@ -958,14 +955,6 @@ struct BGeo {
     static constexpr int MO(int l) { int o = 0; for (int i = 0; i < l; ++i) o += G::nt(i); return o; }
     static constexpr int MS = MO(C);
     static constexpr int LDS(bool rhsf) { return 2 * MS + (rhsf ? 3 * G::T : 0); }
-};
-
-template <int S, int L>
-struct RGeo {
-    using P = PGeo<S, L>;
-    static constexpr int C = L - 1;
-    static constexpr int CI() { return 4 * Geo<S, L>::T; }   // coarse images behind F0 | M0
-    static constexpr int LDS() { return CI() + (C >= 2 ? P::M(C) : 0); }
 };
 
 // the operator records are re-fetched (scalar loads) where each phase uses them: an index the

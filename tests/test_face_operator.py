@@ -95,7 +95,9 @@ def assert_identical(sg, so):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mesh,S,L,solver,ns", [
     ("untitled8.msh", 3, 3, 3, 4), ("untitled8.msh", 3, 3, 1, 2), ("irregular.msh", 4, 3, 3, 2),
-    ("900_ele.msh", 3, 2, 3, 3), ("test_sn2.msh", 4, 2, 1, 1), ("untitled8192.msh", 3, 3, 3, 4)])
+    ("900_ele.msh", 3, 2, 3, 3), ("test_sn2.msh", 4, 2, 1, 1), ("untitled8192.msh", 3, 3, 3, 4),
+    # the fused single-domain sweep's tiles of 1,024 and 4,096 sub-elements
+    ("irregular.msh", 5, 3, 3, 2), ("irregular.msh", 6, 2, 3, 1), ("irregular.msh", 6, 2, 1, 1)])
 @pytest.mark.parametrize("cycle", [0, 1])
 def test_face_operator_is_bitwise_the_oracle(mesh, S, L, solver, ns, cycle):
     g, o = gpu_pair(mesh, S, L, solver, cycle, ns)
