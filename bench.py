@@ -268,6 +268,7 @@ def comm_report(s, world, dist):
 def main():
     a = parse()
     time_loop = None
+    roofline_hbm = None
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -317,6 +318,18 @@ def main():
         if world > 1:
             dist.barrier()
 
+    # Timed region: one barrier aligns the ranks' starts; then each rank times its own call from
+    # its own synchronized stream (no host collective inside the timed region: a gloo barrier is
+    # tens to hundreds of us of TCP, a large part of a rank's 20-cycle call at N = 8) and the
+    # elapsed times are reduced with MAX afterwards. The barrier's own cost is measured beside it.
+    barrier_us = None
+    if world > 1:
+        bt = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            dist.barrier()
+            bt.append(time.perf_counter() - t0)
+        barrier_us = 1e6 * float(np.median(bt))
     barrier()
     torch.cuda.synchronize()
     s.synchronize()
@@ -324,13 +337,16 @@ def main():
     s.vcycle(a.steps)
     s.synchronize()
     torch.cuda.synchronize()
-    barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    rank_elapsed = [elapsed]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        rank_elapsed = [None] * world
+        dist.all_gather_object(rank_elapsed, t1 - t0)
+        barrier()
     if not live_events:
         # per-launch events time each launch on its own: the post-pass runs the pipelined
         # calls as one launch per cycle (the timed region ran the partition's automatic
@@ -368,6 +384,13 @@ def main():
     extra["cycle_alg_bytes"] = tot_bytes / a.steps
     extra["cycle_alg_gbs"] = round(tot_bytes / elapsed / 1e9, 1)
     extra["comm"] = comm_report(s, world, dist)
+    if world > 1:
+        extra["rank_ms_per_step"] = [round(1e3 * v / a.steps, 5) for v in rank_elapsed]
+        extra["barrier_us"] = round(barrier_us, 1)
+        # each rank's resident kernel per cycle (post-pass events), beside the timed ms_per_step
+        kk = [None] * world
+        dist.all_gather_object(kk, ms_per_launch / cycles_per_launch)
+        extra["rank_kernel_ms_per_cycle"] = [round(v, 5) for v in kk]
     if rank == 0 and world == 1 and not a.no_extra:
         # the round-1 form on the same workload: one HBM-bound launch per cycle (call schedule 1),
         # its pipelined launch against the HBM roofline
@@ -400,6 +423,18 @@ def main():
             extra["sweep_assembled" if asm else "sweep_stencil"] = dict(
                 ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
                 frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
+            if asm:
+                # the north star's HBM roofline: one level-1 sweep of the assembled
+                # element-block-sparse operator, 168 B per sub-element (x, b, out, the 3x3 block,
+                # omega/D), HIP events around 20 launches (tests/test_roofline_kernels.py pins its output)
+                roofline_hbm = {"bound": "hbm", "kernel": "k_sweep_assembled (one level-1 Jacobi sweep over the "
+                                "assembled block-CSR operator, matrices.F90:997-1198; contracted arithmetic)",
+                                "achieved": round(by / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "traffic": pmc_traffic("sweep_assembled", a.nsplit, 1),
+                                "alg_bytes_per_launch": by, "bytes_per_sub_element": 168,
+                                "sub_elements": mesh.U * 4 ** a.nsplit, "ms_per_launch": round(ms, 4),
+                                "events": "HIP event pair around each of 20 launches"}
         time_loop = measure_time_loop(s)
         # the matrices.F90 SpMV (csr_mul_array, 3 entries per row) over the level-1 operator's
         # size in the reference's block numbering: 3 N1 rows, 52 B per row (3 x (4 B column +
@@ -471,10 +506,10 @@ def main():
         sx.vcycle(a.warmup)
         sx.synchronize()
         barrier()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         sx.vcycle(a.steps)
         sx.synchronize()
-        barrier()
         t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         extra[f"halo_exchange{mode}_vcycles_per_s"] = round(a.steps / float(t.item()), 2)
@@ -527,6 +562,7 @@ def main():
                           "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                           "alg_bytes_per_launch": bytes_per_launch, "ms_per_launch": round(ms_per_launch, 4)}),
+            "roofline_hbm_smoother": roofline_hbm,
             "cpu_baseline": ({k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")} if cpu else None),
             "time_loop": time_loop,
             "extra": extra,

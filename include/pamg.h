@@ -215,6 +215,11 @@ int pamg_timing_read(pamg_handle *h, int kid, double *ms_total, long *launches, 
  * (assembled=0: per-un_ele stencils; assembled=1: per-sub-element 3x3 blocks,
  * block-CSR with one block per block-row, the matrices.F90 format) */
 int pamg_sweep_bench(pamg_handle *h, int sweeps, int assembled, double *ms_avg, double *bytes_per_launch);
+/* one launch of the same roofline kernel, its output -- one Jacobi sweep of level 1 from
+ * tnew_nonlin and RHS (solve_Jacobi :491-497), the state untouched -- copied to host as
+ * (3, nsub_1, U): assembled = 0 in the reference's operation order, 1 in the contracted one
+ * (arith = 1); the checker of the roofline kernels (tests/test_roofline_kernels.py) */
+int pamg_sweep_bench_output(pamg_handle *h, int assembled, double *out);
 
 /* ---- local block solve: replaces FINDInv (matrix_inversion.F90:50-148 = matrices.F90:1618-1716) ----
  * nb n x n matrices, column-major (n, n, nb) host arrays as the reference's
@@ -253,6 +258,13 @@ int pamg_comm_unique_id(char out[128]);
  * bounds how long pamg_synchronize waits for the stream to drain. */
 int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int U, const int *owner);
 int pamg_owned_count(pamg_handle *h);
+/* one-rank RCCL communicator with a self-peer halo plan: the handle owns the whole mesh, but
+ * the halo words across two virtual parts (part[U], any ids) are exchanged exactly as remote
+ * words are -- packed into the send buffer, grouped ncclSend / ncclRecv to this rank itself,
+ * unpacked -- so the RCCL transport (exchange(), the async error poll) runs on one GPU. The
+ * state is bitwise that of the plain single domain (tests/test_rccl_self.py). Call before
+ * pamg_upload_mesh. */
+int pamg_comm_init_self(pamg_handle *h, const char id[128], int U, const int *part);
 /* single-process exchange of the packed halo of `level` between n partition
  * handles (created with pamg_comm_init(id = NULL)): the same send/recv
  * segments RCCL would carry, copied device to device, then unpacked */

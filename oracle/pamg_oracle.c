@@ -1111,6 +1111,35 @@ void orc_level_geometry(orc_state *s, int l, double *detwei, double *M, double *
     }
 }
 
+/* One Jacobi sweep of level l (the inner loop of the smoother, transport_tri_semi.F90:580-707,
+ * solve_Jacobi :491-497 -- equal to solve_Gauss_Seidel :501-507 for this block-diagonal operator)
+ * from given x and b, both (3, nsub, U) column-major: out = x + (omega / D) (b - A_e x), the
+ * reference's operation order (arith 0) or the contracted one of the build's arith = 1. Nothing
+ * else is touched: the checker of the level-1 roofline sweep kernels (pamg_sweep_bench_output). */
+void orc_sweep_once(orc_state *s, int l, int arith, const double *x, const double *b, double *out) {
+    int nsub = s->nsub[l - 1];
+    double rdt = 1 / s->c.dt, om = s->c.omega;
+    PAMG_ORC_PARALLEL
+    for (int u = 0; u < s->U; ++u) {
+        double M[3][3], Kd[3][3], ml[3], Ae[3][3], w[3], D[3];
+        stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+        contracted_ops(M, Kd, ml, rdt, om, Ae, w);
+        for (int i = 0; i < 3; ++i) D[i] = rdt * ml[i] + Kd[i][i] + 0.0;   /* get_diagonal :481-486 */
+        for (int se = 0; se < nsub; ++se) {
+            size_t o = (size_t)3 * ((size_t)u * nsub + se);
+            if (arith == 1) {
+                double xx[3] = {x[o], x[o + 1], x[o + 2]};
+                contracted_sweep(Ae, w, b + o, xx);
+                for (int i = 0; i < 3; ++i) out[o + i] = xx[i];
+                continue;
+            }
+            double A[3], mo[3];
+            get_A_x(s, M, Kd, rdt, x + o, x + o, A, mo);
+            for (int i = 0; i < 3; ++i) out[o + i] = x[o + i] + om / D[i] * (b[o + i] - A[i]);
+        }
+    }
+}
+
 void orc_copy_to_tnn(orc_state *s, int l) { copy_to_tnn(s, l); }
 void orc_smoother(orc_state *s, int l) { smoother(s, l); }
 void orc_get_residual(orc_state *s, int l) { get_residual(s, l); }

@@ -895,7 +895,7 @@ void free_levels(pamg_handle *h) {
         L = Level();
     }
     dev_free(h->geo1); dev_free(h->tov); dev_free(h->tovo); dev_free(h->tov_b);
-    h->geo1 = h->tov = h->tovo = nullptr;
+    h->geo1 = h->tov = h->tovo = h->tov_b = nullptr;
     h->mesh_ready = false;
 }
 
@@ -978,6 +978,22 @@ int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int
     return PAMG_OK;
 }
 
+int pamg_comm_init_self(pamg_handle *h, const char id[128], int U, const int *part) {
+    if (!h || !id || !part || U < 1) return PAMG_ERR_ARG;
+    if (h->mesh_ready) { h->err = "pamg_comm_init_self must precede pamg_upload_mesh"; return PAMG_ERR_STATE; }
+    if (h->comm) { h->err = "communicator already bound"; return PAMG_ERR_STATE; }
+    h->nranks = 1;
+    h->rank = 0;
+    h->owner.assign(U, 0);
+    h->vpart.assign(part, part + U);
+    HIPCHK(h, hipSetDevice(h->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    h->comm = new Comm;
+    NCCLCHK(h, ncclCommInitRank(&h->comm->nccl, 1, uid, 0));
+    return PAMG_OK;
+}
+
 int pamg_comm_local_group(pamg_handle *const *hs, int n) {
     if (!hs || n < 2) return PAMG_ERR_ARG;
     std::vector<int> seen(n, 0);
@@ -986,6 +1002,19 @@ int pamg_comm_local_group(pamg_handle *const *hs, int n) {
         if (!h || !h->mesh_ready || h->nranks != n || h->comm || h->rank < 0 || h->rank >= n || seen[h->rank]++)
             return PAMG_ERR_ARG;
         if (h->owner != hs[0]->owner) { h->err = "local group: the partitions' owner maps differ"; return PAMG_ERR_ARG; }
+    }
+    // create every handle's events first; bind the group only when all of them exist, so a
+    // failure leaves no handle half-bound (a retry then sees h->comm == nullptr)
+    std::vector<hipEvent_t> evs((size_t)2 * n, nullptr);
+    for (int a = 0; a < n; ++a) {
+        if (hipSetDevice(hs[a]->device) != hipSuccess ||
+            hipEventCreateWithFlags(&evs[2 * a], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&evs[2 * a + 1], hipEventDisableTiming) != hipSuccess) {
+            for (hipEvent_t e : evs)
+                if (e) (void)hipEventDestroy(e);
+            hs[a]->err = "local group: hipEventCreate failed";
+            return PAMG_ERR_HIP;
+        }
     }
     auto *G = new LocalGroup;
     G->n = n;
@@ -997,12 +1026,8 @@ int pamg_comm_local_group(pamg_handle *const *hs, int n) {
         h->comm = new Comm;
         h->comm->local = G;
         h->comm->seq.assign(n, 0);
-        if (hipSetDevice(h->device) != hipSuccess ||
-            hipEventCreateWithFlags(&h->comm->ev_ready, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&h->comm->ev_done, hipEventDisableTiming) != hipSuccess) {
-            h->err = "local group: hipEventCreate failed";
-            return PAMG_ERR_HIP;
-        }
+        h->comm->ev_ready = evs[2 * a];
+        h->comm->ev_done = evs[2 * a + 1];
     }
     return PAMG_OK;
 }
@@ -1473,6 +1498,26 @@ int pamg_sweep_bench(pamg_handle *h, int sweeps, int assembled, double *ms_avg, 
     const long n = h->timing.count[PAMG_K_SWEEP_BENCH] - n0;
     if (ms_avg) *ms_avg = (h->timing.ms[PAMG_K_SWEEP_BENCH] - ms0) / std::max(1L, n);
     if (bytes_per_launch) *bytes_per_launch = bytes;
+    return PAMG_OK;
+}
+
+int pamg_sweep_bench_output(pamg_handle *h, int assembled, double *host) {
+    if (!h || !host) return PAMG_ERR_ARG;
+    CHK(check_level(h, 1));
+    Level &L = h->lv[1];
+    const double rdt = 1 / h->p.dt;
+    // the sweep's output planes, then its (3, nsub, U) image
+    CHK(ensure_scratch(h, 6 * (size_t)L.pitch * sizeof(double)));
+    if (assembled && !L.blocks) {
+        CHK(dev_alloc(h, &L.blocks, 12 * (size_t)L.pitch));
+        HIPCHK(h, launch_build_blocks(h->stream, L, rdt));
+    }
+    if (assembled) HIPCHK(h, launch_sweep_assembled(h->stream, L, h->scratch, rdt));
+    else HIPCHK(h, launch_sweep_stencil(h->stream, L, h->scratch, rdt));
+    double *img = h->scratch + 3 * L.pitch;
+    HIPCHK(h, launch_to_aos(h->stream, L, h->scratch, img));
+    HIPCHK(h, hipMemcpyAsync(host, img, 3 * (size_t)L.N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    CHK(sync_stream(h, h->stream));
     return PAMG_OK;
 }
 

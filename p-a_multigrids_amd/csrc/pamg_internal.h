@@ -173,6 +173,9 @@ struct pamg_handle {
     // multi-GPU
     int nranks = 1, rank = 0;
     std::vector<int> owner;    // global owner map (empty = all local)
+    // self-peer plan (pamg_comm_init_self, one rank): virtual part of every un_ele; the halo
+    // words across two parts go through the RCCL communicator to this rank itself
+    std::vector<int> vpart;
     pamg::Comm *comm = nullptr;
     double *scratch = nullptr; size_t scratch_bytes = 0;
 };

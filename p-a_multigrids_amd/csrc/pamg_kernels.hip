@@ -448,15 +448,18 @@ __global__ __launch_bounds__(kBlock) void k_to_aos(const double *__restrict__ so
 // ---- roofline kernels: one unfused level-1 sweep -------------------------
 // Assembled operator (the north star's "element-block-sparse" matrix in the
 // block-CSR layout of matrices.F90:997-1198 with its single non-zero block per
-// block-row): per sub-element A = rdt*M + Kd (9 planes) and w = omega/D
-// (3 planes). Traffic per sub-element: x 24 + b 24 + out 24 + A 72 + w 24 = 168 B.
+// block-row): per sub-element the 3x3 block A_e = (1/dt) M + Kd (9 planes, the
+// operator record's kStcA words, assembled on the host in fp64) and w = omega/D
+// (3 planes). Traffic per sub-element: x 24 + b 24 + out 24 + A 72 + w 24 = 168 B
+// (SURVEY.md 8d). The sweep is the contracted arithmetic of arith = 1 (one fma chain
+// per row, pamg_device.h StcF): bitwise the oracle's orc_sweep_once(arith = 1).
 __global__ __launch_bounds__(kBlock) void k_build_blocks(const double *__restrict__ stc, double *__restrict__ blk,
-                                                         int64_t pitch, int64_t N, int nsub_log2, double rdt) {
+                                                         int64_t pitch, int64_t N, int nsub_log2) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= N) return;
     const double *r = stc + (s >> nsub_log2) * kStcStride;
 #pragma unroll
-    for (int q = 0; q < 9; ++q) blk[q * pitch + s] = rdt * r[kStcM + q] + r[kStcK + q];
+    for (int q = 0; q < 9; ++q) blk[q * pitch + s] = r[kStcA + q];
 #pragma unroll
     for (int q = 0; q < 3; ++q) blk[(9 + q) * pitch + s] = r[kStcW + q];
 }
@@ -472,14 +475,17 @@ __global__ __launch_bounds__(kBlock) void k_sweep_assembled(const double *__rest
     for (int c = 0; c < 3; ++c) { xv[c] = ld2(x + c * pitch + s); bv[c] = ld2(b + c * pitch + s); }
 #pragma unroll
     for (int q = 0; q < 12; ++q) a[q] = ld2(blk + q * pitch + s);
-    const double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
-    const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
+    StcF S0, S1;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const double A0 = a[3 * i].x * x0[0] + a[3 * i + 1].x * x0[1] + a[3 * i + 2].x * x0[2];
-        const double A1 = a[3 * i].y * x1[0] + a[3 * i + 1].y * x1[1] + a[3 * i + 2].y * x1[2];
-        st2(out + i * pitch + s, make_double2(x0[i] + a[9 + i].x * (b0[i] - A0), x1[i] + a[9 + i].y * (b1[i] - A1)));
-    }
+    for (int q = 0; q < 9; ++q) { S0.A[q] = a[q].x; S1.A[q] = a[q].y; }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) { S0.w[q] = a[9 + q].x; S1.w[q] = a[9 + q].y; }
+    double x0[3] = {xv[0].x, xv[1].x, xv[2].x}, x1[3] = {xv[0].y, xv[1].y, xv[2].y};
+    const double b0[3] = {bv[0].x, bv[1].x, bv[2].x}, b1[3] = {bv[0].y, bv[1].y, bv[2].y};
+    sweep(S0, 0.0, b0, x0);
+    sweep(S1, 0.0, b1, x1);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) st2(out + c * pitch + s, make_double2(x0[c], x1[c]));
 }
 
 // Matrix-free form of the same sweep (the reference's own structure: one
@@ -807,8 +813,9 @@ hipError_t launch_to_aos(hipStream_t s, const Level &L, const double *soa, doubl
 }
 
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt) {
+    (void)rdt;   // the blocks are the records' kStcA words, assembled with rdt on the host
     hipLaunchKernelGGL(k_build_blocks, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.stc, L.blocks, L.pitch, L.N,
-                       log2i(L.nsub), rdt);
+                       log2i(L.nsub));
     return hipGetLastError();
 }
 

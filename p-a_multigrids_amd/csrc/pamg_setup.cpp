@@ -207,6 +207,7 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
         }
     std::vector<std::pair<int, int>> remote_block((size_t)h->U * 3, std::make_pair(-1, -1));   // (peer, first index)
     const bool dist = !h->owner.empty();
+    const bool selfp = dist && !h->vpart.empty();
     std::vector<int> g2l;   // global -> local index (or -1)
     if (dist) {
         g2l.assign(h->U_global, -1);
@@ -263,7 +264,11 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
                     // kslot is i or m - i + 1 (surf_ele(i, f) sits at ipos = 2i-1 on face 1 and in row i on faces 2, 3)
                     const int rev_flag = (kslot == i) ? 0 : 1;
                     if (kslot != i && kslot != m - i + 1) { h->err = "halo: slot map"; return PAMG_ERR_STATE; }
-                    if (!dist || h->owner[ng] == h->rank) {
+                    // self-peer plan (pamg_comm_init_self): a face between two virtual parts is a
+                    // remote face whose peer is this rank itself
+                    const bool remote = selfp ? h->vpart[ng] != h->vpart[ug] : (dist && h->owner[ng] != h->rank);
+                    const int peer = selfp ? h->rank : (dist ? h->owner[ng] : 0);
+                    if (!remote) {
                         const int nl = dist ? g2l[ng] : ng;
                         if (i == 1) {
                             P.hface[3 * (size_t)q + f - 1] =
@@ -273,11 +278,11 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
                         P.local.push_back(HaloCopy{src, nl * sl * 3 + off_in_elem});
                     } else {
                         if (i == 1) {
-                            remote_block[3 * (size_t)q + f - 1] = std::make_pair(h->owner[ng], (int)by_peer[h->owner[ng]].size());
+                            remote_block[3 * (size_t)q + f - 1] = std::make_pair(peer, (int)by_peer[peer].size());
                             P.hface[3 * (size_t)q + f - 1] = make_int4(2, 0, 0, P.n_told);
                             P.n_told += m;
                         }
-                        by_peer[h->owner[ng]].push_back(HaloCopy{src, off_in_elem});
+                        by_peer[peer].push_back(HaloCopy{src, off_in_elem});
                     }
                 }
             }
@@ -287,7 +292,7 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
         // send side: peers in ascending rank order
         P.send_peer_off.push_back(0);
         for (int r = 0; r < h->nranks; ++r) {
-            if (r == h->rank) continue;
+            if (r == h->rank && !selfp) continue;
             bool has_send = !by_peer[r].empty();
             // receive side from r: enumerate r's owned elements in the same order
             std::vector<int> rd;
@@ -297,6 +302,7 @@ int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const i
                     const int f = face_order[fo];
                     const int npos = neig[3 * (size_t)ug + f - 1];
                     if (npos == 0 || h->owner[npos - 1] != h->rank) continue;
+                    if (selfp && h->vpart[npos - 1] == h->vpart[ug]) continue;
                     const int nside = fneig[3 * (size_t)ug + f - 1];
                     const int dr = dir[3 * (size_t)ug + f - 1];
                     for (int i = 1; i <= m; ++i) {

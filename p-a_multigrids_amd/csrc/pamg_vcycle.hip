@@ -1203,7 +1203,9 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     __shared__ __attribute__((aligned(16))) double MB[B::LDS(RHSF)];
     double *const SQ = MB + 2 * B::MS;
     auto means = [&](int c, int l) { return MB + (c & 1) * B::MS + B::MO(l); };
-    const int t = threadIdx.x, lane = t & 63;
+    const int t = threadIdx.x;
+    // the lane index, recomputed where it is used (mbcnt), so that it holds no VGPR across the loops
+    auto lane_id = [] { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); };
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const double rdt = A.rdt;
     const int ns = A.n_smooth, m = A.cycles;
@@ -1248,8 +1250,9 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
         ST St;
         stencil(true, sp1, opaque(gc >> G::lg(1)), St);
         if (last && keepc && vc) {
-            if constexpr (K == 2) store3p(V.RHS(), V.pitch, gc, bs[0], bs[1]);
-            else store3(V.RHS(), V.pitch, gc, bs[0]);
+            const uint32_t g = opaque(gc);
+            if constexpr (K == 2) store3p(V.RHS(), V.pitch, g, bs[0], bs[1]);
+            else store3(V.RHS(), V.pitch, g, bs[0]);
         }
         sweeps_tnew<K>(St, rdt, ns, bs, xs);   // restriction-leg call (:331): its tnew, in place
         double rr[2][3];
@@ -1258,18 +1261,19 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
         if (vc) {
             double *M = means(c, 1);
             if constexpr (K == 2) {
-                if (last && keepc) store3p(V.RES(), V.pitch, gc, rr[0], rr[1]);
+                if (last && keepc) store3p(V.RES(), V.pitch, opaque(gc), rr[0], rr[1]);
                 *reinterpret_cast<double2 *>(M + i0) =
                     make_double2(div3(rr[0][0] + rr[0][1] + rr[0][2]), div3(rr[1][0] + rr[1][1] + rr[1][2]));
             } else {
-                if (last && keepc) store3(V.RES(), V.pitch, gc, rr[0]);
+                if (last && keepc) store3(V.RES(), V.pitch, opaque(gc), rr[0]);
                 M[i0] = div3(rr[0][0] + rr[0][1] + rr[0][2]);
             }
         }
         sweeps_tnew<K>(St, rdt, ns, bs, xs);   // prolongation-leg call (:367-376), from that tnew
         if (last && vc) {
-            if constexpr (K == 2) store3p(V.T(), V.pitch, gc, xs[0], xs[1]);
-            else store3(V.T(), V.pitch, gc, xs[0]);
+            const uint32_t g = opaque(gc);
+            if constexpr (K == 2) store3p(V.T(), V.pitch, g, xs[0], xs[1]);
+            else store3(V.T(), V.pitch, g, xs[0]);
         }
     };
     // after the call's last cycle: level 2's RHSN, the restriction of that cycle's level-1 means
@@ -1279,20 +1283,21 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
         double bn[2][3];
 #pragma unroll
         for (int k = 0; k < K; ++k) restrict_rhs(c, 1, i0 + k, bn[k]);
-        if constexpr (K == 2) store3p(A.rhsn2, A.lv[1].pitch, gc, bn[0], bn[1]);
-        else store3(A.rhsn2, A.lv[1].pitch, gc, bn[0]);
+        const uint32_t g = opaque(gc);
+        if constexpr (K == 2) store3p(A.rhsn2, A.lv[1].pitch, g, bn[0], bn[1]);
+        else store3(A.rhsn2, A.lv[1].pitch, g, bn[0]);
     };
     if (wv == 4) {
         // ---- the coarsest level: its restriction-leg call, get_residual, 1 + n_coarse calls
         const VLevel &V = A.lv[C];
         bool vc;
-        const uint32_t gc = tile_index<S>(A, tb, P::nt(C), C, lane, vc);
+        const uint32_t gc = tile_index<S>(A, tb, P::nt(C), C, lane_id(), vc);
         double xs[3], bs[3];
         load3(V.T(), V.pitch, gc, xs);
         load3(V.RHSN(), V.pitch, gc, bs);
         auto cycle = [&](int c, auto lastc) {
             constexpr bool last = decltype(lastc)::value;
-            if (c > 0) restrict_rhs(c - 1, C, lane, bs);   // (:336) of level C-1's residual of cycle c-1
+            if (c > 0 && vc) restrict_rhs(c - 1, C, lane_id(), bs);   // (:336) of level C-1's residual of cycle c-1
             ST St;
             stencil(true, C == 2 ? sp2 : C == 3 ? sp3 : sp4, opaque(gc >> G::lg(C)), St);
             constexpr int prio = std::is_same<ST, StcF>::value ? PAMG_CHAIN_PRIO : 0;
@@ -1312,7 +1317,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
             __syncthreads();
             if (last && vc) {   // RHSN: the restriction of level C-1's residual of the last cycle
                 double bn[3];
-                restrict_rhs(c, C, lane, bn);
+                restrict_rhs(c, C, lane_id(), bn);
                 store3(V.RHSN(), V.pitch, gc, bn);
             }
         };
@@ -1321,7 +1326,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     } else if (wv == 0) {
         // ---- level 2: sub-elements 128 + 2 lane, +1; levels 3 .. L-1 (1-based), one sub-element
         //      of each per lane (none with L = 3)
-        const int i2 = 128 + 2 * lane;
+        const int i2 = 128 + 2 * lane_id();
         double x2[2][3], b2[2][3];
         uint32_t g2 = 0;
         bool v2 = false;
@@ -1332,7 +1337,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
         static_for<2, C>([&](auto lc) {
             constexpr int l = decltype(lc)::value;
             const VLevel &V = A.lv[l];
-            gc[l - 2] = tile_index<S>(A, tb, P::nt(l), l, lane, vc[l - 2]);
+            gc[l - 2] = tile_index<S>(A, tb, P::nt(l), l, lane_id(), vc[l - 2]);
             load3(V.T(), V.pitch, gc[l - 2], xs[l - 2]);
             load3(V.RHSN(), V.pitch, gc[l - 2], bs[l - 2]);
         });
@@ -1343,7 +1348,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
             static_for<2, C>([&](auto lc) {
                 constexpr int l = decltype(lc)::value, k = l - 2;
                 const VLevel &V = A.lv[l];
-                if (c > 0) restrict_rhs(c - 1, l, lane, bs[k]);
+                if (c > 0 && vc[k]) restrict_rhs(c - 1, l, lane_id(), bs[k]);
                 ST St;
                 stencil(true, SP[l], opaque(gc[k] >> G::lg(l)), St);
                 if (last && keepc && vc[k]) store3(V.RHS(), V.pitch, gc[k], bs[k]);
@@ -1353,7 +1358,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
                 double r[3];
                 residual(St, rdt, xs[k], bs[k], r);
                 if (last && keepc && vc[k]) store3(V.RES(), V.pitch, gc[k], r);
-                if (vc[k]) means(c, l)[lane] = div3(r[0] + r[1] + r[2]);
+                if (vc[k]) means(c, l)[lane_id()] = div3(r[0] + r[1] + r[2]);
                 sweeps_tnew<1>(St, rdt, ns, b1, x1);   // prolongation-leg call (:367-376), from that tnew
                 if (last && vc[k]) store3(V.T(), V.pitch, gc[k], xs[k]);
             });
@@ -1364,7 +1369,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
                     constexpr int l = decltype(lc)::value, k = l - 2;
                     if (!vc[k]) return;
                     double bn[3];
-                    restrict_rhs(c, l, lane, bn);
+                    restrict_rhs(c, l, lane_id(), bn);
                     store3(A.lv[l].RHSN(), A.lv[l].pitch, gc[k], bn);
                 });
             }
@@ -1379,7 +1384,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
         constexpr int hmask = (1 << G::lg(0)) - 1;
         auto level1 = [&](auto nc) {
             constexpr int N = decltype(nc)::value;   // level-1 sub-elements of the thread
-            const int ga = (wv == 5 ? 3 : wv - 1) * 64 + lane, gb = (wv - 6) * 64 + lane;
+            const int ga = (wv == 5 ? 3 : wv - 1) * 64 + lane_id(), gb = (wv - 6) * 64 + lane_id();
             const int jp = N == 3 ? 2 * ga : 768 + 2 * gb, js = 512 + ga;
             bool vp, vq = false;
             const uint32_t sp = tile_index<S>(A, tb, T, 0, jp, vp);

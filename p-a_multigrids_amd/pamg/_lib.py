@@ -88,6 +88,7 @@ def lib():
         "pamg_timing_issued": (I, [P, I, C.POINTER(C.c_long)]),
         "pamg_timing_read": (I, [P, I, C.POINTER(D), C.POINTER(C.c_long), C.POINTER(D)]),
         "pamg_sweep_bench": (I, [P, I, I, C.POINTER(D), C.POINTER(D)]),
+        "pamg_sweep_bench_output": (I, [P, I, dp]),
         "pamg_block_inverse": (I, [P, I, C.c_long, dp, dp, ip]),
         "pamg_direct_solve": (I, [P, I]),
         "pamg_write_vtu": (I, [P, C.c_char_p, I]),
@@ -101,6 +102,7 @@ def lib():
         "pamg_owned_count": (I, [P]),
         "pamg_halo_loopback": (I, [C.POINTER(P), I, I]),
         "pamg_comm_local_group": (I, [C.POINTER(P), I]),
+        "pamg_comm_init_self": (I, [P, C.c_char_p, I, ip]),
         "pamg_comm_info": (I, [P, C.POINTER(I), C.c_char_p, I]),
         "pamg_plan_build": (I, [I, dp, ip, ip, ip, I, I, I, I, ip, C.POINTER(P)]),
         "pamg_plan_sizes": (I, [P, ip]),

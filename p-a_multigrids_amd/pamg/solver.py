@@ -112,7 +112,7 @@ class SemiImplicitIterative:
 
     def __init__(self, mesh, n_split, multi_levels, n_smooth=4, solver=3, n_coarse=15, device=0,
                  dt=1.0 * 0.0000125, k=1.0, omega=0.8, halo_mode=0, comm=None, fused=3, coarse_solver=0,
-                 arith=0, halo_exchange=0, cycle=0, op=0):
+                 arith=0, halo_exchange=0, cycle=0, op=0, self_peer=None):
         self.L = lib()
         self.mesh = mesh
         self.params = default_params(n_split=n_split, multi_levels=multi_levels, n_smooth=n_smooth,
@@ -126,6 +126,11 @@ class SemiImplicitIterative:
             nranks, rank, uid, owner = comm
             owner = np.ascontiguousarray(owner, np.int32)
             self._call("pamg_comm_init", nranks, rank, uid, mesh.U, owner)
+        if self_peer is not None:
+            # one-rank RCCL communicator whose halo plan sends the words across the parts of
+            # self_peer = (unique id, part[U]) to this rank itself (pamg_comm_init_self)
+            uid, part = self_peer
+            self._call("pamg_comm_init_self", uid, mesh.U, np.ascontiguousarray(part, np.int32))
         self._call("pamg_upload_mesh", mesh.U, mesh.X, mesh.region, mesh.neig, mesh.fneig, mesh.dir)
         self.U = self.L.pamg_owned_count(self.h)
         self.n_split, self.levels = n_split, multi_levels
@@ -243,6 +248,14 @@ class SemiImplicitIterative:
         ms, by = C.c_double(), C.c_double()
         self._call("pamg_sweep_bench", sweeps, 1 if assembled else 0, C.byref(ms), C.byref(by))
         return ms.value, by.value
+
+    def sweep_bench_output(self, assembled):
+        """one launch of the level-1 roofline sweep kernel (assembled: the block-CSR operator in the
+        contracted arithmetic; else the per-un_ele stencil in the reference's order) from tnew_nonlin
+        and RHS; its output as (3, nsub_1, U) (pamg_sweep_bench_output)"""
+        out = np.empty(3 * self.nsub(1) * self.U, np.float64)
+        self._call("pamg_sweep_bench_output", 1 if assembled else 0, out)
+        return out.reshape((3, self.nsub(1), self.U), order="F")
 
 
 class Sparse:

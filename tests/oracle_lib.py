@@ -59,6 +59,8 @@ def lib():
         ipc = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
         L.orc_csr_mul_array.restype = None
         L.orc_csr_mul_array.argtypes = [C.c_long, ipc, dpc, dpc, dpc]
+        L.orc_sweep_once.restype = None
+        L.orc_sweep_once.argtypes = [P, C.c_int, C.c_int, dpc, dpc, dpc]
         for name in ("orc_copy_to_tnn", "orc_smoother", "orc_get_residual", "orc_restrictor",
                      "orc_prolongator", "orc_update_overlaps", "orc_direct_solve"):
             getattr(L, name).argtypes = [P, C.c_int]
@@ -157,6 +159,15 @@ class Oracle:
     def vcycle(self): self.L.orc_vcycle(self.h)
     def vcycle_corrected(self): self.L.orc_vcycle_corrected(self.h)
     def run(self): self.L.orc_run(self.h)
+
+    def sweep_once(self, level, arith, x, b):
+        """one Jacobi sweep of `level` from x and b, (3, nsub, U) each, the state untouched
+        (orc_sweep_once: the reference's operation order, or the contracted one with arith = 1)"""
+        xf = np.ascontiguousarray(np.asarray(x, np.float64).reshape(-1, order="F"))
+        bf = np.ascontiguousarray(np.asarray(b, np.float64).reshape(-1, order="F"))
+        out = np.empty_like(xf)
+        self.L.orc_sweep_once(self.h, level, arith, xf, bf, out)
+        return out.reshape((3, self.nsub(level), self.mesh.U), order="F")
 
     def state(self):
         d = {}

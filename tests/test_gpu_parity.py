@@ -166,16 +166,6 @@ def test_partitioned_run_matches_single_gpu(S, nparts, fused, exch):
             np.testing.assert_array_equal(x, y[:, :, own])
 
 
-def test_roofline_kernels_agree():
-    """The assembled (block-CSR) and matrix-free forms of one sweep agree to rounding."""
-    mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
-    s = pamg.SemiImplicitIterative(mesh, 3, 1)
-    s.begin_timestep()
-    ms0, b0 = s.sweep_bench(3, False)
-    ms1, b1 = s.sweep_bench(3, True)
-    assert ms0 > 0 and ms1 > 0 and b1 > b0
-
-
 def test_state_errors_are_reported():
     meta, _ = goldens.load("u8_s3_l3_gs")
     s = gpu_solver(meta)

@@ -1,0 +1,66 @@
+"""The RCCL transport itself on one GPU: a one-rank communicator with a self-peer halo plan.
+
+RCCL refuses two ranks on one GPU, so the multi-rank tests (tests/test_multirank.py) run the
+exchange path through the device-copy transport. Here the halo words across the parts of a
+virtual partition are the plan's "remote" words with this rank as their peer
+(pamg_comm_init_self): the V-cycle launches pack them into the send buffers, `exchange()`
+issues the grouped ncclSend / ncclRecv (ncclGroupStart/End, splitting.F90:1210-1397's words)
+on the one-rank communicator, the unpack kernel writes them into t_overlap, and the async
+error state is polled (ncclCommGetAsyncError) at the end of every call. Every field of every
+level, t_overlap and t_overlap_old must equal the plain single domain's bit for bit.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import goldens
+import pamg
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(mesh, S, L, parts, **kw):
+    full = pamg.SemiImplicitIterative(mesh, S, L, **kw)
+    part = mesh.x_strip_owner(parts)
+    s = pamg.SemiImplicitIterative(mesh, S, L, self_peer=(pamg.unique_id(), part), **kw)
+    assert s.comm_info()[0] == "rccl"
+    return full, s
+
+
+def _same(full, s):
+    a, b = full.state(), s.state()
+    for k in a:
+        np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+    for x, y in zip(s.overlap(), full.overlap()):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("how", ["vcycle", "run", "per_step", "halo_every_cycle"])
+def test_rccl_self_peer_exchange_is_the_single_domain(how):
+    mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
+    kw = dict(n_smooth=4, solver=3, arith=1)
+    if how == "per_step":
+        kw["fused"] = 0            # an exchange after every smoother call
+    if how == "halo_every_cycle":
+        kw["halo_exchange"] = 1    # an exchange after every cycle, on the comm stream
+    full, s = _pair(mesh, 3, 3, 4, **kw)
+    for x in (full, s):
+        if how == "run":
+            x.run(3, 2)
+        else:
+            x.begin_timestep()
+            x.vcycle(3)
+    _same(full, s)
+    s.close()
+    full.close()
+
+
+def test_rccl_self_peer_face_operator():
+    """op = 1 reads the halo every sweep: the words exchanged through RCCL are load-bearing"""
+    mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "irregular.msh"))
+    full, s = _pair(mesh, 3, 3, 3, op=1, cycle=1, n_smooth=2)
+    for x in (full, s):
+        x.begin_timestep()
+        x.vcycle(2)
+    _same(full, s)
