@@ -535,8 +535,10 @@ double vcycle_res_bytes(pamg_handle *h, int keep, bool rhsf) {
 int call_schedule(pamg_handle *h);
 double vcycle_flops(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth, nc = h->p.n_coarse;
-    const bool f = h->p.arith == 1;
-    const double sw = f ? 24.0 : 42.0, rs = f ? 18.0 : 36.0;
+    const bool f = h->p.arith == 1 && h->p.solver != 2;
+    // Richardson's update is x + omega b (a multiply and an add per component), its residual the
+    // reference's order
+    const double sw = h->p.solver == 2 ? 6.0 : f ? 24.0 : 42.0, rs = f ? 18.0 : 36.0;
     // the resident kernels (call schedule 3) do not compute the dead prolongator (pamg_vcycle.hip
     // k_vc_res, k_vc_resb); every other fused form executes its cascade
     const bool prolong = !(call_schedule(h) == 3 && vcycle_resident_supported(h->p.n_split, L));
@@ -659,6 +661,19 @@ int call_schedule(pamg_handle *h) {
     return h->nranks > 1 ? 2 : 1;
 }
 
+// the fused forms of the V-cycle apply; Richardson (solver 2) has its update only in the resident
+// call (pamg_vcycle.hip k_vc_res with StcR), so it is fused there and nowhere else
+bool fused_ok(pamg_handle *h) {
+    const int L = h->p.multi_levels;
+    if (!(h->p.fused && h->p.cycle == 0 && h->p.coarse_solver == 0 && h->p.op == 0 &&
+          vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth)))
+        return false;
+    if (h->p.solver != 2) return true;
+    return h->p.fused == 3 && h->p.halo_exchange == 0 && call_schedule(h) == 3 && !h->coarse_ahead &&
+           vcycle_resident_supported(h->p.n_split, L);
+}
+
+
 // dead_after (pamg_run, every step but the last): the next call rewrites the fields this one
 // leaves for an observer -- level 1's residual and tnew_nonlin, the coarse levels' RHS and
 // residual, the halo words -- before any read (nothing reads t_overlap, the next step's first
@@ -727,6 +742,11 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
     if (steps > 1 && !(pipe && n >= 1 && sched == 3 && h->p.halo_exchange == 0 && !h->coarse_ahead && rhs_first &&
                        vcycle_resident_run_supported(h->p.n_split, L))) {
         h->err = "internal: a resident run outside the resident schedule";
+        return PAMG_ERR_STATE;
+    }
+    if (h->p.solver == 2 && n >= 1 &&
+        !(pipe && sched == 3 && h->p.halo_exchange == 0 && !h->coarse_ahead && vcycle_resident_supported(h->p.n_split, L))) {
+        h->err = "internal: Richardson outside the resident call";
         return PAMG_ERR_STATE;
     }
     if (pipe && n >= 1 && sched == 3 && h->p.halo_exchange == 0 && !h->coarse_ahead &&
@@ -1109,7 +1129,10 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         Level &L = h->lv[l];
         L.pos = pos[l];
         L.isplit = S - l + 1;
-        L.arith = h->p.arith;
+        // the contracted arithmetic is for solvers 1 and 3; Richardson's residual keeps the
+        // reference's order (as the oracle's get_residual)
+        L.arith = h->p.solver == 2 ? 0 : h->p.arith;
+        L.richardson = h->p.solver == 2;
         L.nsub = 1 << (2 * L.isplit);
         L.N = (int64_t)L.nsub * Ul;
         L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64);
@@ -1245,7 +1268,9 @@ int pamg_get_overlap(pamg_handle *h, double *tov, double *tovo) {
 // TOLD itself (one launch instead of k_told_halo + k_overlap_static)
 int begin_timestep(pamg_handle *h, bool tnn_dead, bool told_lazy = false, bool defer_rhs = false) {
     CHK(check_level(h, 1));
-    if (defer_rhs && h->p.solver != 2) {   // the first launch of the step's fused V-cycle does k_rhs's work
+    // the first launch of the step's fused V-cycle does k_rhs's work (Richardson: the resident
+    // launch, which also rebuilds the RHS where get_residual does)
+    if (defer_rhs && (h->p.solver != 2 || fused_ok(h))) {
         h->tnn_level = 1;
         h->overlap_static_l1 = false;
         h->told_halo_stale_l1 = true;
@@ -1322,14 +1347,11 @@ int pamg_prolongator(pamg_handle *h, int level) {
 
 int vcycle(pamg_handle *h, int n, bool dead_after) {
     CHK(check_level(h, 1));
-    const int L = h->p.multi_levels;
     if (h->p.cycle == 1) {
         for (int c = 0; c < n; ++c) CHK(vcycle_corrected(h));
         return PAMG_OK;
     }
-    if (h->p.fused && h->p.coarse_solver == 0 && h->p.op == 0 &&
-        vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth))
-        return vcycle_fused(h, n, dead_after);
+    if (fused_ok(h)) return vcycle_fused(h, n, dead_after);
     for (int c = 0; c < n; ++c) CHK(vcycle_steps(h));
     return PAMG_OK;
 }
@@ -1379,8 +1401,7 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
         // through all ntime steps on-chip and only the run's final state is stored
         const int L = h->p.multi_levels;
         if (ntime >= 2 && n_multigrid >= 1 && h->p.cycle == 0 && h->p.fused == 3 && h->p.coarse_solver == 0 &&
-            h->p.op == 0 && h->p.halo_exchange == 0 && !h->coarse_ahead && call_schedule(h) == 3 &&
-            vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth) &&
+            h->p.op == 0 && h->p.halo_exchange == 0 && !h->coarse_ahead && call_schedule(h) == 3 && fused_ok(h) &&
             vcycle_resident_run_supported(h->p.n_split, L) && vcycle_rhsf_supported(h->p.n_split) &&
             !PAMG_RHS_TOLD_HALO && getenv("PAMG_NO_RHS_FUSION") == nullptr && getenv("PAMG_NO_RESIDENT_RUN") == nullptr) {
             int rc = begin_timestep(h, true, true, true);
@@ -1395,8 +1416,7 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
     }
     for (int t = 0; t < ntime; ++t) {
         const int L = h->p.multi_levels;
-        const bool fused_next = n_multigrid > 0 && h->p.cycle == 0 && h->p.fused && h->p.coarse_solver == 0 && h->p.op == 0 &&
-                                vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth);
+        const bool fused_next = n_multigrid > 0 && fused_ok(h);
         // told := tnew and the RHS inside the step's first level-1 launch when that launch is a
         // pipelined one on the one-stream schedule
         // (the resident schedule starts the step in its one launch, for any n_multigrid)

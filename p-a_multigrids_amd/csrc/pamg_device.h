@@ -144,6 +144,29 @@ __device__ __forceinline__ void resid(const StcF &S, double, const double x[3], 
     }
 }
 
+// solve_Richardson (:511-518, solver = 2): the smoother zeroes its mass, stiffness and flux terms
+// (:585-612), so a sweep is x_i + omega (b_i - (0 - 0 + 0)) = x_i + omega b_i, the reference's two
+// roundings (no contraction); get_residual keeps the full operator in the reference's order (the
+// contracted arithmetic is for solvers 1 and 3, pamg_params.arith)
+struct StcR {
+    Stc s;
+    double om;
+};
+
+__device__ __forceinline__ void load_stc(const double *__restrict__ rec, StcR &S) {
+    load_stc(rec, S.s);
+    S.om = rec[kStcOm];
+}
+
+__device__ __forceinline__ void sweep(const StcR &S, double, const double b[3], double x[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = x[i] + S.om * b[i];
+}
+
+__device__ __forceinline__ void resid(const StcR &S, double rdt, const double x[3], const double b[3], double r[3]) {
+    resid(S.s, rdt, x, b, r);
+}
+
 // Halo words written by the smoother (update_overlaps, splitting.F90:1210-1397).
 struct HaloArgs {
     const int4 *hsub;     // per sub-element: position along faces 1, 2, 3 (0 = none)

@@ -13,15 +13,16 @@ namespace pamg {
 
 constexpr int kMaxLevels = 12;
 constexpr int kMaxFusedLevels = 5;
-constexpr int kMaxFusedSplit = 7;   // fused V-cycle instances: n_split <= 7 (a tile is a part of an un_ele at >= 6)
+constexpr int kMaxFusedSplit = 8;   // fused V-cycle instances: n_split <= 8 (a tile is a part of an un_ele at >= 6)
 
 // Per (un_ele, level) operator record, fp64, 32 doubles = 256 B (two 128-B lines):
 // M (3x3 row-major) | Kd (3x3 row-major) | w = omega / D (3) | c = M_12 |
-// A = (1/dt) M + Kd (3x3 row-major, the contracted operator of arith = 1) | pad.
+// A = (1/dt) M + Kd (3x3 row-major, the contracted operator of arith = 1) | omega (the Richardson
+// update's relaxation, solve_Richardson :511-518).
 // M and Kd are get_un_ele_mass_stiff_diffvol (ShapFun_unstruc.F90:304-335) reduced as
 // transport_tri_semi.F90:592-607; D is get_diagonal (:481-486); M = c [[2,1,1],[1,2,1],[1,1,2]]
 // exactly (checked in level_stencil), which the smoother kernels use (pamg_device.h apply_A).
-constexpr int kStcM = 0, kStcK = 9, kStcW = 18, kStcC = 21, kStcA = 22, kStcStride = 32;
+constexpr int kStcM = 0, kStcK = 9, kStcW = 18, kStcC = 21, kStcA = 22, kStcOm = 31, kStcStride = 32;
 
 // Level-1 geometry record per un_ele (get_splitting, Msh2Tri.F90:69-107):
 // x3, y3, v1x, v1y, v2x, v2y (v = edge / 2**i_split), pad to 8 doubles.
@@ -107,6 +108,7 @@ struct Level {
     double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
     int arith = 0;                    // operator arithmetic of this level's kernels (pamg_params.arith)
+    bool richardson = false;          // solver 2: the Richardson update (solve_Richardson, :511-518)
     HaloPlan halo;
 };
 

@@ -169,6 +169,7 @@ void level_stencil(const double *X, int i_split, double k, double dt, double ome
         for (int j = 0; j < 3; ++j) rec[kStcA + 3 * i + j] = rdt * M[i][j] + Kd[i][j];
     }
     rec[kStcC] = M[0][1];
+    rec[kStcOm] = omega;
 }
 
 bool mass_is_p1_midpoint(const double *rec) {

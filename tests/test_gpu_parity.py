@@ -267,7 +267,9 @@ def test_resident_run_is_one_launch():
     ("untitled2048.msh", 5, 5, 3, 1), ("untitled8192.msh", 5, 3, 3, 4), ("test_sn2.msh", 4, 2, 3, 2),
     # n_split >= 6: a tile is a part of an un_ele (4 tiles at 6, 16 at 7)
     ("irregular.msh", 6, 3, 3, 4), ("irregular.msh", 7, 4, 1, 2), ("untitled2048.msh", 6, 3, 3, 4),
-    ("900_ele.msh", 6, 5, 3, 1), ("test_sn2.msh", 7, 2, 3, 1)])
+    ("900_ele.msh", 6, 5, 3, 1), ("test_sn2.msh", 7, 2, 3, 1),
+    # n_split = 8: 64 tiles per un_ele, 256 positions along an un_ele face
+    ("untitled8.msh", 8, 3, 3, 2), ("irregular.msh", 8, 5, 1, 1)])
 @pytest.mark.parametrize("fused", [1, 2, 3])
 def test_fused_vcycle_equals_kernel_sequence_bitwise(mesh, S, L, solver, ns, fused):
     """The one-launch V-cycle (pamg_vcycle.hip) computes the same operations in
@@ -427,7 +429,7 @@ def test_contracted_full_size_against_oracle(mesh, S, L):
 @pytest.mark.parametrize("mesh,S,L,ns", [("untitled8.msh", 3, 3, 1), ("irregular.msh", 3, 3, 4),
                                          ("900_ele.msh", 4, 4, 2), ("untitled2048.msh", 5, 5, 3),
                                          ("irregular.msh", 6, 3, 4), ("untitled2048.msh", 6, 4, 2),
-                                         ("irregular.msh", 7, 5, 1)])
+                                         ("irregular.msh", 7, 5, 1), ("untitled8.msh", 8, 4, 2)])
 @pytest.mark.parametrize("fused", [1, 2, 3])
 def test_contracted_fused_equals_kernel_sequence_bitwise(mesh, S, L, ns, fused):
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
@@ -561,3 +563,34 @@ def test_state_round_trip_through_the_storage_order(mesh, S, L):
     sa, sb = a.state(), b.state()
     for k in sb:
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+
+
+@pytest.mark.parametrize("mesh,S,L,ns", [("untitled8.msh", 2, 2, 4), ("irregular.msh", 3, 3, 2), ("900_ele.msh", 4, 4, 1),
+                                         ("untitled2048.msh", 5, 3, 4), ("irregular.msh", 6, 3, 3),
+                                         ("test_sn2.msh", 7, 2, 2)])
+def test_richardson_resident_equals_kernel_sequence_bitwise(mesh, S, L, ns):
+    """solver = 2 (solve_Richardson, transport_tri_semi.F90:511-518) in the resident call: the update
+    x + omega b and get_residual's rebuild of level 1's RHS from told (:865-867) after the step's
+    first smoother call. A whole pamg_run is one resident launch, the public step sequence one per
+    call; both equal the per-step kernels bit for bit, t_overlap included."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    ref = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=2, fused=0)
+    ref.run(3, 2)
+    run = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=2, fused=3)
+    run.timing_enable(0x3F7F)
+    run.timing_reset()
+    run.run(3, 2)
+    t = run.timing()
+    assert t["vcycle_res_rhsf"]["launches"] == 1 and t["smooth_L1"]["launches"] == 0
+    steps = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=2, fused=3)
+    for _ in range(3):
+        steps.begin_timestep()
+        steps.vcycle(1)
+        steps.vcycle(1)
+    sr = ref.state()
+    for s in (run, steps):
+        st = s.state()
+        for k in sr:
+            np.testing.assert_array_equal(st[k], sr[k], err_msg=k)
+        for x, y in zip(s.overlap(), ref.overlap()):
+            np.testing.assert_array_equal(x, y)
