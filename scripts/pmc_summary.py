@@ -20,7 +20,8 @@ def per_kernel(d, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].replace("pamg::(anonymous namespace)::", "").split("(")[0]
+        name = r["Kernel_Name"].replace("pamg::(anonymous namespace)::", "").replace("(anonymous namespace)::", "")
+        name = name.split("(")[0]
         acc[(name, int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
     return acc
 
@@ -39,7 +40,7 @@ def main():
                          hbm_bytes=2 * fk * 1024 + wk * 1024, n=len(f.get(key, []))))
     smooth = [r for r in rows if r["kernel"].replace("void ", "").startswith(prefix.replace("void ", ""))]
     smooth.sort(key=lambda r: -r["grid"])
-    res = {"n_split": nsplit, "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1, KiB->B",
+    res = {"n_split": nsplit, "levels": int(sys.argv[7]) if len(sys.argv) > 7 else 3, "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1, KiB->B",
            "kernels": rows}
     if smooth:
         res["hbm_bytes_per_launch"] = smooth[0]["hbm_bytes"]
