@@ -339,6 +339,46 @@ int sync_stream(pamg_handle *h, hipStream_t s) {
     }
 }
 
+// the face-coupled operator's smoother call on a single domain, one launch per sweep
+// (k_face_sweep): the halo snapshots alternate between two t_overlap buffers so that a sweep's
+// halo words for the next sweep never overwrite the ones it reads; the call's last sweep reads
+// h->tov, which therefore holds the words of its start, as after the per-colour sequence.
+// dead_last (the fused face V-cycle, vcycle_face_fused): the call's last sweep only produces a
+// tnew_nonlin that the cycle overwrites unread (:327, :348, :367) -- it is not run; the sweep before
+// it stores its result as tnew (the dead sweep's :550) and writes the dead sweep's :555 words into
+// h->tov, so tnew and t_overlap are what the full call leaves.
+bool face_fusable(pamg_handle *h, int l) {
+    static const bool fuse_env = !getenv("PAMG_FACE_FUSED") || atoi(getenv("PAMG_FACE_FUSED")) != 0;
+    return fuse_env && h->p.op == 1 && h->nranks == 1 && !h->comm && face_sweep_fusable(h->lv[l]);
+}
+
+int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) {
+    Level &L = h->lv[l];
+    h->tnn_level = l;
+    h->overlap_static_l1 = false;
+    const double rdt = 1 / h->p.dt;
+    const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
+    if (src_is_T) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
+    if (!h->tov_b) CHK(dev_alloc(h, &h->tov_b, (size_t)h->slots * 3 * std::max(h->U, 1)));
+    double *buf[2] = {h->tov, h->tov_b};
+    const int run = dead_last ? sweeps - 1 : sweeps;   // the sweeps that are executed
+    if (run <= 0) {   // a call of one dead sweep: tnew := tnew_nonlin and its :555 words
+        if (sweeps > 0) HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, true));
+        return PAMG_OK;
+    }
+    HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
+    for (int s = 0; s < run; ++s) {
+        const bool fin = s + 1 == run;
+        // read tnew_nonlin, RHS; write tnew_nonlin (+ tnew in the last sweep, + the next halo words)
+        const int store = fin ? (dead_last ? 2 : 1) : 0;
+        Span sp(h, kid, (store == 1 ? 96.0 : 72.0) * (double)L.N + 168.0 * h->U);
+        HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
+                                          s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
+                                          h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store));
+    }
+    return PAMG_OK;
+}
+
 // `sweeps` sweeps on level l reading the iterate from T (src_is_T: the leg
 // copy tnew_nonlin := tnew is folded into the launch) or from TNN.
 int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
@@ -353,26 +393,9 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
     const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
     const double bytes = 96.0 * (double)L.N + 168.0 * h->U;
     if (h->p.op == 1) {   // face-coupled operator: the halo is read, so it is refreshed (and exchanged) every sweep
+        // single domain: one launch per sweep (PAMG_FACE_FUSED=0: the per-colour sequence)
+        if (face_fusable(h, l)) return face_call(h, l, src_is_T, sweeps, false);
         if (src_is_T) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
-        // single domain: one launch per sweep (k_face_sweep), the halo snapshots alternating
-        // between two t_overlap buffers so that a sweep's halo words for the next sweep never
-        // overwrite the ones it reads; the call's last sweep reads h->tov, which therefore holds
-        // the words of its start, as after the per-colour sequence (PAMG_FACE_FUSED=0: that sequence)
-        static const bool fuse_env = !getenv("PAMG_FACE_FUSED") || atoi(getenv("PAMG_FACE_FUSED")) != 0;
-        if (fuse_env && h->nranks == 1 && !h->comm && face_sweep_fusable(L)) {
-            if (!h->tov_b) CHK(dev_alloc(h, &h->tov_b, (size_t)h->slots * 3 * std::max(h->U, 1)));
-            double *buf[2] = {h->tov, h->tov_b};
-            HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
-            for (int s = 0; s < sweeps; ++s) {
-                // read tnew_nonlin, RHS; write tnew_nonlin (+ tnew in the last sweep, + halo words)
-                Span sp(h, kid, (s + 1 == sweeps ? 96.0 : 72.0) * (double)L.N + 168.0 * h->U);
-                HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
-                                                  s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
-                                                  h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots,
-                                                  s + 1 == sweeps));
-            }
-            return PAMG_OK;
-        }
         for (int s = 0; s < sweeps; ++s) {
             HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, true));   // tnew := tnew_nonlin (:550), :555
             CHK(halo(h, l));
@@ -595,6 +618,43 @@ int vcycle_steps(pamg_handle *h) {
         CHK(prolong(h, l, true));
         CHK(smooth(h, l, false, ns));
     }
+    return PAMG_OK;
+}
+
+// The face-coupled operator's V-cycle (op = 1, cycle = 0) on a single domain, as the per-step
+// sequence above with its dead work dropped: a smoother call's last sweep only makes a
+// tnew_nonlin that the cycle overwrites before any read (:367 after the restriction leg, :348 at the
+// coarsest level, the next cycle's :327 after the prolongation leg), so it runs only in the call's
+// last cycle, where it is observable; the sweep before it leaves tnew and the dead sweep's halo words
+// (face_call), which are also what get_residual's refresh from tnew (:555 via update_overlaps) would
+// write, so the residual reads them as they are; the prolongator's output is overwritten by the
+// smoother's first statement (:550, SURVEY.md A3 iv) and is not computed. The state after a call --
+// every field of every level, t_overlap, t_overlap_old -- is bitwise the per-step sequence's
+// (tests/test_face_operator.py).
+bool face_cycle_fusable(pamg_handle *h) {
+    if (!(h->p.fused && h->p.op == 1 && h->p.cycle == 0 && h->p.coarse_solver == 0)) return false;
+    for (int l = 1; l <= h->p.multi_levels; ++l)
+        if (!face_fusable(h, l)) return false;
+    return true;
+}
+
+int vcycle_face_fused(pamg_handle *h, int n) {
+    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    const double rdt = 1 / h->p.dt;
+    for (int c = 0; c < n; ++c) {
+        const bool last = c + 1 == n;
+        for (int l = 1; l <= L; ++l) {   // :323-340
+            CHK(face_call(h, l, true, ns, true));
+            CHK(restrict_(h, l));
+            Level &V = h->lv[l];
+            h->rhsn_valid = false;
+            Span sp(h, PAMG_K_RESIDUAL, 144.0 * (double)V.N + 168.0 * h->U);
+            HIPCHK(h, launch_face_residual(h->stream, V, h->tov, false, l == 1, rdt, h->slots));
+        }
+        CHK(face_call(h, L, true, ns * h->p.n_coarse, !last));   // :344-359
+        for (int l = L - 1; l >= 1; --l) CHK(face_call(h, l, true, ns, !last));   // :363-378
+    }
+    h->tnn_level = 1;
     return PAMG_OK;
 }
 
@@ -1352,6 +1412,7 @@ int vcycle(pamg_handle *h, int n, bool dead_after) {
         return PAMG_OK;
     }
     if (fused_ok(h)) return vcycle_fused(h, n, dead_after);
+    if (face_cycle_fusable(h)) return vcycle_face_fused(h, n);
     for (int c = 0; c < n; ++c) CHK(vcycle_steps(h));
     return PAMG_OK;
 }

@@ -131,7 +131,11 @@ __global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, c
 // :555, from the new tnew_nonlin that its :550 copies into tnew) written through `Hn` into the
 // other t_overlap buffer. Single domain only (a partition's halo crosses ranks between sweeps).
 // tnew is rewritten by every sweep's :550 before anything reads it, so only the call's last
-// sweep stores it (store_t; the call's first copy comes from the halo refresh before it).
+// sweep stores it (store 1: tnew_nonlin and tnew from the sweep's start; the call's first copy
+// comes from the halo refresh before it). store 2 is the last executed sweep of a call whose final
+// sweep is dead (its tnew_nonlin is overwritten unread inside a fused V-cycle): it
+// stores its result as tnew -- the dead sweep's :550 -- and not tnew_nonlin, and its next-halo
+// words are the dead sweep's :555 ones. store 0 stores tnew_nonlin only.
 // Every sub-element's operations are face_point's, so the result is bitwise the per-colour
 // kernels' (and the oracle's).
 // (waves per SIMD: 6 for the wave-uniform 1024-tiles, 72-76 VGPRs; the others spill there)
@@ -142,7 +146,7 @@ template <int TS, int NT, bool UNI, bool RB>
 __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_sweep(double *T, double *TNN, const double *__restrict__ RHS,
                                                    const double *__restrict__ stc, const int4 *__restrict__ fnb,
                                                    const double *__restrict__ fface, const int *__restrict__ fsx,
-                                                   const double *__restrict__ tin, HaloArgs Hn, int next_halo, int store_t,
+                                                   const double *__restrict__ tin, HaloArgs Hn, int next_halo, int store,
                                                    int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                    double rdt, double omega) {
     constexpr int PER = TS / NT;
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
             const double v = TNN[c * pitch + s];
             b[k][c] = RHS[c * pitch + s];
             X[c][j] = v;
-            if (store_t && s0 + j < N) T[c * pitch + s] = v;
+            if (store == 1 && s0 + j < N) T[c * pitch + s] = v;
         }
     }
     __syncthreads();
@@ -210,12 +214,12 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
         pass(std::integral_constant<int, 2>{});
     }
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {   // tnew_nonlin
+    for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew)
         const int j = t + NT * k;
         const int64_t s = s0 + j;
         if (s < N)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) TNN[c * pitch + s] = X[c][j];
+            for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s] = X[c][j];
     }
     if (!next_halo) return;
 #pragma unroll
@@ -271,12 +275,12 @@ hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, i
 bool face_sweep_fusable(const Level &L) { return L.nsub <= 4096; }
 
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots, bool store_t) {
+                                   bool rb, bool level1, double rdt, double omega, int slots, int store) {
     if (L.N == 0) return hipSuccess;
     if (!L.fnb || !L.fface || !L.fsx || !face_sweep_fusable(L)) return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
     HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tout, tovo, P.d_send, 1 << L.isplit};
-    const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0, nh = tout ? 1 : 0, st = store_t ? 1 : 0;
+    const int lg = log2i(L.nsub), l1 = level1 ? 1 : 0, nh = tout ? 1 : 0, st = store;
     const bool uni = L.nsub >= 64;
 #define PAMG_FSW(TS, NT, U, R)                                                                                      \
     hipLaunchKernelGGL((k_face_sweep<TS, NT, U, R>), dim3((unsigned)((L.N + TS - 1) / TS)), dim3(NT), 0, s, L.T,   \

@@ -283,8 +283,10 @@ hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov
 // one whole face-operator sweep in one launch (copy, both colours or Jacobi, the next sweep's halo
 // words into tout; single domain, un_eles of at most 4096 sub-elements)
 bool face_sweep_fusable(const Level &L);
+// store: 0 tnew_nonlin; 1 tnew_nonlin and tnew (the sweep's start); 2 tnew := the result only (the
+// last executed sweep of a call whose final sweep is dead)
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots, bool store_t);
+                                   bool rb, bool level1, double rdt, double omega, int slots, int store);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg

@@ -86,8 +86,6 @@ struct VArgs {
     int cycles;             // the resident launch: cycles of the call (of each time step)
     int steps;              // the resident launch starting time steps (RHSF): steps of the run, each
                             // told := tnew and its RHS, then `cycles` cycles; 1 otherwise
-    unsigned *claim;        // k_vc_resb: per-CU mask of the SIMDs hosting a coarsest chain (null: off)
-    int want_claim;         // the dispatcher's request for it (each n_split's code object has its own mask)
 };
 
 }  // namespace vc
@@ -1046,6 +1044,8 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
     if constexpr (RHSF) {   // the start of a time step (:316-317, get_RHS :452-464), as k_vc_fine
         load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
         load3p<PAMG_NT_RL>(V0.SRC(), V0.pitch, s0, q[0], q[1]);
+        // Richardson: the step's first smoother call reads the RHS the previous get_residual built
+        if constexpr (RICH) load3p(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
         start_step(x0, A.steps == 1);
     } else {
         load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
@@ -1233,76 +1233,6 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
 #define PAMG_RESB_WAVES 6
 #endif
 
-// Chain placement. The hardware puts waves w and w+4 of a 512-thread workgroup on one SIMD
-// (scripts/micro/wave_simd.hip), so wave 4's SIMD -- the coarsest chain, 753 of a tile's ~2,370
-// wave-instructions per cycle, with the 172 of wave 0 -- carries 925 units against 516 on each of
-// the other three. Workgroups that run in lockstep (a partition whose tiles all start at once: one
-// round at N = 8) and land their chains on one SIMD leave that SIMD the bottleneck: with random
-// placement of 3-4 workgroups per CU the busiest SIMD carries ~1.2x the mean. So the chain role
-// goes to the wave pair on a SIMD that no other resident workgroup's chain occupies: a per-CU mask
-// (global memory, one word per CU: XCC, SE, SH, CU ids from the hardware registers) claimed with a
-// vector atomicOr by thread 0 and released when the chain's last cycle is done. The mask is only a
-// placement hint -- a lost race or a full mask leaves a valid role map -- and the roles (vw) are
-// a permutation of the wave indices, remapped only when the four wave pairs are verified to sit
-// on four distinct SIMDs, so every role runs exactly once whatever the hardware does.
-__device__ unsigned g_chain_claim[2048];
-
-// the claimed word (-1: none) and bit, for the release by the chain wave
-struct ChainClaim {
-    int key, bit;
-};
-
-__device__ __forceinline__ unsigned *vgpr_ptr(unsigned *p) {
-    uint64_t v = reinterpret_cast<uint64_t>(p);
-    __asm__ volatile("" : "+v"(v));
-    return reinterpret_cast<unsigned *>(v);
-}
-
-// the workgroup's role index of wave t >> 6 (a permutation of 0..7 keeping the pairs w, w+4)
-__device__ __forceinline__ int chain_roles(unsigned *mask, int t, ChainClaim &cl) {
-    __shared__ int sid[8];
-    __shared__ int sch, skey;
-    const int w = t >> 6;
-    unsigned hw, xcc;
-    __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const int simd = (hw >> 4) & 3;
-    if ((t & 63) == 0) sid[w] = simd;
-    __syncthreads();
-    bool ok = true;
-    int seen = 0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        ok = ok && sid[p + 4] == sid[p];
-        seen |= 1 << sid[p];
-    }
-    ok = ok && seen == 15;
-    if (t == 0) {
-        int c = sid[4], key = -1;
-        if (ok) {
-            const int k0 = (int)(((xcc & 7u) << 8) | ((hw >> 8) & 0xffu));   // XCC, SE, SH, CU
-            unsigned *m = vgpr_ptr(mask + k0);
-            for (int k = 0; k < 4; ++k) {
-                const int q = (sid[4] + k) & 3;
-                const unsigned old = atomicOr(m, 1u << q);
-                if (!(old & (1u << q))) { c = q; key = k0; break; }
-            }
-        }
-        sch = c;
-        skey = key;
-    }
-    __syncthreads();
-    cl.key = skey;
-    cl.bit = sch;
-    if (!ok) return __builtin_amdgcn_readfirstlane(w);
-    return __builtin_amdgcn_readfirstlane(((simd - sch) & 3) + (w >= 4 ? 4 : 0));
-}
-
-// the chain wave, after its last cycle: the SIMD is free for the next workgroup's chain
-__device__ __forceinline__ void chain_release(unsigned *mask, const ChainClaim &cl) {
-    if (mask && cl.key >= 0 && (threadIdx.x & 63) == 0) atomicAnd(vgpr_ptr(mask + cl.key), ~(1u << cl.bit));
-}
-
 template <int S, int L, class ST, bool RHSF>
 __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) void k_vc_resb(VArgs A, const double *__restrict__ sp0,
                                                                 const double *__restrict__ sp1,
@@ -1322,10 +1252,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     const int t = threadIdx.x;
     // the lane index, recomputed where it is used (mbcnt), so that it holds no VGPR across the loops
     auto lane_id = [] { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); };
-    // roles by SIMD (A.claim): the coarsest chain goes to the wave pair on a SIMD of this CU that
-    // hosts no other workgroup's chain (chain_roles); otherwise wave 4 carries it
-    ChainClaim cl{-1, 0};
-    const int wv = A.claim ? chain_roles(A.claim, t, cl) : __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const double rdt = A.rdt;
     const int ns = A.n_smooth, m = A.cycles;
     const int64_t tb = (int64_t)blockIdx.x + A.tile0;
@@ -1442,7 +1369,6 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
         };
         for (int c = 0; c + 1 < total; ++c) cycle(c, std::false_type{});
         cycle(total - 1, std::true_type{});
-        chain_release(A.claim, cl);
     } else if (wv == 0) {
         // ---- level 2: sub-elements 128 + 2 lane, +1; levels 3 .. L-1 (1-based), one sub-element
         //      of each per lane (none with L = 3)

@@ -10,16 +10,6 @@
 
 namespace pamg {
 hipError_t PAMG_VC_CAT(launch_vcycle_s, PAMG_VC_S)(hipStream_t s, vc::VArgs A, unsigned grid, int L, int part, int ar) {
-    A.claim = nullptr;
-    if (A.want_claim) {   // k_vc_resb's chain-placement mask: this code object's own g_chain_claim
-        static unsigned *claim_ptr[64] = {};
-        int dev = 0;
-        if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-            if (!claim_ptr[dev] && hipGetSymbolAddress((void **)&claim_ptr[dev], HIP_SYMBOL(g_chain_claim)) != hipSuccess)
-                claim_ptr[dev] = nullptr;
-            A.claim = claim_ptr[dev];
-        }
-    }
     return launch_s<PAMG_VC_S>(s, A, grid, L, part, ar);
 }
 }  // namespace pamg

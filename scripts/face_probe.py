@@ -10,8 +10,9 @@ sys.path.insert(0, os.path.join(ROOT, "p-a_multigrids_amd"))
 import pamg  # noqa: E402
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+CYCLES = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1]
 mesh = pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "untitled8192.msh"))
-for cycle in (0, 1):
+for cycle in CYCLES:
     s = pamg.SemiImplicitIterative(mesh, S, 3, n_smooth=4, solver=3, op=1, cycle=cycle)
     s.begin_timestep()
     s.vcycle(3)

@@ -97,7 +97,9 @@ def assert_identical(sg, so):
     ("untitled8.msh", 3, 3, 3, 4), ("untitled8.msh", 3, 3, 1, 2), ("irregular.msh", 4, 3, 3, 2),
     ("900_ele.msh", 3, 2, 3, 3), ("test_sn2.msh", 4, 2, 1, 1), ("untitled8192.msh", 3, 3, 3, 4),
     # the fused single-domain sweep's tiles of 1,024 and 4,096 sub-elements
-    ("irregular.msh", 5, 3, 3, 2), ("irregular.msh", 6, 2, 3, 1), ("irregular.msh", 6, 2, 1, 1)])
+    ("irregular.msh", 5, 3, 3, 2), ("irregular.msh", 6, 2, 3, 1), ("irregular.msh", 6, 2, 1, 1),
+    # one sweep per call (every sweep of the fused cycle's non-final calls is dead), one level
+    ("irregular.msh", 4, 3, 3, 1), ("untitled8.msh", 3, 1, 3, 2)])
 @pytest.mark.parametrize("cycle", [0, 1])
 def test_face_operator_is_bitwise_the_oracle(mesh, S, L, solver, ns, cycle):
     g, o = gpu_pair(mesh, S, L, solver, cycle, ns)
@@ -133,3 +135,28 @@ def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, s
             np.testing.assert_array_equal(v, ref[k][:, :, own], err_msg=f"rank {r} {k}")
         for x, y in zip(p.overlap(), ref_ov):
             np.testing.assert_array_equal(x, y[:, :, own])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,solver,ns", [("untitled8192.msh", 4, 3, 3, 4), ("irregular.msh", 6, 3, 1, 2),
+                                                ("900_ele.msh", 3, 3, 3, 1), ("test_sn2.msh", 4, 4, 3, 3)])
+def test_face_fused_cycle_equals_per_step_sequence(mesh, S, L, solver, ns):
+    """The fused face V-cycle (vcycle_face_fused: dead last sweeps and the dead prolongator dropped,
+    the residual reading the halo its smoother call left) leaves the per-step sequence's state bit
+    for bit, whatever the split of the cycles into calls (only a call's last cycle runs its calls'
+    last sweeps)."""
+    import pamg
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    ref = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, op=1, fused=0)
+    ref.begin_timestep()
+    ref.vcycle(4)
+    rs, rov = ref.state(), ref.overlap()
+    for split in ([4], [1, 3], [1, 1, 1, 1]):
+        g = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, op=1)
+        g.begin_timestep()
+        for n in split:
+            g.vcycle(n)
+        assert_identical(g.state(), rs)
+        for x, y in zip(g.overlap(), rov):
+            np.testing.assert_array_equal(x, y)
+        g.close()
