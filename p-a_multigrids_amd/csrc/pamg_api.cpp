@@ -347,6 +347,65 @@ int sync_stream(pamg_handle *h, hipStream_t s) {
 // tnew_nonlin that the cycle overwrites unread (:327, :348, :367) -- it is not run; the sweep before
 // it stores its result as tnew (the dead sweep's :550) and writes the dead sweep's :555 words into
 // h->tov, so tnew and t_overlap are what the full call leaves.
+// the persistent chain (pamg_face.hip k_face_chain) for a smoother call of level l: a single
+// domain whose level fits one workgroup per CU (face_chain_fits); PAMG_FACE_CHAIN=0 turns it off
+bool face_chain_ok(pamg_handle *h, int l) {
+    static const bool env = !getenv("PAMG_FACE_CHAIN") || atoi(getenv("PAMG_FACE_CHAIN")) != 0;
+    if (!env || h->nranks != 1 || h->comm || h->neig_local.empty()) return false;
+    if (!h->cus) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || n <= 0) n = 1;
+        h->cus = n;
+    }
+    return face_chain_fits(h->lv[l].nsub, h->U, h->cus);
+}
+
+// its neighbour lists: workgroup w owns un_eles [w k, (w+1) k); its neighbours are the other
+// workgroups owning a neighbour of one of them (they write the halo words w reads)
+int face_chain_setup(pamg_handle *h, int l) {
+    Level &L = h->lv[l];
+    if (L.chain_g) return PAMG_OK;
+    const int U = h->U, g0 = std::max(1, std::min(h->cus, U)), k = (U + g0 - 1) / g0, G = (U + k - 1) / k;
+    std::vector<int> off(1, 0), list;
+    for (int w = 0; w < G; ++w) {
+        std::vector<int> nb;
+        for (int q = w * k; q < std::min(U, (w + 1) * k); ++q)
+            for (int f = 0; f < 3; ++f) {
+                const int n = h->neig_local[3 * (size_t)q + f];
+                if (n >= 0 && n / k != w) nb.push_back(n / k);
+            }
+        std::sort(nb.begin(), nb.end());
+        nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+        list.insert(list.end(), nb.begin(), nb.end());
+        off.push_back((int)list.size());
+    }
+    if (list.empty()) list.push_back(0);
+    CHK(dev_upload(h, &L.chain_nb_off, off));
+    CHK(dev_upload(h, &L.chain_nb_list, list));
+    // the polled words in one block of their own, a multiple of 16 bytes from the allocation's start
+    L.chain_flag_bytes = ((size_t)G * sizeof(unsigned) + 15) / 16 * 16;
+    CHK(dev_alloc(h, &L.chain_flags, L.chain_flag_bytes / sizeof(unsigned)));
+    if (!h->chain_tmo) {
+        CHK(dev_alloc(h, &h->chain_tmo, 4));
+        HIPCHK(h, hipMemsetAsync(h->chain_tmo, 0, 4 * sizeof(unsigned), h->stream));
+    }
+    L.chain_g = G;
+    return PAMG_OK;
+}
+
+// the sticky give-up word of the chain's bounded spins: a call that hit it failed
+int face_chain_check(pamg_handle *h) {
+    if (!h->chain_tmo) return PAMG_OK;
+    unsigned v = 0;
+    HIPCHK(h, hipMemcpyAsync(&v, h->chain_tmo, sizeof v, hipMemcpyDeviceToHost, h->stream));
+    CHK(sync_stream(h, h->stream));
+    if (v) {
+        h->err = "face chain: a workgroup gave up waiting for its neighbours' halo words";
+        return PAMG_ERR_HIP;
+    }
+    return PAMG_OK;
+}
+
 bool face_fusable(pamg_handle *h, int l) {
     static const bool fuse_env = !getenv("PAMG_FACE_FUSED") || atoi(getenv("PAMG_FACE_FUSED")) != 0;
     return fuse_env && h->p.op == 1 && h->nranks == 1 && !h->comm && face_sweep_fusable(h->lv[l]);
@@ -367,6 +426,16 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         return PAMG_OK;
     }
     HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
+    if (run >= 2 && face_chain_ok(h, l)) {   // the whole call in one launch
+        CHK(face_chain_setup(h, l));
+        HIPCHK(h, hipMemsetAsync(L.chain_flags, 0, L.chain_flag_bytes, h->stream));
+        // the state crosses HBM once per call: tnew_nonlin and RHS in, tnew (+ tnew_nonlin) out
+        Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
+        HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags, L.chain_nb_off,
+                                    L.chain_nb_list, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
+                                    l == 1, rdt, h->p.omega, h->slots));
+        return PAMG_OK;
+    }
     for (int s = 0; s < run; ++s) {
         const bool fin = s + 1 == run;
         // read tnew_nonlin, RHS; write tnew_nonlin (+ tnew in the last sweep, + the next halo words)
@@ -655,7 +724,7 @@ int vcycle_face_fused(pamg_handle *h, int n) {
         for (int l = L - 1; l >= 1; --l) CHK(face_call(h, l, true, ns, !last));   // :363-378
     }
     h->tnn_level = 1;
-    return PAMG_OK;
+    return face_chain_check(h);
 }
 
 // the corrected V-cycle (params.cycle = 1; oracle orc_vcycle_corrected):
@@ -968,6 +1037,7 @@ void free_levels(pamg_handle *h) {
         Level &L = h->lv[l];
         dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.d_pos); dev_free(L.blocks);
         dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx);
+        dev_free(L.chain_nb_off); dev_free(L.chain_nb_list); dev_free(L.chain_flags);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
         dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
@@ -1151,6 +1221,17 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
     h->Xo.resize(6 * h->owned.size());
     for (size_t q = 0; q < h->owned.size(); ++q)
         for (int c = 0; c < 6; ++c) h->Xo[6 * q + c] = X[6 * (size_t)h->owned[q] + c];
+    h->neig_local.clear();
+    if (h->p.op == 1) {   // the face chain's workgroup neighbour lists (face_chain_setup)
+        std::vector<int> g2l(U, -1);
+        for (size_t q = 0; q < h->owned.size(); ++q) g2l[h->owned[q]] = (int)q;
+        h->neig_local.assign(3 * h->owned.size(), -1);
+        for (size_t q = 0; q < h->owned.size(); ++q)
+            for (int f = 0; f < 3; ++f) {
+                const int n = neig[3 * (size_t)h->owned[q] + f];
+                if (n >= 1 && n <= U) h->neig_local[3 * q + f] = g2l[n - 1];
+            }
+    }
     for (int g = 0; g < U; ++g)
         for (int f = 0; f < 3; ++f) {
             const int n = neig[3 * g + f];
@@ -1374,7 +1455,8 @@ int pamg_smoother(pamg_handle *h, int level, int n_calls) {
         h->err = "smoother: tnew_nonlin holds another level (call pamg_copy_to_nonlin first)";
         return PAMG_ERR_STATE;
     }
-    return smooth(h, level, false, h->p.n_smooth * n_calls);
+    CHK(smooth(h, level, false, h->p.n_smooth * n_calls));
+    return h->p.op == 1 ? face_chain_check(h) : PAMG_OK;
 }
 
 int pamg_sweep(pamg_handle *h, int level, int n_sweeps) {
@@ -1384,7 +1466,8 @@ int pamg_sweep(pamg_handle *h, int level, int n_sweeps) {
         h->err = "sweep: tnew_nonlin holds another level (call pamg_copy_to_nonlin first)";
         return PAMG_ERR_STATE;
     }
-    return smooth(h, level, false, n_sweeps);
+    CHK(smooth(h, level, false, n_sweeps));
+    return h->p.op == 1 ? face_chain_check(h) : PAMG_OK;
 }
 
 int pamg_restrictor(pamg_handle *h, int level) {
@@ -1414,7 +1497,7 @@ int vcycle(pamg_handle *h, int n, bool dead_after) {
     if (fused_ok(h)) return vcycle_fused(h, n, dead_after);
     if (face_cycle_fusable(h)) return vcycle_face_fused(h, n);
     for (int c = 0; c < n; ++c) CHK(vcycle_steps(h));
-    return PAMG_OK;
+    return h->p.op == 1 ? face_chain_check(h) : PAMG_OK;
 }
 
 int pamg_vcycle(pamg_handle *h, int n) {
@@ -1617,6 +1700,7 @@ int pamg_destroy(pamg_handle *h) {
     if (h->stream_c) (void)hipStreamSynchronize(h->stream_c);
     free_levels(h);
     dev_free(h->scratch);
+    dev_free(h->chain_tmo);
     for (auto e : h->timing.pool) (void)hipEventDestroy(e);
     for (auto &r : h->timing.pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     if (h->comm) {

@@ -177,6 +177,27 @@ struct HaloArgs {
     int m;                // 2**i_split sub-elements per face
 };
 
+// Words another workgroup of the same launch reads (the persistent face-operator chain,
+// pamg_face.hip k_face_chain): written through to the device-coherent level (a relaxed agent-scope
+// atomic store of the 8-byte pattern on a global-address-space pointer: global_store_dwordx2 sc1)
+// and read the same way (global_load_dwordx2 sc1, which bypasses this CU's L1), the hand-off form
+// of cdna_hip_programming.md 6 Guideline 16 (R1) with one workgroup per CU
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef __attribute__((address_space(1))) unsigned g_u32;
+__device__ __forceinline__ void st_coh(double *p, double x) {
+    __hip_atomic_store((g_u64 *)p, (unsigned long long)__double_as_longlong(x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_coh(const double *p) {
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((g_u64 *)const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+template <bool COH>
+__device__ __forceinline__ void st_halo(double *p, double x) {
+    if constexpr (COH) st_coh(p, x);
+    else *p = x;
+}
+
 // The reference rewrites the halo at the start of every sweep from the then
 // current tnew (:550-556); the last write of a smoother call therefore carries
 // the iterate before the last sweep, which is what these threads hold in p[].
@@ -187,7 +208,8 @@ struct HaloArgs {
 // not change within a time step (t_overlap_old from told, the boundary values of
 // both arrays, the told half of a send entry). The per-step kernels write both;
 // the fused V-cycle writes TNEW only and leaves STATIC to k_overlap_static.
-template <bool TNEW = true, bool STATIC = true>
+// COH: the t_overlap words are written through (st_coh) for readers in other workgroups
+template <bool TNEW = true, bool STATIC = true, bool COH = false>
 __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, int i, const double t[3],
                                           const double to[3]) {
     const int mode = rec.x & 3;
@@ -196,8 +218,8 @@ __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, in
         const int a = (i - 1) * 3 + (f == 3 ? 1 : 0);
         const int b = (i - 1) * 3 + (f == 2 ? 1 : 2);
         const double2 v = H.bcv[rec.z + i - 1];
-        H.tov[rec.y + a] = v.x;
-        H.tov[rec.y + b] = v.y;
+        st_halo<COH>(H.tov + rec.y + a, v.x);
+        st_halo<COH>(H.tov + rec.y + b, v.y);
         H.tovo[rec.y + a] = v.x;
         H.tovo[rec.y + b] = v.y;
     } else if (mode == 1) {   // neighbour on this rank: t_overlap(slot, Nside) of the neighbour
@@ -205,7 +227,7 @@ __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, in
         const int64_t d = rec.y + (int64_t)(k - 1) * 3;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            if (TNEW) H.tov[d + c] = t[c];
+            if (TNEW) st_halo<COH>(H.tov + d + c, t[c]);
             if (STATIC) H.tovo[d + c] = to[c];
         }
     } else {                  // neighbour on another rank: packed send buffer (RCCL)
@@ -249,16 +271,17 @@ __device__ __forceinline__ void halo_prefetch(const HaloArgs &H, int64_t s, int6
     }
 }
 
+template <bool COH = false>
 __device__ __forceinline__ void halo_write(const HaloArgs &H, const HaloPre &P, const double p0[3],
                                            const double p1[3]) {
     if (!P.any) return;
     const double t0[3] = {P.a0, P.a1, P.a2}, t1[3] = {P.c0, P.c1, P.c2};
-    if (P.hs0.x) halo_face(H, P.r1, 1, P.hs0.x, p0, t0);
-    if (P.hs0.y) halo_face(H, P.r2, 2, P.hs0.y, p0, t0);
-    if (P.hs0.z) halo_face(H, P.r3, 3, P.hs0.z, p0, t0);
-    if (P.hs1.x) halo_face(H, P.r1, 1, P.hs1.x, p1, t1);
-    if (P.hs1.y) halo_face(H, P.r2, 2, P.hs1.y, p1, t1);
-    if (P.hs1.z) halo_face(H, P.r3, 3, P.hs1.z, p1, t1);
+    if (P.hs0.x) halo_face<true, true, COH>(H, P.r1, 1, P.hs0.x, p0, t0);
+    if (P.hs0.y) halo_face<true, true, COH>(H, P.r2, 2, P.hs0.y, p0, t0);
+    if (P.hs0.z) halo_face<true, true, COH>(H, P.r3, 3, P.hs0.z, p0, t0);
+    if (P.hs1.x) halo_face<true, true, COH>(H, P.r1, 1, P.hs1.x, p1, t1);
+    if (P.hs1.y) halo_face<true, true, COH>(H, P.r2, 2, P.hs1.y, p1, t1);
+    if (P.hs1.z) halo_face<true, true, COH>(H, P.r3, 3, P.hs1.z, p1, t1);
 }
 
 

@@ -18,6 +18,8 @@
 #include "pamg_device.h"
 #include "pamg_internal.h"
 
+#include <algorithm>
+
 namespace pamg {
 namespace {
 
@@ -48,10 +50,12 @@ __global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *_
 // MODE <= 2 the smoother update x_i + omega / D_i (b_i - (A x)_i), MODE 3 / 4 the residual
 // A x - b / b - A x. x: the sub-element's values; xin(c, q): component c of the inner neighbour
 // at un_ele position q; tov: the halo snapshot (t_overlap) the sweep reads.
-template <int MODE, class XIN>
+// COH: the halo words are read through to the device-coherent level (ld_coh): the persistent chain's
+// snapshot is written by other workgroups of the same launch
+template <int MODE, class XIN, bool COH = false>
 __device__ __forceinline__ void face_point(const XIN &xin, const double x[3], const double b[3], int4 nb, int64_t u,
                                            const double *__restrict__ stc, const double *__restrict__ fface,
-                                           const int *__restrict__ fsx, const double *__restrict__ tov, int slots,
+                                           const int *__restrict__ fsx, const double *tov, int slots,
                                            int level1, double rdt, double omega, double out[3]) {
     Stc S;
     load_stc(stc + u * kStcStride, S);
@@ -75,8 +79,13 @@ __device__ __forceinline__ void face_point(const XIN &xin, const double x[3], co
                 yb = 0.0;
             } else {
                 const double *slot = tov + u * slots * 3 + (int64_t)(mface - 1) * slots + (int64_t)(-nbf[fi] - 1) * 3;
-                ya = slot[(sx & 3) - 1];
-                yb = slot[((sx >> 2) & 3) - 1];
+                if constexpr (COH) {
+                    ya = ld_coh(slot + (sx & 3) - 1);
+                    yb = ld_coh(slot + ((sx >> 2) & 3) - 1);
+                } else {
+                    ya = slot[(sx & 3) - 1];
+                    yb = slot[((sx >> 2) & 3) - 1];
+                }
             }
             wf = w[3 + mface - 1];
         }
@@ -234,6 +243,150 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
     }
 }
 
+// ---- the persistent chain: every sweep of one smoother call in ONE launch, for a level whose
+// iterate fits in the LDS of one workgroup per CU (the coarsest level of the face-coupled V-cycle:
+// 524,288 sub-elements at n_split = 5, L = 3 -- 62 of the cycle's 74 sweeps). Workgroup w keeps the
+// iterate of its un_eles [w k, (w+1) k) in LDS for the whole call (no HBM traffic between sweeps)
+// and the RHS in registers. A sweep reads a halo snapshot that the PREVIOUS sweep of every
+// neighbouring workgroup wrote (update_overlaps, :555), so the workgroups hand the words over inside
+// the launch (cdna_hip_programming.md 6 Guideline 16, R1 with one workgroup per CU): each writes its
+// next-sweep words through to the coherent level (st_coh), drains them (s_waitcnt vmcnt(0) in every
+// wave, then the barrier) and publishes one flag word, flags[w] = sweeps done; before its sweep s a
+// workgroup polls (one wave, relaxed agent-scope loads, s_sleep) the flags of the workgroups owning
+// its un_eles' neighbours until each is >= s, and reads the words with ld_coh only. The snapshot
+// buffers alternate as in face_call; a neighbour can overwrite buffer (s+1) & 1 only after it has
+// seen flags[w] >= s, i.e. after w has finished sweep s - 1, the last reader of that buffer. Every
+// sub-element's arithmetic is face_point's, so the result is bitwise the per-sweep launches'. The
+// spin is bounded: a workgroup that waits > 2^22 polls sets *tmo and goes on (the host reports the
+// call as failed). Resident by construction: grid <= CUs, 1,024 threads, launched cooperatively.
+constexpr int kChainNT = 1024, kChainPer = 2;   // threads, sub-elements per thread (<= 2,048 per workgroup)
+
+template <bool UNI, bool RB>
+__global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *TNN, const double *__restrict__ RHS,
+                                                          const double *__restrict__ stc, const int4 *__restrict__ fnb,
+                                                          const double *__restrict__ fface, const int *__restrict__ fsx,
+                                                          double *buf0, double *buf1, HaloArgs H, unsigned *flags,
+                                                          const int *__restrict__ nb_off, const int *__restrict__ nb_list,
+                                                          unsigned *tmo, int run, int total, int store, int E,
+                                                          int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
+                                                          double rdt, double omega) {
+    constexpr int NT = kChainNT, PER = kChainPer;
+    __shared__ double X[3][NT * PER];
+    const int t = threadIdx.x, w = blockIdx.x;
+    const int64_t s0 = (int64_t)w * E;
+    const int64_t nsm = (1ll << nsub_log2) - 1;
+    double b[PER][3];
+    int4 nbr[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int j = t + NT * k;
+        const bool v = j < E && s0 + j < N;
+        const int64_t s = v ? s0 + j : s0;
+        nbr[k] = fnb[s & nsm];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            b[k][c] = RHS[c * pitch + s];
+            X[c][j] = TNN[c * pitch + s];
+        }
+    }
+    __syncthreads();
+    auto pass = [&](auto mc, const double *tin) {
+        constexpr int MODE = decltype(mc)::value;
+        double r[PER][3];
+        bool on[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = t + NT * k;
+            const int64_t s = s0 + j;
+            on[k] = false;
+            if (j >= E || s >= N) continue;
+            int64_t u = s >> nsub_log2;
+            if (UNI) u = __builtin_amdgcn_readfirstlane((int)u);
+            const int4 nb = nbr[k];
+            if ((MODE == 0 && !nb.w) || (MODE == 1 && nb.w)) continue;
+            on[k] = true;
+            const int jb = (int)((u << nsub_log2) - s0);
+            double x[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[c] = X[c][j];
+            auto xin = [&](int c, int q) { return X[c][jb + q]; };
+            face_point<MODE, decltype(xin), true>(xin, x, b[k], nb, u, stc, fface, fsx, tin, slots, level1, rdt, omega,
+                                                  r[k]);
+            if (MODE != 2)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) X[c][j] = r[k][c];
+        }
+        if (MODE == 2) {
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PER; ++k)
+                if (on[k])
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][t + NT * k] = r[k][c];
+        }
+        __syncthreads();
+    };
+    const int na = nb_off[w], nn = nb_off[w + 1] - na;
+    for (int sw = 0; sw < run; ++sw) {
+        const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
+        double *tout = sw + 1 < total ? (((total - 2 - sw) & 1) ? buf1 : buf0) : nullptr;
+        if (sw > 0 && t < 64) {   // wait for the neighbours' words of this sweep: one wave polls
+            for (int base = 0; base < nn; base += 64) {
+                const int i = base + t;
+                const unsigned *f = i < nn ? flags + nb_list[na + i] : nullptr;
+                bool ok = f == nullptr;
+                for (unsigned spins = 0;; ++spins) {
+                    if (!ok) ok = __hip_atomic_load((g_u32 *)const_cast<unsigned *>(f), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)sw;
+                    if (__all(ok)) break;
+                    if (spins > (1u << 22)) {
+                        if (t == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+        }
+        __syncthreads();
+        if (store == 1 && sw + 1 == run)   // the call's last sweep: tnew := tnew_nonlin (:550)
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                const int j = t + NT * k;
+                if (j < E && s0 + j < N)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = X[c][j];
+            }
+        if constexpr (RB) {
+            pass(std::integral_constant<int, 0>{}, tin);
+            pass(std::integral_constant<int, 1>{}, tin);
+        } else {
+            pass(std::integral_constant<int, 2>{}, tin);
+        }
+        if (tout) {   // the next sweep's halo words (:550, :555 of sweep sw + 1), written through
+            HaloArgs Hn = H;
+            Hn.tov = tout;
+            const int j = 2 * t;   // an adjacent pair per thread (PER = 2)
+            const int64_t s = s0 + j;
+            if (j < E && s < N) {
+                HaloPre hp;
+                halo_prefetch(Hn, s, s >> nsub_log2, nsub_log2, hp);
+                const double p0[3] = {X[0][j], X[1][j], X[2][j]}, p1[3] = {X[0][j + 1], X[1][j + 1], X[2][j + 1]};
+                halo_write<true>(Hn, hp, p0, p1);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+            __syncthreads();
+            if (t == 0) __hip_atomic_store((g_u32 *)flags + w, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew, the dead last sweep's :550)
+        const int j = t + NT * k;
+        if (j < E && s0 + j < N)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+    }
+}
+
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 inline int log2i(int v) { int r = 0; while ((1 << r) < v) ++r; return r; }
 
@@ -302,6 +455,39 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
     }
 #undef PAMG_FSW
     return hipGetLastError();
+}
+
+int face_chain_per_wg(int nsub, int U, int cus) {
+    const int g = std::max(1, std::min(cus, U));
+    const int k = (U + g - 1) / g;
+    return (int)std::min<int64_t>((int64_t)k * nsub, 1 << 30);
+}
+
+bool face_chain_fits(int nsub, int U, int cus) { return U >= 1 && face_chain_per_wg(nsub, U, cus) <= kChainNT * kChainPer; }
+
+hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
+                             unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
+                             int store, bool rb, bool level1, double rdt, double omega, int slots) {
+    if (L.N == 0 || run <= 0) return hipSuccess;
+    if (!face_chain_fits(L.nsub, U, cus) || !L.fnb) return hipErrorInvalidValue;
+    const int g = std::max(1, std::min(cus, U));
+    const int k = (U + g - 1) / g;
+    const int grid = (U + k - 1) / k;
+    const int E = k * L.nsub;
+    const HaloPlan &P = L.halo;
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << L.isplit};
+    int lg = log2i(L.nsub), l1 = level1 ? 1 : 0;
+    double *T = L.T, *TNN = L.TNN;
+    const double *RHS = L.RHS, *stc = L.stc, *fface = L.fface;
+    const int4 *fnb = L.fnb;
+    const int *fsx = L.fsx;
+    int64_t pitch = L.pitch, N = L.N;
+    void *args[] = {&T, &TNN, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
+                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega};
+    const bool uni = L.nsub >= 64;
+    const void *f = uni ? (rb ? (const void *)k_face_chain<true, true> : (const void *)k_face_chain<true, false>)
+                        : (rb ? (const void *)k_face_chain<false, true> : (const void *)k_face_chain<false, false>);
+    return hipLaunchCooperativeKernel(f, dim3(grid), dim3(kChainNT), args, 0, s);
 }
 
 hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov, bool neg, bool level1, double rdt,

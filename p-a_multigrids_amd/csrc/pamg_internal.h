@@ -107,6 +107,12 @@ struct Level {
     int *fsx = nullptr;
     double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
+    // the persistent face chain (pamg_face.hip k_face_chain; lazy): its workgroups' neighbour lists
+    // (CSR over chain_g workgroups) and the flag words it polls (zeroed before every launch)
+    int chain_g = 0;
+    int *chain_nb_off = nullptr, *chain_nb_list = nullptr;
+    unsigned *chain_flags = nullptr;
+    size_t chain_flag_bytes = 0;
     int arith = 0;                    // operator arithmetic of this level's kernels (pamg_params.arith)
     bool richardson = false;          // solver 2: the Richardson update (solve_Richardson, :511-518)
     HaloPlan halo;
@@ -180,6 +186,10 @@ struct pamg_handle {
     std::vector<int> vpart;
     pamg::Comm *comm = nullptr;
     double *scratch = nullptr; size_t scratch_bytes = 0;
+    // op = 1: the local un_eles' neighbours (0-based local ids, -1: none or another rank), 3 per un_ele
+    std::vector<int> neig_local;
+    unsigned *chain_tmo = nullptr;   // sticky give-up word of the face chain's bounded spins
+    int cus = 0;                     // compute units of the device
 };
 
 // ---- setup (pamg_setup.cpp) ----
@@ -287,6 +297,15 @@ bool face_sweep_fusable(const Level &L);
 // last executed sweep of a call whose final sweep is dead)
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
                                    bool rb, bool level1, double rdt, double omega, int slots, int store);
+// the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of
+// the call's `total` sweeps in one launch, the iterate in LDS, the halo handed over between
+// workgroups inside the launch; store 1: tnew (the last sweep's start) and tnew_nonlin, 2: tnew :=
+// the result (dead last sweep)
+bool face_chain_fits(int nsub, int U, int cus);
+int face_chain_per_wg(int nsub, int U, int cus);
+hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
+                             unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
+                             int store, bool rb, bool level1, double rdt, double omega, int slots);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg
