@@ -19,6 +19,9 @@
 #include "pamg_internal.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 namespace pamg {
 namespace {
@@ -50,19 +53,19 @@ __global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *_
 // MODE <= 2 the smoother update x_i + omega / D_i (b_i - (A x)_i), MODE 3 / 4 the residual
 // A x - b / b - A x. x: the sub-element's values; xin(c, q): component c of the inner neighbour
 // at un_ele position q; tov: the halo snapshot (t_overlap) the sweep reads.
-// COH: the halo words are read through to the device-coherent level (ld_coh): the persistent chain's
-// snapshot is written by other workgroups of the same launch
-template <int MODE, class XIN, bool COH = false>
+// hv(u, mface, sp, k): component k of slot sp of t_overlap(:, mface) of un_ele u, the halo snapshot
+// the sweep reads (global memory, or the persistent chain's LDS image of it)
+template <int MODE, class XIN, class HV>
 __device__ __forceinline__ void face_point(const XIN &xin, const double x[3], const double b[3], int4 nb, int64_t u,
                                            const double *__restrict__ stc, const double *__restrict__ fface,
-                                           const int *__restrict__ fsx, const double *tov, int slots,
-                                           int level1, double rdt, double omega, double out[3]) {
+                                           const int *__restrict__ fsx, const HV &hv, int level1, double rdt,
+                                           double omega, double out[3]) {
     Stc S;
     load_stc(stc + u * kStcStride, S);
     double A[3];
     apply_A(S, rdt, x, A);
     const double *w = fface + u * kFaceStride;
-    double ds[3] = {0.0, 0.0, 0.0}, D[3] = {w[6], w[7], w[8]};
+    double ds[3] = {0.0, 0.0, 0.0};
     const int nbf[3] = {nb.x, nb.y, nb.z};
 #pragma unroll
     for (int fi = 0; fi < 3; ++fi) {
@@ -78,26 +81,22 @@ __device__ __forceinline__ void face_point(const XIN &xin, const double x[3], co
                 ya = 0.0;     // coarse levels carry the error equation: homogeneous boundary data
                 yb = 0.0;
             } else {
-                const double *slot = tov + u * slots * 3 + (int64_t)(mface - 1) * slots + (int64_t)(-nbf[fi] - 1) * 3;
-                if constexpr (COH) {
-                    ya = ld_coh(slot + (sx & 3) - 1);
-                    yb = ld_coh(slot + ((sx >> 2) & 3) - 1);
-                } else {
-                    ya = slot[(sx & 3) - 1];
-                    yb = slot[((sx >> 2) & 3) - 1];
-                }
+                ya = hv(u, mface, -nbf[fi], (sx & 3) - 1);
+                yb = hv(u, mface, -nbf[fi], ((sx >> 2) & 3) - 1);
             }
             wf = w[3 + mface - 1];
         }
         ds[a] = ds[a] + wf * (((2.0 * x[a] + x[bb]) - 2.0 * ya) - yb);
         ds[bb] = ds[bb] + wf * (((x[a] + 2.0 * x[bb]) - ya) - 2.0 * yb);
-        D[a] = D[a] + 2.0 * wf;
-        D[bb] = D[bb] + 2.0 * wf;
     }
+    // omega / D_i of the sub-element's pattern of inner faces (kFaceWD: D accumulated and divided on
+    // the host in the oracle's order -- no division here)
+    const double *wd = w + kFaceWD + 3 * ((nbf[0] >= 0) | ((nbf[1] >= 0) << 1) | ((nbf[2] >= 0) << 2));
+    (void)omega;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const double ai = A[i] + ds[i];
-        if (MODE <= 2) out[i] = x[i] + omega / D[i] * (b[i] - ai);
+        if (MODE <= 2) out[i] = x[i] + wd[i] * (b[i] - ai);
         else if (MODE == 3) out[i] = ai - b[i];
         else out[i] = b[i] - ai;
     }
@@ -127,7 +126,8 @@ __global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, c
         b[c] = RHS[c * pitch + s];
     }
     auto xin = [&](int c, int q) { return X[c * pitch + base + q]; };
-    face_point<MODE>(xin, x, b, nb, u, stc, fface, fsx, tov, slots, level1, rdt, omega, r);
+    auto hv = [&](int64_t uu, int mf, int sp, int k) { return tov[uu * slots * 3 + (int64_t)(mf - 1) * slots + (sp - 1) * 3 + k]; };
+    face_point<MODE>(xin, x, b, nb, u, stc, fface, fsx, hv, level1, rdt, omega, r);
 #pragma unroll
     for (int i = 0; i < 3; ++i) OUT[i * pitch + s] = r[i];
 }
@@ -200,7 +200,10 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
 #pragma unroll
             for (int c = 0; c < 3; ++c) x[c] = X[c][j];
             auto xin = [&](int c, int q) { return X[c][jb + q]; };
-            face_point<MODE>(xin, x, b[k], nb, u, stc, fface, fsx, tin, slots, level1, rdt, omega, r[k]);
+            auto hv = [&](int64_t uu, int mf, int sp, int kk) {
+                return tin[uu * slots * 3 + (int64_t)(mf - 1) * slots + (sp - 1) * 3 + kk];
+            };
+            face_point<MODE>(xin, x, b[k], nb, u, stc, fface, fsx, hv, level1, rdt, omega, r[k]);
             // a colour's values are read only by the other colour: in place (red-black)
             if (MODE != 2)
 #pragma unroll
@@ -243,6 +246,121 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
     }
 }
 
+// ---- the streamed sweep: k_face_sweep's work on whole-un_ele tiles (TS a multiple of nsub, so every
+// tile has the same neighbour records), by a grid of two workgroups per CU that loop over the tiles
+// with the next tile's tnew_nonlin and RHS in flight while the current one is smoothed: the one-
+// launch-per-tile form serialises each workgroup's load, passes and stores (SQ: 79 % of the waves'
+// cycles waiting, r03_b_face_sq.txt). Same operations per sub-element (face_point), same stores.
+template <int TS, int NT, bool RB>
+__global__ __launch_bounds__(NT, 2 * NT / 256) void k_face_stream(double *T, double *TNN, const double *__restrict__ RHS,
+                                                                const double *__restrict__ stc,
+                                                                const int4 *__restrict__ fnb,
+                                                                const double *__restrict__ fface,
+                                                                const int *__restrict__ fsx, const double *__restrict__ tin,
+                                                                HaloArgs Hn, int next_halo, int store, int64_t pitch,
+                                                                int64_t N, int nsub_log2, int slots, int level1, double rdt,
+                                                                double omega, int ntiles) {
+    constexpr int PER = TS / NT;
+    static_assert(PER == 2, "an adjacent pair of sub-elements per thread");
+    __shared__ double X[3][TS];
+    const int t = threadIdx.x;
+    const int64_t nsm = (1ll << nsub_log2) - 1;
+    int4 nbr[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) nbr[k] = fnb[(t + NT * k) & nsm];
+    double b[PER][3], pn[PER][3], pb[PER][3];
+    auto fetch = [&](int tl) {
+        const int64_t s0 = (int64_t)tl * TS;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int64_t s = s0 + t + NT * k < N ? s0 + t + NT * k : s0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                pn[k][c] = TNN[c * pitch + s];
+                pb[k][c] = RHS[c * pitch + s];
+            }
+        }
+    };
+    int tile = blockIdx.x;
+    if (tile < ntiles) fetch(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t s0 = (int64_t)tile * TS;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {   // tnew := tnew_nonlin (:550); the iterate into LDS
+            const int j = t + NT * k;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                X[c][j] = pn[k][c];
+                b[k][c] = pb[k][c];
+                if (store == 1 && s0 + j < N) T[c * pitch + s0 + j] = pn[k][c];
+            }
+        }
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight during the passes
+        __syncthreads();
+        auto pass = [&](auto mc) {
+            constexpr int MODE = decltype(mc)::value;
+            double r[PER][3];
+            bool on[PER];
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                const int j = t + NT * k;
+                const int64_t s = s0 + j;
+                on[k] = false;
+                if (s >= N) continue;
+                const int64_t u = __builtin_amdgcn_readfirstlane((int)(s >> nsub_log2));
+                const int4 nb = nbr[k];
+                if ((MODE == 0 && !nb.w) || (MODE == 1 && nb.w)) continue;
+                on[k] = true;
+                const int jb = (int)((u << nsub_log2) - s0);
+                double x[3];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) x[c] = X[c][j];
+                auto xin = [&](int c, int q) { return X[c][jb + q]; };
+                auto hv = [&](int64_t uu, int mf, int sp, int kk) {
+                    return tin[uu * slots * 3 + (int64_t)(mf - 1) * slots + (sp - 1) * 3 + kk];
+                };
+                face_point<MODE>(xin, x, b[k], nb, u, stc, fface, fsx, hv, level1, rdt, omega, r[k]);
+                if (MODE != 2)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][j] = r[k][c];
+            }
+            if (MODE == 2) {
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < PER; ++k)
+                    if (on[k])
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) X[c][t + NT * k] = r[k][c];
+            }
+            __syncthreads();
+        };
+        if constexpr (RB) {
+            pass(std::integral_constant<int, 0>{});
+            pass(std::integral_constant<int, 1>{});
+        } else {
+            pass(std::integral_constant<int, 2>{});
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew)
+            const int j = t + NT * k;
+            if (s0 + j < N)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+        }
+        if (next_halo) {   // the next sweep's halo words, an adjacent pair per thread
+            const int j = 2 * t;
+            const int64_t s = s0 + j;
+            if (s < N) {
+                HaloPre hp;
+                halo_prefetch(Hn, s, s >> nsub_log2, nsub_log2, hp);
+                const double p0[3] = {X[0][j], X[1][j], X[2][j]}, p1[3] = {X[0][j + 1], X[1][j + 1], X[2][j + 1]};
+                halo_write(Hn, hp, p0, p1);
+            }
+        }
+        __syncthreads();   // X is rewritten by the next tile
+    }
+}
+
 // ---- the persistent chain: every sweep of one smoother call in ONE launch, for a level whose
 // iterate fits in the LDS of one workgroup per CU (the coarsest level of the face-coupled V-cycle:
 // 524,288 sub-elements at n_split = 5, L = 3 -- 62 of the cycle's 74 sweeps). Workgroup w keeps the
@@ -260,6 +378,38 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
 // spin is bounded: a workgroup that waits > 2^22 polls sets *tmo and goes on (the host reports the
 // call as failed). Resident by construction: grid <= CUs, 1,024 threads, launched cooperatively.
 constexpr int kChainNT = 1024, kChainPer = 2;   // threads, sub-elements per thread (<= 2,048 per workgroup)
+constexpr int kChainHalo = 9216;                 // LDS image of the halo snapshot (doubles): 9 k m <= 9 * 1024
+
+// the next sweep's halo words of one sub-element (update_overlaps, :555) from its iterate t, written
+// through (st_coh): h = its positions along faces 1..3, 10 bits each; bc: also the boundary words
+// (constant within a call: the first publish writes them into the second snapshot buffer)
+__device__ __forceinline__ void chain_halo(const HaloArgs &H, int64_t u, int h, const double t[3], bool bc) {
+    const int pos[3] = {h & 1023, (h >> 10) & 1023, h >> 20};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        const int i = pos[f];
+        if (!i) continue;
+        const int4 r = H.hface[3 * u + f];
+        const int mode = r.x & 3;
+        if (mode == 0) {
+            if (!bc) continue;
+            const int a = (i - 1) * 3 + (f == 2 ? 1 : 0);
+            const int b = (i - 1) * 3 + (f == 1 ? 1 : 2);
+            const double2 v = H.bcv[r.z + i - 1];
+            st_coh(H.tov + r.y + a, v.x);
+            st_coh(H.tov + r.y + b, v.y);
+        } else if (mode == 1) {
+            const int k = (r.x >> 2) ? (H.m - i + 1) : i;
+            double *d = H.tov + r.y + (int64_t)(k - 1) * 3;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) st_coh(d + c, t[c]);
+        } else {
+            double *o = H.send + 6 * (int64_t)(r.z + i - 1);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) st_coh(o + c, t[c]);
+        }
+    }
+}
 
 template <bool UNI, bool RB>
 __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *TNN, const double *__restrict__ RHS,
@@ -269,12 +419,16 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                                                           const int *__restrict__ nb_off, const int *__restrict__ nb_list,
                                                           unsigned *tmo, int run, int total, int store, int E,
                                                           int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
-                                                          double rdt, double omega) {
+                                                          double rdt, double omega, long long *stamps) {
     constexpr int NT = kChainNT, PER = kChainPer;
     __shared__ double X[3][NT * PER];
+    __shared__ double HI[kChainHalo];   // this workgroup's un_eles' t_overlap(1 : 3m, 1 : 3) of the sweep
     const int t = threadIdx.x, w = blockIdx.x;
     const int64_t s0 = (int64_t)w * E;
     const int64_t nsm = (1ll << nsub_log2) - 1;
+    const int m = H.m, ke = E >> nsub_log2;   // positions along an un_ele face, un_eles of the workgroup
+    const int64_t u0 = s0 >> nsub_log2;
+    const int nhalo = ke * 9 * m;
     double b[PER][3];
     int4 nbr[PER];
 #pragma unroll
@@ -289,8 +443,16 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             X[c][j] = TNN[c * pitch + s];
         }
     }
+    // the halo positions of the thread's pair (2t, 2t + 1), packed 10 bits per face
+    int hp[2] = {0, 0};
+    if (2 * t < E && s0 + 2 * t < N)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int4 e = H.hsub[(s0 + 2 * t + q) & nsm];
+            hp[q] = e.x | (e.y << 10) | (e.z << 20);
+        }
     __syncthreads();
-    auto pass = [&](auto mc, const double *tin) {
+    auto pass = [&](auto mc) {
         constexpr int MODE = decltype(mc)::value;
         double r[PER][3];
         bool on[PER];
@@ -310,8 +472,10 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 #pragma unroll
             for (int c = 0; c < 3; ++c) x[c] = X[c][j];
             auto xin = [&](int c, int q) { return X[c][jb + q]; };
-            face_point<MODE, decltype(xin), true>(xin, x, b[k], nb, u, stc, fface, fsx, tin, slots, level1, rdt, omega,
-                                                  r[k]);
+            auto hv = [&](int64_t uu, int mf, int sp, int kk) {
+                return HI[(((int)(uu - u0) * 3 + mf - 1) * m + sp - 1) * 3 + kk];
+            };
+            face_point<MODE>(xin, x, b[k], nb, u, stc, fface, fsx, hv, level1, rdt, omega, r[k]);
             if (MODE != 2)
 #pragma unroll
                 for (int c = 0; c < 3; ++c) X[c][j] = r[k][c];
@@ -330,6 +494,12 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
         double *tout = sw + 1 < total ? (((total - 2 - sw) & 1) ? buf1 : buf0) : nullptr;
+        // diagnostics (PAMG_CHAIN_STAMPS): wall clock at the sweep's start, after the wait and the
+        // snapshot's load, after the passes, after the publish -- workgroup 0..7's thread 0
+        auto stamp = [&](int i) {
+            if (stamps && t == 0 && w < 8) stamps[((int64_t)w * run + sw) * 4 + i] = wall_clock64();
+        };
+        stamp(0);
         if (sw > 0 && t < 64) {   // wait for the neighbours' words of this sweep: one wave polls
             for (int base = 0; base < nn; base += 64) {
                 const int i = base + t;
@@ -348,6 +518,13 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             }
         }
         __syncthreads();
+        // the snapshot of this workgroup's un_eles into LDS (every load of the handed-over words: ld_coh)
+        for (int idx = t; idx < nhalo; idx += NT) {
+            const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
+            HI[idx] = ld_coh(tin + (u0 + uk) * slots * 3 + (int64_t)mf * slots + off);
+        }
+        __syncthreads();
+        stamp(1);
         if (store == 1 && sw + 1 == run)   // the call's last sweep: tnew := tnew_nonlin (:550)
 #pragma unroll
             for (int k = 0; k < PER; ++k) {
@@ -357,26 +534,30 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                     for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = X[c][j];
             }
         if constexpr (RB) {
-            pass(std::integral_constant<int, 0>{}, tin);
-            pass(std::integral_constant<int, 1>{}, tin);
+            pass(std::integral_constant<int, 0>{});
+            pass(std::integral_constant<int, 1>{});
         } else {
-            pass(std::integral_constant<int, 2>{}, tin);
+            pass(std::integral_constant<int, 2>{});
         }
+        stamp(2);
         if (tout) {   // the next sweep's halo words (:550, :555 of sweep sw + 1), written through
             HaloArgs Hn = H;
             Hn.tov = tout;
-            const int j = 2 * t;   // an adjacent pair per thread (PER = 2)
-            const int64_t s = s0 + j;
-            if (j < E && s < N) {
-                HaloPre hp;
-                halo_prefetch(Hn, s, s >> nsub_log2, nsub_log2, hp);
-                const double p0[3] = {X[0][j], X[1][j], X[2][j]}, p1[3] = {X[0][j + 1], X[1][j + 1], X[2][j + 1]};
-                halo_write<true>(Hn, hp, p0, p1);
+            const int j = 2 * t;
+            if ((hp[0] | hp[1]) != 0) {
+                int64_t u = (s0 + j) >> nsub_log2;
+                if (UNI) u = __builtin_amdgcn_readfirstlane((int)u);
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const double tv[3] = {X[0][j + q], X[1][j + q], X[2][j + q]};
+                    chain_halo(Hn, u, hp[q], tv, sw == 0);
+                }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
             __syncthreads();
             if (t == 0) __hip_atomic_store((g_u32 *)flags + w, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        stamp(3);
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew, the dead last sweep's :550)
@@ -444,8 +625,28 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
         if (rb) PAMG_FSW(4096, 1024, true, true);
         else PAMG_FSW(4096, 1024, true, false);
     } else if (L.nsub == 1024) {
-        if (rb) PAMG_FSW(1024, 512, true, true);
-        else PAMG_FSW(1024, 512, true, false);
+        // streamed (k_face_stream): a grid of two workgroups per CU (PAMG_FACE_STREAM=0: one per tile)
+        static const bool stream_env = !getenv("PAMG_FACE_STREAM") || atoi(getenv("PAMG_FACE_STREAM")) != 0;
+        static const int cus = [] {
+            int d = 0, n = 0;
+            if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+                n = 256;
+            return n;
+        }();
+        const int ntiles = (int)((L.N + 1023) / 1024);
+        if (stream_env) {
+            const unsigned g = (unsigned)std::min(ntiles, 2 * cus);
+#define PAMG_FST(R)                                                                                                    \
+    hipLaunchKernelGGL((k_face_stream<1024, 512, R>), dim3(g), dim3(512), 0, s, L.T, L.TNN, L.RHS, L.stc, L.fnb, L.fface, \
+                       L.fsx, tin, H, nh, st, L.pitch, L.N, lg, slots, l1, rdt, omega, ntiles)
+            if (rb) PAMG_FST(true);
+            else PAMG_FST(false);
+#undef PAMG_FST
+        } else if (rb) {
+            PAMG_FSW(1024, 512, true, true);
+        } else {
+            PAMG_FSW(1024, 512, true, false);
+        }
     } else if (uni) {
         if (rb) PAMG_FSW(256, 128, true, true);
         else PAMG_FSW(256, 128, true, false);
@@ -463,7 +664,12 @@ int face_chain_per_wg(int nsub, int U, int cus) {
     return (int)std::min<int64_t>((int64_t)k * nsub, 1 << 30);
 }
 
-bool face_chain_fits(int nsub, int U, int cus) { return U >= 1 && face_chain_per_wg(nsub, U, cus) <= kChainNT * kChainPer; }
+bool face_chain_fits(int nsub, int U, int cus) {
+    const int E = face_chain_per_wg(nsub, U, cus);
+    int m = 1;
+    while (m * m < nsub) m *= 2;
+    return U >= 1 && E <= kChainNT * kChainPer && 9 * (E / nsub) * m <= kChainHalo;
+}
 
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
@@ -482,12 +688,35 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     const int4 *fnb = L.fnb;
     const int *fsx = L.fsx;
     int64_t pitch = L.pitch, N = L.N;
+    // PAMG_CHAIN_STAMPS=<file>: append every launch's per-sweep phase stamps of workgroups 0..7
+    static const char *stamp_path = getenv("PAMG_CHAIN_STAMPS");
+    long long *stamps = nullptr;
+    const size_t nst = (size_t)8 * run * 4;
+    if (stamp_path) {
+        hipError_t e = hipMalloc(&stamps, nst * sizeof(long long));
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(stamps, 0, nst * sizeof(long long), s);
+        if (e != hipSuccess) return e;
+    }
     void *args[] = {&T, &TNN, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
-                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega};
+                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &stamps};
     const bool uni = L.nsub >= 64;
     const void *f = uni ? (rb ? (const void *)k_face_chain<true, true> : (const void *)k_face_chain<true, false>)
                         : (rb ? (const void *)k_face_chain<false, true> : (const void *)k_face_chain<false, false>);
-    return hipLaunchCooperativeKernel(f, dim3(grid), dim3(kChainNT), args, 0, s);
+    hipError_t e = hipLaunchCooperativeKernel(f, dim3(grid), dim3(kChainNT), args, 0, s);
+    if (stamp_path) {
+        std::vector<long long> h(nst);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpy(h.data(), stamps, nst * sizeof(long long), hipMemcpyDeviceToHost);
+        (void)hipFree(stamps);
+        if (FILE *fp = fopen(stamp_path, "ab")) {
+            const long long hdr[4] = {run, grid, E, L.nsub};
+            fwrite(hdr, sizeof hdr, 1, fp);
+            fwrite(h.data(), sizeof(long long), nst, fp);
+            fclose(fp);
+        }
+    }
+    return e;
 }
 
 hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov, bool neg, bool level1, double rdt,

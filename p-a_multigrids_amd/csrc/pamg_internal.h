@@ -206,7 +206,10 @@ void level_stencil(const double *X, int i_split, double k, double dt, double ome
 bool mass_is_p1_midpoint(const double *rec);
 int build_halo(pamg_handle *h, int l, const double *Xg, const int *neig, const int *fneig, const int *dir);
 // face-coupled operator tables of level l (Level::fnb / fface / fsx, host copies returned)
-constexpr int kFaceStride = 12;
+// fface record per (un_ele, level): w_in[3] | w_b[3] | D0[3] | pad[3] | omega / D[8][3] -- D of a
+// sub-element whose faces are inner (bit fi of the pattern) or across an un_ele face, accumulated in
+// the oracle's face order (face_terms), divided on the host (IEEE: bitwise the device's division)
+constexpr int kFaceStride = 36, kFaceWD = 12;
 int build_face(pamg_handle *h, int l, const double *Xg, const int *neig, const int *fneig, const int *dir,
                std::vector<int4> &fnb, std::vector<double> &fface, std::vector<int> &fsx);
 }  // namespace pamg

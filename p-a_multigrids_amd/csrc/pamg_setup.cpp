@@ -477,6 +477,18 @@ int build_face(pamg_handle *h, int l, const double *Xg, const int *neig, const i
         }
         double rec[kStcStride];
         level_stencil(X, is, h->p.k, h->p.dt, h->p.omega, rec, w + 6);   // D0 = rdt ml + Kd_ii + 0.0
+        // omega / D for each pattern of inner faces (get_diagonal's surface term, :481-486): D_i =
+        // D0_i + 2 w_f over the faces containing node i, in face order, as the oracle's face_terms
+        for (int pt = 0; pt < 8; ++pt) {
+            double D[3] = {w[6], w[7], w[8]};
+            for (int fi = 0; fi < 3; ++fi) {
+                const int a = kFNode[fi][0] - 1, b = kFNode[fi][1] - 1;
+                const double wf = ((pt >> fi) & 1) ? w[fi] : w[3 + kFMface[fi] - 1];
+                D[a] = D[a] + 2.0 * wf;
+                D[b] = D[b] + 2.0 * wf;
+            }
+            for (int i = 0; i < 3; ++i) w[kFaceWD + 3 * pt + i] = h->p.omega / D[i];
+        }
     }
     return PAMG_OK;
 }

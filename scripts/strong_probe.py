@@ -11,9 +11,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import pamg  # noqa: E402
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-mesh = pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "untitled8192.msh"))
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 FUSED = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+MESH = sys.argv[3] if len(sys.argv) > 3 else "untitled8192.msh"
+mesh = pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", MESH))
 base = None
 for n in (1, 2, 4, 8):
     comm = None if n == 1 else (n, 0, None, mesh.x_strip_owner(n))
@@ -38,6 +39,7 @@ for n in (1, 2, 4, 8):
     d20 = (time.perf_counter() - t0) / 20 * 1e3
     if base is None:
         base = res[0][0]
-    print(f"fused={FUSED} N={n}: {res[0][0]:.4f} ms/cycle (ideal {base / n:.4f}, eff {base / n / res[0][0]:.2f}); "
-          f"20-cycle call {d20:.4f} ms/cycle; timed {res[1][0]:.4f} {res[1][1]}", flush=True)
+    print(f"{MESH} S={S} fused={FUSED} N={n} (rank 0: {s.U} un_eles): {res[0][0]:.4f} ms/cycle (ideal {base / n:.4f}, eff {base / n / res[0][0]:.2f}); "
+          f"20-cycle call {d20:.4f} ms/cycle; timed {res[1][0]:.4f} {res[1][1]}; rank fp64 "
+          f"{s.vcycle_flops() / (res[0][0] * 1e-3) / 1e12 / 78.6:.3f} of peak", flush=True)
     s.close()
