@@ -11,8 +11,12 @@
 // -- with several ranks, after the exchange: the first consumer of the halo. A sweep is
 // red-black Gauss-Seidel on the up / down sub-elements (solver 3: every inner neighbour of an up
 // sub-element is a down one) or Jacobi (solver 1). The operation order is the oracle's
-// (oracle/pamg_oracle.c face_terms / face_sweep), so the results are bitwise its own; these
-// kernels gather neighbours and stay off the fused V-cycle (per-step kernels only).
+// (oracle/pamg_oracle.c face_terms / face_sweep), so the results are bitwise its own. The forms:
+// per-colour kernels (k_face), one launch per sweep on LDS tiles (k_face_sweep), and a whole
+// smoother call in one cooperative launch for a level that fits on-chip (k_face_chain); the face
+// V-cycle (pamg_api.cpp vcycle_face_fused) strings them together. A grid-stride form that kept the
+// next tile in flight (two workgroups per CU) measured 5 % slower than one launch per tile and was
+// dropped (profiles/r03_c_face_ab.txt).
 #include <hip/hip_runtime.h>
 
 #include "pamg_device.h"
@@ -246,121 +250,6 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
     }
 }
 
-// ---- the streamed sweep: k_face_sweep's work on whole-un_ele tiles (TS a multiple of nsub, so every
-// tile has the same neighbour records), by a grid of two workgroups per CU that loop over the tiles
-// with the next tile's tnew_nonlin and RHS in flight while the current one is smoothed: the one-
-// launch-per-tile form serialises each workgroup's load, passes and stores (SQ: 79 % of the waves'
-// cycles waiting, r03_b_face_sq.txt). Same operations per sub-element (face_point), same stores.
-template <int TS, int NT, bool RB>
-__global__ __launch_bounds__(NT, 2 * NT / 256) void k_face_stream(double *T, double *TNN, const double *__restrict__ RHS,
-                                                                const double *__restrict__ stc,
-                                                                const int4 *__restrict__ fnb,
-                                                                const double *__restrict__ fface,
-                                                                const int *__restrict__ fsx, const double *__restrict__ tin,
-                                                                HaloArgs Hn, int next_halo, int store, int64_t pitch,
-                                                                int64_t N, int nsub_log2, int slots, int level1, double rdt,
-                                                                double omega, int ntiles) {
-    constexpr int PER = TS / NT;
-    static_assert(PER == 2, "an adjacent pair of sub-elements per thread");
-    __shared__ double X[3][TS];
-    const int t = threadIdx.x;
-    const int64_t nsm = (1ll << nsub_log2) - 1;
-    int4 nbr[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) nbr[k] = fnb[(t + NT * k) & nsm];
-    double b[PER][3], pn[PER][3], pb[PER][3];
-    auto fetch = [&](int tl) {
-        const int64_t s0 = (int64_t)tl * TS;
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int64_t s = s0 + t + NT * k < N ? s0 + t + NT * k : s0;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                pn[k][c] = TNN[c * pitch + s];
-                pb[k][c] = RHS[c * pitch + s];
-            }
-        }
-    };
-    int tile = blockIdx.x;
-    if (tile < ntiles) fetch(tile);
-    for (; tile < ntiles; tile += gridDim.x) {
-        const int64_t s0 = (int64_t)tile * TS;
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {   // tnew := tnew_nonlin (:550); the iterate into LDS
-            const int j = t + NT * k;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                X[c][j] = pn[k][c];
-                b[k][c] = pb[k][c];
-                if (store == 1 && s0 + j < N) T[c * pitch + s0 + j] = pn[k][c];
-            }
-        }
-        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight during the passes
-        __syncthreads();
-        auto pass = [&](auto mc) {
-            constexpr int MODE = decltype(mc)::value;
-            double r[PER][3];
-            bool on[PER];
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const int j = t + NT * k;
-                const int64_t s = s0 + j;
-                on[k] = false;
-                if (s >= N) continue;
-                const int64_t u = __builtin_amdgcn_readfirstlane((int)(s >> nsub_log2));
-                const int4 nb = nbr[k];
-                if ((MODE == 0 && !nb.w) || (MODE == 1 && nb.w)) continue;
-                on[k] = true;
-                const int jb = (int)((u << nsub_log2) - s0);
-                double x[3];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) x[c] = X[c][j];
-                auto xin = [&](int c, int q) { return X[c][jb + q]; };
-                auto hv = [&](int64_t uu, int mf, int sp, int kk) {
-                    return tin[uu * slots * 3 + (int64_t)(mf - 1) * slots + (sp - 1) * 3 + kk];
-                };
-                face_point<MODE>(xin, x, b[k], nb, u, stc, fface, fsx, hv, level1, rdt, omega, r[k]);
-                if (MODE != 2)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) X[c][j] = r[k][c];
-            }
-            if (MODE == 2) {
-                __syncthreads();
-#pragma unroll
-                for (int k = 0; k < PER; ++k)
-                    if (on[k])
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) X[c][t + NT * k] = r[k][c];
-            }
-            __syncthreads();
-        };
-        if constexpr (RB) {
-            pass(std::integral_constant<int, 0>{});
-            pass(std::integral_constant<int, 1>{});
-        } else {
-            pass(std::integral_constant<int, 2>{});
-        }
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew)
-            const int j = t + NT * k;
-            if (s0 + j < N)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
-        }
-        if (next_halo) {   // the next sweep's halo words, an adjacent pair per thread
-            const int j = 2 * t;
-            const int64_t s = s0 + j;
-            if (s < N) {
-                HaloPre hp;
-                halo_prefetch(Hn, s, s >> nsub_log2, nsub_log2, hp);
-                const double p0[3] = {X[0][j], X[1][j], X[2][j]}, p1[3] = {X[0][j + 1], X[1][j + 1], X[2][j + 1]};
-                halo_write(Hn, hp, p0, p1);
-            }
-        }
-        __syncthreads();   // X is rewritten by the next tile
-    }
-}
-
 // ---- the persistent chain: every sweep of one smoother call in ONE launch, for a level whose
 // iterate fits in the LDS of one workgroup per CU (the coarsest level of the face-coupled V-cycle:
 // 524,288 sub-elements at n_split = 5, L = 3 -- 62 of the cycle's 74 sweeps). Workgroup w keeps the
@@ -545,8 +434,8 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             Hn.tov = tout;
             const int j = 2 * t;
             if ((hp[0] | hp[1]) != 0) {
-                int64_t u = (s0 + j) >> nsub_log2;
-                if (UNI) u = __builtin_amdgcn_readfirstlane((int)u);
+                // per lane: a wave's pairs span 128 sub-elements, two un_eles when nsub = 64
+                const int64_t u = (s0 + j) >> nsub_log2;
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const double tv[3] = {X[0][j + q], X[1][j + q], X[2][j + q]};
@@ -625,28 +514,8 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
         if (rb) PAMG_FSW(4096, 1024, true, true);
         else PAMG_FSW(4096, 1024, true, false);
     } else if (L.nsub == 1024) {
-        // streamed (k_face_stream): a grid of two workgroups per CU (PAMG_FACE_STREAM=0: one per tile)
-        static const bool stream_env = !getenv("PAMG_FACE_STREAM") || atoi(getenv("PAMG_FACE_STREAM")) != 0;
-        static const int cus = [] {
-            int d = 0, n = 0;
-            if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-                n = 256;
-            return n;
-        }();
-        const int ntiles = (int)((L.N + 1023) / 1024);
-        if (stream_env) {
-            const unsigned g = (unsigned)std::min(ntiles, 2 * cus);
-#define PAMG_FST(R)                                                                                                    \
-    hipLaunchKernelGGL((k_face_stream<1024, 512, R>), dim3(g), dim3(512), 0, s, L.T, L.TNN, L.RHS, L.stc, L.fnb, L.fface, \
-                       L.fsx, tin, H, nh, st, L.pitch, L.N, lg, slots, l1, rdt, omega, ntiles)
-            if (rb) PAMG_FST(true);
-            else PAMG_FST(false);
-#undef PAMG_FST
-        } else if (rb) {
-            PAMG_FSW(1024, 512, true, true);
-        } else {
-            PAMG_FSW(1024, 512, true, false);
-        }
+        if (rb) PAMG_FSW(1024, 512, true, true);
+        else PAMG_FSW(1024, 512, true, false);
     } else if (uni) {
         if (rb) PAMG_FSW(256, 128, true, true);
         else PAMG_FSW(256, 128, true, false);
