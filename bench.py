@@ -255,6 +255,38 @@ def measure_workload(pamg, m, S, L, ns, arith, device, cycles=100):
     return out
 
 
+def measure_face(pamg, m, S, L, device, cycles=20):
+    """the face-coupled operator (op = 1) on mesh m: V-cycles/s of the reference's
+    cycle (n_smooth 4, red-black GS) and, from an evented pass, each kernel class's time and
+    algorithmic bytes per cycle; the level-1 sweeps (HBM-bound) against the HBM roofline"""
+    s = pamg.SemiImplicitIterative(m, S, L, n_smooth=4, solver=3, device=device, op=1, cycle=0)
+    s.begin_timestep()
+    s.vcycle(3)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.vcycle(cycles)
+    s.synchronize()
+    dt = (time.perf_counter() - t0) / cycles
+    s.timing_enable(ALL_CLASSES)
+    s.timing_stride(1)
+    s.timing_reset()
+    s.vcycle(cycles)
+    s.synchronize()
+    tm = s.timing()
+    out = dict(n_split=S, levels=L, n_smooth=4, vcycles_per_s=round(1 / dt, 1), ms_per_cycle=round(dt * 1e3, 4),
+               kernels={k: dict(launches_per_cycle=v["launches"] // cycles, ms_per_cycle=round(v["ms"] / cycles, 4),
+                                gbs=round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None)
+                        for k, v in tm.items() if v["launches"]})
+    k1 = tm["smooth_L1"]
+    if k1["launches"] and k1["ms"] > 0:
+        gbs = k1["bytes"] / (k1["ms"] * 1e-3) / 1e9
+        out["roofline_level1_sweep"] = dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                                            frac=round(gbs / HBM_PEAK_GBS, 4),
+                                            ms_per_sweep=round(k1["ms"] / k1["launches"], 4))
+    s.close()
+    return out
+
+
 def comm_report(s, world, dist):
     kind, ver, path = s.comm_info()
     mine = {"transport": kind, "rccl_version": ver, "librccl": path}
@@ -495,6 +527,8 @@ def main():
                             ("untitled8192_nsplit6", mesh, 6),
                             ("strip256x64_nsplit5", pamg.Mesh.strip(256, 64), 5)):
             extra[tag] = measure_workload(pamg, m_, S_, a.levels, a.nsmooth, a.arith, device)
+        # the face-coupled operator on the benchmarked mesh, n_split 5, 3 levels
+        extra["op1"] = measure_face(pamg, mesh, a.nsplit, 3, device)
     if world > 1 and not a.no_extra:
         # the other exchange mode on the same partition (timed region the same shape): halo words
         # exchanged after every cycle, overlapped with the next one

@@ -183,7 +183,8 @@ int local_timeout_s() {
     return t > 0 ? t : 120;
 }
 
-int exchange_local(pamg_handle *h, int l, const double *send, hipStream_t st) {
+// w words per entry (6: tnew and told; 3: the tnew words of the resident call's ring), into recv
+int exchange_local(pamg_handle *h, int l, const double *send, hipStream_t st, int w, double *recv) {
     Comm &C = *h->comm;
     LocalGroup &G = *C.local;
     const HaloPlan &P = h->lv[l].halo;
@@ -211,7 +212,7 @@ int exchange_local(pamg_handle *h, int l, const double *send, hipStream_t st) {
         std::lock_guard<std::mutex> lk(G.mu);
         for (int q = 0; q < np; ++q) {
             const int peer = P.peers[q];
-            G.ready[(size_t)me * G.n + peer] = {C.seq[peer] + 1, send + 6 * (size_t)P.send_peer_off[q], C.ev_ready};
+            G.ready[(size_t)me * G.n + peer] = {C.seq[peer] + 1, send + w * (size_t)P.send_peer_off[q], C.ev_ready};
         }
     }
     G.cv.notify_all();
@@ -220,7 +221,7 @@ int exchange_local(pamg_handle *h, int l, const double *send, hipStream_t st) {
         const size_t nr = (size_t)(P.recv_peer_off[q + 1] - P.recv_peer_off[q]);
         HIPCHK(h, hipStreamWaitEvent(st, got[q].ev, 0));
         if (nr)
-            HIPCHK(h, hipMemcpyAsync(P.d_recv + 6 * (size_t)P.recv_peer_off[q], got[q].ptr, 6 * nr * sizeof(double),
+            HIPCHK(h, hipMemcpyAsync(recv + w * (size_t)P.recv_peer_off[q], got[q].ptr, w * nr * sizeof(double),
                                      hipMemcpyDeviceToDevice, st));
     }
     // 2. this rank's reads are issued; its send words may be repacked once every peer's are
@@ -247,7 +248,7 @@ int exchange(pamg_handle *h, int l, int buf, hipStream_t st) {
     const double *send = P.send_buf(buf);
     Span sp(h, PAMG_K_HALO, 2.0 * 48.0 * (double)(P.remote.size() + P.recv_dst.size()), st);
     if (h->comm->local) {
-        CHK(exchange_local(h, l, send, st));
+        CHK(exchange_local(h, l, send, st, 6, P.d_recv));
         HIPCHK(h, launch_halo_unpack(st, L, h->tov, h->tovo));
         return PAMG_OK;
     }
@@ -262,6 +263,66 @@ int exchange(pamg_handle *h, int l, int buf, hipStream_t st) {
     }
     NCCLCHK(h, ncclGroupEnd());
     HIPCHK(h, launch_halo_unpack(st, L, h->tov, h->tovo));
+    return PAMG_OK;
+}
+
+// the tnew words of cycle c of a resident call with halo_exchange = 1 (level 1's ring, 3 words per
+// entry; the told words do not change within a time step and travel with the last cycle's exchange)
+int exchange_ring(pamg_handle *h, int c, hipStream_t st) {
+    Level &L = h->lv[1];
+    const HaloPlan &P = L.halo;
+    const double *send = P.d_ring + (size_t)c * 3 * P.remote.size();
+    Span sp(h, PAMG_K_HALO, 2.0 * 24.0 * (double)(P.remote.size() + P.recv_dst.size()), st);
+    if (h->comm->local) {
+        CHK(exchange_local(h, 1, send, st, 3, P.d_recv3));
+        HIPCHK(h, launch_halo_unpack3(st, L, h->tov));
+        return PAMG_OK;
+    }
+    NCCLCHK(h, ncclGroupStart());
+    for (size_t q = 0; q < P.peers.size(); ++q) {
+        const int peer = P.peers[q];
+        const size_t ns = (size_t)(P.send_peer_off[q + 1] - P.send_peer_off[q]);
+        const size_t nr = (size_t)(P.recv_peer_off[q + 1] - P.recv_peer_off[q]);
+        if (ns) NCCLCHK(h, ncclSend(send + 3 * (size_t)P.send_peer_off[q], 3 * ns, ncclDouble, peer, h->comm->nccl, st));
+        if (nr) NCCLCHK(h, ncclRecv(P.d_recv3 + 3 * (size_t)P.recv_peer_off[q], 3 * nr, ncclDouble, peer,
+                                    h->comm->nccl, st));
+    }
+    NCCLCHK(h, ncclGroupEnd());
+    HIPCHK(h, launch_halo_unpack3(st, L, h->tov));
+    return PAMG_OK;
+}
+
+int sync_stream(pamg_handle *h, hipStream_t s);
+
+// the ring, counters and signal of a resident call of `cycles` cycles with halo_exchange = 1
+int xc_setup(pamg_handle *h, int cycles) {
+    HaloPlan &P = h->lv[1].halo;
+    const int need = cycles - 1;
+    if (P.ring_cap < need) {
+        CHK(sync_stream(h, h->stream));
+        CHK(sync_stream(h, h->stream_comm));
+        dev_free(P.d_ring);
+        P.d_ring = nullptr;
+        P.ring_cap = 0;
+        CHK(dev_alloc(h, &P.d_ring, (size_t)need * 3 * P.remote.size()));
+        P.ring_cap = need;
+    }
+    if (!P.d_recv3 && !P.recv_dst.empty()) CHK(dev_alloc(h, &P.d_recv3, 3 * P.recv_dst.size()));
+    if (h->xc_cap < need) {
+        CHK(sync_stream(h, h->stream));
+        dev_free(h->xc_done);
+        h->xc_done = nullptr;
+        h->xc_cap = 0;
+        CHK(dev_alloc(h, &h->xc_done, (size_t)need));
+        h->xc_cap = need;
+    }
+    if (!h->xc_sig) {
+        // the comm stream waits on it (hipStreamWaitValue64): HIP's signal memory
+        HIPCHK(h, hipExtMallocWithFlags((void **)&h->xc_sig, sizeof(unsigned long long), hipMallocSignalMemory));
+        unsigned long long v = 0;
+        HIPCHK(h, hipMemcpy(&v, h->xc_sig, sizeof v, hipMemcpyDeviceToHost));
+        h->xc_sig_base = v;
+    }
     return PAMG_OK;
 }
 
@@ -443,7 +504,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         Span sp(h, kid, (store == 1 ? 96.0 : 72.0) * (double)L.N + 168.0 * h->U);
         HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
                                           s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
-                                          h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store));
+                                          h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store, s == 0));
     }
     return PAMG_OK;
 }
@@ -786,7 +847,7 @@ int call_schedule(pamg_handle *h) {
     static const int cs_env = getenv("PAMG_CALL_SCHEDULE") ? atoi(getenv("PAMG_CALL_SCHEDULE")) : -1;
     const int s = cs_env >= 0 ? cs_env : h->call_schedule;
     if (s) return s;
-    if (vcycle_resident_supported(h->p.n_split, h->p.multi_levels) && h->p.halo_exchange == 0) return 3;
+    if (vcycle_resident_supported(h->p.n_split, h->p.multi_levels)) return 3;
     return h->nranks > 1 ? 2 : 1;
 }
 
@@ -798,8 +859,7 @@ bool fused_ok(pamg_handle *h) {
           vcycle_fusable(h->lv, L, h->p.n_split, h->p.solver, h->p.halo_mode, h->p.n_smooth)))
         return false;
     if (h->p.solver != 2) return true;
-    return h->p.fused == 3 && h->p.halo_exchange == 0 && call_schedule(h) == 3 && !h->coarse_ahead &&
-           vcycle_resident_supported(h->p.n_split, L);
+    return h->p.fused == 3 && call_schedule(h) == 3 && !h->coarse_ahead && vcycle_resident_supported(h->p.n_split, L);
 }
 
 
@@ -874,12 +934,11 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
         return PAMG_ERR_STATE;
     }
     if (h->p.solver == 2 && n >= 1 &&
-        !(pipe && sched == 3 && h->p.halo_exchange == 0 && !h->coarse_ahead && vcycle_resident_supported(h->p.n_split, L))) {
+        !(pipe && sched == 3 && !h->coarse_ahead && vcycle_resident_supported(h->p.n_split, L))) {
         h->err = "internal: Richardson outside the resident call";
         return PAMG_ERR_STATE;
     }
-    if (pipe && n >= 1 && sched == 3 && h->p.halo_exchange == 0 && !h->coarse_ahead &&
-        vcycle_resident_supported(h->p.n_split, L)) {
+    if (pipe && n >= 1 && sched == 3 && !h->coarse_ahead && vcycle_resident_supported(h->p.n_split, L)) {
         const int buf = two ? 1 - P1.send_cur : 0;
         if (h->sent_pending[buf]) {
             HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[buf], 0));
@@ -887,9 +946,37 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
         }
         const bool rhsf = rhs_first;
         const int kt = rhsf && !dead_after ? PAMG_KEEP_TOLD : 0;
-        const int keep = (dead_after ? pipe_keep_env() : PAMG_KEEP_ALL) | kt;
+        // inside pamg_run (dead_after) the halo words die unread too -- unless every cycle's are exchanged
+        const bool hx = h->p.halo_exchange == 1;
+        const int keep = (dead_after ? pipe_keep_env() | (hx ? PAMG_KEEP_HALO : 0) : PAMG_KEEP_ALL) | kt;
         if (kt) CHK(join_comm(h));   // the send buffers' told halves are rewritten
-        {
+        // halo_exchange = 1: every cycle's words are exchanged. Cycles 0 .. n-2 pack the tnew words
+        // of their remote entries into level 1's ring (k_vc_res / k_vc_resb with XC) and publish
+        // each completed cycle on xc_sig; the comm stream waits for cycle c's count
+        // (hipStreamWaitValue64) and exchanges it (exchange_ring) while the launch runs on; the last
+        // cycle's words (6 per entry, with told) go as in the plain call, after the launch
+        const bool xc = hx && n >= 2 && !P1.remote.empty();
+        if (xc && (rhsf || steps != 1)) {
+            h->err = "internal: a per-cycle exchange inside a resident time step";
+            return PAMG_ERR_STATE;
+        }
+        if (xc) {
+            CHK(xc_setup(h, n));
+            HIPCHK(h, hipMemsetAsync(h->xc_done, 0, (size_t)(n - 1) * sizeof(unsigned), h->stream));
+            {
+                Span sp(h, PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, false) + 24.0 * (n - 1) * P1.remote.size());
+                HIPCHK(h, launch_vcycle_resident_xc(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt,
+                                                    h->tov, h->tovo, P1.send_buf(buf), L2.RHSN, keep, n, P1.d_ring,
+                                                    3 * (int64_t)P1.remote.size(), h->xc_done, h->xc_sig));
+            }
+            if (h->comm && !P1.peers.empty())
+                for (int c = 0; c + 1 < n; ++c) {
+                    HIPCHK(h, hipStreamWaitValue64(h->stream_comm, h->xc_sig, h->xc_sig_base + c + 1,
+                                                   hipStreamWaitValueGte));
+                    CHK(exchange_ring(h, c, h->stream_comm));
+                }
+            h->xc_sig_base += (unsigned long long)(n - 1);
+        } else {
             Span sp(h, rhsf ? PAMG_K_VCYCLE_RES_RHSF : PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, rhsf));
             HIPCHK(h, launch_vcycle_resident(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
                                              h->tovo, P1.send_buf(buf), L2.RHSN, keep, rhsf,
@@ -900,7 +987,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
             h->told_halo_stale_l1 = kt == 0;
         }
         h->tnn_level = 1;
-        if (dead_after) {
+        if (dead_after && !hx) {
             P1.send_cur = buf;
             return join_comm(h);
         }
@@ -1040,6 +1127,7 @@ void free_levels(pamg_handle *h) {
         dev_free(L.chain_nb_off); dev_free(L.chain_nb_list); dev_free(L.chain_flags);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
+        dev_free(L.halo.d_ring); dev_free(L.halo.d_recv3);
         dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
         dev_free(L.halo.d_surf); dev_free(L.halo.d_told_halo);
         L = Level();
@@ -1701,6 +1789,8 @@ int pamg_destroy(pamg_handle *h) {
     free_levels(h);
     dev_free(h->scratch);
     dev_free(h->chain_tmo);
+    dev_free(h->xc_done);
+    if (h->xc_sig) (void)hipFree(h->xc_sig);
     for (auto e : h->timing.pool) (void)hipEventDestroy(e);
     for (auto &r : h->timing.pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     if (h->comm) {

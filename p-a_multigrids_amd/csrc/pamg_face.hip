@@ -53,6 +53,69 @@ __global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *_
     halo_write(H, hp, p0, p1);
 }
 
+// The operator record of one un_ele as face_apply reads it: the element stencil, the face weights
+// w_f (inner faces 0..2 by sub-element face, then the un_ele faces 1..3) and the un_ele faces' node
+// selectors (fsx) under sub-element faces 0..2
+struct FaceRec {
+    Stc S;
+    double w[6];
+    int sx[3];
+};
+
+__device__ __forceinline__ void load_face_rec(const double *__restrict__ stc, const double *__restrict__ fface,
+                                              const int *__restrict__ fsx, int64_t u, FaceRec &R) {
+    load_stc(stc + u * kStcStride, R.S);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) R.w[q] = fface[u * kFaceStride + q];
+#pragma unroll
+    for (int fi = 0; fi < 3; ++fi) R.sx[fi] = fsx[4 * u + cFMface[fi] - 1];
+}
+
+// the sub-element's pattern of inner faces (selects omega / D_i, kFaceWD)
+__device__ __forceinline__ int face_pattern(int4 nb) { return (nb.x >= 0) | ((nb.y >= 0) << 1) | ((nb.z >= 0) << 2); }
+
+// face_point's arithmetic from a loaded record; wd(i): omega / D_i of the sub-element's pattern
+template <int MODE, class XIN, class HV, class WD>
+__device__ __forceinline__ void face_apply(const FaceRec &R, const XIN &xin, const double x[3], const double b[3],
+                                           int4 nb, int64_t u, const HV &hv, const WD &wd, int level1, double rdt,
+                                           double out[3]) {
+    double A[3];
+    apply_A(R.S, rdt, x, A);
+    double ds[3] = {0.0, 0.0, 0.0};
+    const int nbf[3] = {nb.x, nb.y, nb.z};
+#pragma unroll
+    for (int fi = 0; fi < 3; ++fi) {
+        const int a = cFNode[fi][0], bb = cFNode[fi][1];
+        double ya, yb, wf;
+        if (nbf[fi] >= 0) {   // inner neighbour: its nodes at my face nodes a, b are its b, a
+            ya = xin(bb, nbf[fi]);
+            yb = xin(a, nbf[fi]);
+            wf = R.w[fi];
+        } else {              // across the un_ele face: the halo (t_overlap slot sp)
+            const int mface = cFMface[fi], sx = R.sx[fi];
+            if (!level1 && (sx & 16)) {
+                ya = 0.0;     // coarse levels carry the error equation: homogeneous boundary data
+                yb = 0.0;
+            } else {
+                ya = hv(u, mface, -nbf[fi], (sx & 3) - 1);
+                yb = hv(u, mface, -nbf[fi], ((sx >> 2) & 3) - 1);
+            }
+            wf = R.w[3 + mface - 1];
+        }
+        ds[a] = ds[a] + wf * (((2.0 * x[a] + x[bb]) - 2.0 * ya) - yb);
+        ds[bb] = ds[bb] + wf * (((x[a] + 2.0 * x[bb]) - ya) - 2.0 * yb);
+    }
+    // omega / D_i of the sub-element's pattern of inner faces (kFaceWD: D accumulated and divided on
+    // the host in the oracle's order -- no division here)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double ai = A[i] + ds[i];
+        if (MODE <= 2) out[i] = x[i] + wd(i) * (b[i] - ai);
+        else if (MODE == 3) out[i] = ai - b[i];
+        else out[i] = b[i] - ai;
+    }
+}
+
 // One sub-element of the face-coupled operator (the oracle's face_terms / face_sweep order):
 // MODE <= 2 the smoother update x_i + omega / D_i (b_i - (A x)_i), MODE 3 / 4 the residual
 // A x - b / b - A x. x: the sub-element's values; xin(c, q): component c of the inner neighbour
@@ -64,46 +127,11 @@ __device__ __forceinline__ void face_point(const XIN &xin, const double x[3], co
                                            const double *__restrict__ stc, const double *__restrict__ fface,
                                            const int *__restrict__ fsx, const HV &hv, int level1, double rdt,
                                            double omega, double out[3]) {
-    Stc S;
-    load_stc(stc + u * kStcStride, S);
-    double A[3];
-    apply_A(S, rdt, x, A);
-    const double *w = fface + u * kFaceStride;
-    double ds[3] = {0.0, 0.0, 0.0};
-    const int nbf[3] = {nb.x, nb.y, nb.z};
-#pragma unroll
-    for (int fi = 0; fi < 3; ++fi) {
-        const int a = cFNode[fi][0], bb = cFNode[fi][1];
-        double ya, yb, wf;
-        if (nbf[fi] >= 0) {   // inner neighbour: its nodes at my face nodes a, b are its b, a
-            ya = xin(bb, nbf[fi]);
-            yb = xin(a, nbf[fi]);
-            wf = w[fi];
-        } else {              // across the un_ele face: the halo (t_overlap slot sp)
-            const int mface = cFMface[fi], sx = fsx[4 * u + mface - 1];
-            if (!level1 && (sx & 16)) {
-                ya = 0.0;     // coarse levels carry the error equation: homogeneous boundary data
-                yb = 0.0;
-            } else {
-                ya = hv(u, mface, -nbf[fi], (sx & 3) - 1);
-                yb = hv(u, mface, -nbf[fi], ((sx >> 2) & 3) - 1);
-            }
-            wf = w[3 + mface - 1];
-        }
-        ds[a] = ds[a] + wf * (((2.0 * x[a] + x[bb]) - 2.0 * ya) - yb);
-        ds[bb] = ds[bb] + wf * (((x[a] + 2.0 * x[bb]) - ya) - 2.0 * yb);
-    }
-    // omega / D_i of the sub-element's pattern of inner faces (kFaceWD: D accumulated and divided on
-    // the host in the oracle's order -- no division here)
-    const double *wd = w + kFaceWD + 3 * ((nbf[0] >= 0) | ((nbf[1] >= 0) << 1) | ((nbf[2] >= 0) << 2));
     (void)omega;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const double ai = A[i] + ds[i];
-        if (MODE <= 2) out[i] = x[i] + wd[i] * (b[i] - ai);
-        else if (MODE == 3) out[i] = ai - b[i];
-        else out[i] = b[i] - ai;
-    }
+    FaceRec R;
+    load_face_rec(stc, fface, fsx, u, R);
+    const double *wd = fface + u * kFaceStride + kFaceWD + 3 * face_pattern(nb);
+    face_apply<MODE>(R, xin, x, b, nb, u, hv, [&](int i) { return wd[i]; }, level1, rdt, out);
 }
 
 // MODE 0 / 1: one colour of a red-black sweep (up / down sub-elements), X = OUT = tnew_nonlin;
@@ -269,34 +297,147 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
 constexpr int kChainNT = 1024, kChainPer = 2;   // threads, sub-elements per thread (<= 2,048 per workgroup)
 constexpr int kChainHalo = 9216;                 // LDS image of the halo snapshot (doubles): 9 k m <= 9 * 1024
 
-// the next sweep's halo words of one sub-element (update_overlaps, :555) from its iterate t, written
-// through (st_coh): h = its positions along faces 1..3, 10 bits each; bc: also the boundary words
-// (constant within a call: the first publish writes them into the second snapshot buffer)
-__device__ __forceinline__ void chain_halo(const HaloArgs &H, int64_t u, int h, const double t[3], bool bc) {
+// the next sweep's halo words of one sub-element (update_overlaps, :555) from its iterate t: h = its
+// positions along faces 1..3, 10 bits each, rec the un_ele's face records; bc: also the boundary
+// words (constant within a time step: the call's halo refresh writes them into one snapshot buffer,
+// the call's first sweep into the other). COH: written through (st_coh) for readers in other
+// workgroups of the same launch. The t_overlap_old words (told, constant within a time step) are the
+// call's halo refresh's (launch_face_halo), so the sweeps leave them alone.
+template <bool COH>
+__device__ __forceinline__ void halo_words(const HaloArgs &H, const int4 rec[3], int h, const double t[3], bool bc) {
     const int pos[3] = {h & 1023, (h >> 10) & 1023, h >> 20};
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
         const int i = pos[f];
         if (!i) continue;
-        const int4 r = H.hface[3 * u + f];
+        const int4 r = rec[f];
         const int mode = r.x & 3;
         if (mode == 0) {
             if (!bc) continue;
             const int a = (i - 1) * 3 + (f == 2 ? 1 : 0);
             const int b = (i - 1) * 3 + (f == 1 ? 1 : 2);
             const double2 v = H.bcv[r.z + i - 1];
-            st_coh(H.tov + r.y + a, v.x);
-            st_coh(H.tov + r.y + b, v.y);
+            st_halo<COH>(H.tov + r.y + a, v.x);
+            st_halo<COH>(H.tov + r.y + b, v.y);
         } else if (mode == 1) {
             const int k = (r.x >> 2) ? (H.m - i + 1) : i;
             double *d = H.tov + r.y + (int64_t)(k - 1) * 3;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) st_coh(d + c, t[c]);
+            for (int c = 0; c < 3; ++c) st_halo<COH>(d + c, t[c]);
         } else {
             double *o = H.send + 6 * (int64_t)(r.z + i - 1);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) st_coh(o + c, t[c]);
+            for (int c = 0; c < 3; ++c) st_halo<COH>(o + c, t[c]);
         }
+    }
+}
+
+__device__ __forceinline__ void chain_halo(const HaloArgs &H, int64_t u, int h, const double t[3], bool bc) {
+    const int4 rec[3] = {H.hface[3 * u], H.hface[3 * u + 1], H.hface[3 * u + 2]};
+    halo_words<true>(H, rec, h, t, bc);
+}
+
+// ---- one sweep on a tile that is exactly one un_ele (nsub = TS: levels of 256, 1,024 or 4,096
+// sub-elements per un_ele): k_face_sweep's sweep with every input the passes read issued at the
+// start, side by side with the iterate's and RHS's streams -- the un_ele's operator record (scalar
+// registers), its omega / D table and its halo snapshot (LDS), the face positions of the thread's
+// halo pairs -- so a tile waits on memory once (k_face_sweep waited on the record, the selector and
+// the snapshot word in turn inside each colour pass, then on the halo metadata: SQ 79 % of the waves'
+// cycles waiting, r03_b_face_sq.txt). The next sweep's halo words are halo_words' (no told reads).
+// Same face_apply arithmetic per sub-element: bitwise k_face_sweep's.
+template <int TS, int NT, bool RB>
+__global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_tile(
+    double *T, double *TNN, const double *__restrict__ RHS, const double *__restrict__ stc,
+    const int4 *__restrict__ fnb, const double *__restrict__ fface, const int *__restrict__ fsx,
+    const double *__restrict__ tin, HaloArgs Hn, int next_halo, int bc, int store, int64_t pitch, int slots,
+    int level1, double rdt) {
+    constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
+    static_assert(PER % 2 == 0 && M * M == TS, "whole un_ele tiles, adjacent pairs per thread");
+    __shared__ double X[3][TS];
+    __shared__ double HI[NH];
+    __shared__ double WD[24];
+    const int t = threadIdx.x;
+    const int64_t u = blockIdx.x, s0 = u * TS;
+    int4 nbr[PER];
+    double b[PER][3];
+    int hp[PER];
+    int4 hf[3];
+    if (next_halo) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {   // pair k = q / 2: sub-elements 2 (t + NT k) + (q & 1)
+            const int4 e = Hn.hsub[2 * (t + NT * (q / 2)) + (q & 1)];
+            hp[q] = e.x | (e.y << 10) | (e.z << 20);
+        }
+#pragma unroll
+        for (int f = 0; f < 3; ++f) hf[f] = Hn.hface[3 * u + f];
+    }
+    FaceRec R;
+    load_face_rec(stc, fface, fsx, u, R);
+    for (int i = t; i < NH; i += NT) HI[i] = tin[u * slots * 3 + (int64_t)(i / (3 * M)) * slots + i % (3 * M)];
+    if (t < 24) WD[t] = fface[u * kFaceStride + kFaceWD + t];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {   // tnew := tnew_nonlin (:550); the iterate into LDS
+        const int j = t + NT * k;
+        nbr[k] = fnb[j];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double v = TNN[c * pitch + s0 + j];
+            b[k][c] = RHS[c * pitch + s0 + j];
+            X[c][j] = v;
+            if (store == 1) T[c * pitch + s0 + j] = v;
+        }
+    }
+    __syncthreads();
+    auto xin = [&](int c, int q) { return X[c][q]; };
+    auto hv = [&](int64_t, int mf, int sp, int kk) { return HI[((mf - 1) * M + sp - 1) * 3 + kk]; };
+    auto pass = [&](auto mc) {
+        constexpr int MODE = decltype(mc)::value;
+        double r[PER][3];
+        bool on[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = t + NT * k;
+            const int4 nb = nbr[k];
+            on[k] = !((MODE == 0 && !nb.w) || (MODE == 1 && nb.w));
+            if (!on[k]) continue;
+            double x[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[c] = X[c][j];
+            const int wb = 3 * face_pattern(nb);
+            face_apply<MODE>(R, xin, x, b[k], nb, u, hv, [&](int i) { return WD[wb + i]; }, level1, rdt, r[k]);
+            if (MODE != 2)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) X[c][j] = r[k][c];
+        }
+        if (MODE == 2) {
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PER; ++k)
+                if (on[k])
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][t + NT * k] = r[k][c];
+        }
+        __syncthreads();
+    };
+    if constexpr (RB) {
+        pass(std::integral_constant<int, 0>{});
+        pass(std::integral_constant<int, 1>{});
+    } else {
+        pass(std::integral_constant<int, 2>{});
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew)
+        const int j = t + NT * k;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+    }
+    if (!next_halo) return;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (!hp[q]) continue;
+        const int j = 2 * (t + NT * (q / 2)) + (q & 1);
+        const double tv[3] = {X[0][j], X[1][j], X[2][j]};
+        halo_words<false>(Hn, hf, hp[q], tv, bc != 0);
     }
 }
 
@@ -498,7 +639,7 @@ hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, i
 bool face_sweep_fusable(const Level &L) { return L.nsub <= 4096; }
 
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots, int store) {
+                                   bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc) {
     if (L.N == 0) return hipSuccess;
     if (!L.fnb || !L.fface || !L.fsx || !face_sweep_fusable(L)) return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
@@ -508,14 +649,28 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
 #define PAMG_FSW(TS, NT, U, R)                                                                                      \
     hipLaunchKernelGGL((k_face_sweep<TS, NT, U, R>), dim3((unsigned)((L.N + TS - 1) / TS)), dim3(NT), 0, s, L.T,   \
                        L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tin, H, nh, st, L.pitch, L.N, lg, slots, l1, rdt, omega)
-    // tiles of one un_ele of 4,096 or 1,024 sub-elements; the coarse levels in tiles of 256 (more
-    // workgroups per CU for sweeps that are short and latency-bound)
-    if (L.nsub > 1024) {
+    // un_eles of 256, 1,024 or 4,096 sub-elements: one tile per un_ele (k_face_tile); the smaller
+    // ones in tiles of 256 (more workgroups per CU for sweeps that are short and latency-bound)
+    if ((L.nsub == 256 || L.nsub == 1024 || L.nsub == 4096) && L.N % L.nsub == 0) {
+        const dim3 g((unsigned)(L.N / L.nsub));
+        const int b = bc ? 1 : 0;
+#define PAMG_FTL(TS, NT, R)                                                                                         \
+    hipLaunchKernelGGL((k_face_tile<TS, NT, R>), g, dim3(NT), 0, s, L.T, L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, \
+                       tin, H, nh, b, st, L.pitch, slots, l1, rdt)
+        if (L.nsub == 4096) {
+            if (rb) PAMG_FTL(4096, 1024, true);
+            else PAMG_FTL(4096, 1024, false);
+        } else if (L.nsub == 1024) {
+            if (rb) PAMG_FTL(1024, 512, true);
+            else PAMG_FTL(1024, 512, false);
+        } else {
+            if (rb) PAMG_FTL(256, 128, true);
+            else PAMG_FTL(256, 128, false);
+        }
+#undef PAMG_FTL
+    } else if (L.nsub > 1024) {
         if (rb) PAMG_FSW(4096, 1024, true, true);
         else PAMG_FSW(4096, 1024, true, false);
-    } else if (L.nsub == 1024) {
-        if (rb) PAMG_FSW(1024, 512, true, true);
-        else PAMG_FSW(1024, 512, true, false);
     } else if (uni) {
         if (rb) PAMG_FSW(256, 128, true, true);
         else PAMG_FSW(256, 128, true, false);

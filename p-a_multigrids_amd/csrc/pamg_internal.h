@@ -66,6 +66,10 @@ struct HaloPlan {
     // flight; send_cur = the buffer holding the last packed words
     double *d_send_b = nullptr;
     int send_cur = 0;
+    // halo_exchange = 1 with the resident call: the tnew words of every cycle but the last, 3 per
+    // remote entry, ring_cap cycles (on first use), and the receive side of one of them
+    double *d_ring = nullptr, *d_recv3 = nullptr;
+    int ring_cap = 0;
     double *send_buf(int i) const { return i ? d_send_b : d_send; }
 };
 
@@ -189,6 +193,12 @@ struct pamg_handle {
     // op = 1: the local un_eles' neighbours (0-based local ids, -1: none or another rank), 3 per un_ele
     std::vector<int> neig_local;
     unsigned *chain_tmo = nullptr;   // sticky give-up word of the face chain's bounded spins
+    // the resident call's per-cycle exchange (halo_exchange = 1): per-cycle workgroup counters and
+    // the signal the comm stream waits on (cycles published so far: xc_sig_base after the last call)
+    unsigned *xc_done = nullptr;
+    int xc_cap = 0;
+    unsigned long long *xc_sig = nullptr;
+    unsigned long long xc_sig_base = 0;
     int cus = 0;                     // compute units of the device
 };
 
@@ -230,6 +240,8 @@ hipError_t launch_rhs(hipStream_t s, const Level &L, double rdt, int start_of_st
 // s' of level 1 into L.SRC (once, at upload): the source term of get_RHS from the geometry
 hipError_t launch_source(hipStream_t s, const Level &L, const double *geo1, double k);
 hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double *tovo);
+// the tnew words of one cycle of the resident call's ring exchange (3 per entry, d_recv3) into t_overlap
+hipError_t launch_halo_unpack3(hipStream_t s, const Level &L, double *tov);
 hipError_t launch_copy(hipStream_t s, const double *src, double *dst, int64_t n);
 hipError_t launch_told_halo(hipStream_t s, const Level &L, int U);
 // from_told: read told from the TOLD planes and also write the compact told copy
@@ -272,6 +284,13 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
 hipError_t launch_vcycle_resident(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                   int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
                                   int keep, bool rhsf, double *send_b, int cycles, int steps = 1);
+// the resident call with an exchange after every cycle (halo_exchange = 1): cycle c < cycles - 1
+// packs its remote halo words (3 per entry) into ring + c ring_stride and, once every workgroup has,
+// adds 1 to *xc_sig (xc_done: cycles - 1 zeroed counters); the last cycle is the plain resident call's
+hipError_t launch_vcycle_resident_xc(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                                     int n_coarse, double rdt, double *tov, double *tovo, double *send1,
+                                     double *rhsn2, int keep, int cycles, double *ring, int64_t ring_stride,
+                                     unsigned *xc_done, unsigned long long *xc_sig);
 bool vcycle_resident_supported(int n_split, int L);
 bool vcycle_resident_run_supported(int n_split, int L);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
@@ -297,9 +316,10 @@ hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov
 // words into tout; single domain, un_eles of at most 4096 sub-elements)
 bool face_sweep_fusable(const Level &L);
 // store: 0 tnew_nonlin; 1 tnew_nonlin and tnew (the sweep's start); 2 tnew := the result only (the
-// last executed sweep of a call whose final sweep is dead)
+// last executed sweep of a call whose final sweep is dead); bc: the call's first sweep (its next-halo
+// words include the boundary words of the other snapshot buffer)
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots, int store);
+                                   bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc);
 // the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of
 // the call's `total` sweeps in one launch, the iterate in LDS, the halo handed over between
 // workgroups inside the launch; store 1: tnew (the last sweep's start) and tnew_nonlin, 2: tnew :=

@@ -418,6 +418,15 @@ __global__ __launch_bounds__(kBlock) void k_halo_unpack(const double *__restrict
     }
 }
 
+__global__ __launch_bounds__(kBlock) void k_halo_unpack3(const double *__restrict__ recv, const int *__restrict__ dst,
+                                                         int n, double *__restrict__ tov) {
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const int d = dst[e];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) tov[d + q] = recv[3 * (int64_t)e + q];
+}
+
 // device-to-device copy of whole planes (tnew_nonlin := tnew, told := tnew)
 __global__ __launch_bounds__(kBlock) void k_copy(const double *__restrict__ a, double *__restrict__ b, int64_t n2) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (int64_t)gridDim.x * kBlock)
@@ -737,6 +746,14 @@ hipError_t launch_halo_unpack(hipStream_t s, const Level &L, double *tov, double
     const int n = (int)P.recv_dst.size();
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_halo_unpack, dim3(grid_for(n)), dim3(kBlock), 0, s, P.d_recv, P.d_recv_dst, n, tov, tovo);
+    return hipGetLastError();
+}
+
+hipError_t launch_halo_unpack3(hipStream_t s, const Level &L, double *tov) {
+    const HaloPlan &P = L.halo;
+    const int n = (int)P.recv_dst.size();
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_halo_unpack3, dim3(grid_for(n)), dim3(kBlock), 0, s, P.d_recv3, P.d_recv_dst, n, tov);
     return hipGetLastError();
 }
 

@@ -51,10 +51,13 @@ namespace {
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
                        double rdt, double *tov, double *tovo, double *send1, double *rhsn2, int part, int keep,
-                       int ua, int ub, double *send_b = nullptr, int cycles = 1, int steps = 1) {
+                       int ua, int ub, double *send_b = nullptr, int cycles = 1, int steps = 1,
+                       const VArgs *xc = nullptr) {
     const bool coarse = part == 1;
     if (part >= 2 && L < 2) return hipErrorInvalidValue;
     if (part >= 4 && cycles < 1) return hipErrorInvalidValue;
+    if ((part == 6) != (xc != nullptr) || (part == 6 && (cycles < 2 || !xc->ring || !xc->xc_done || !xc->xc_sig)))
+        return hipErrorInvalidValue;
     if (steps != 1 && !(part == 5 && steps > 1 && vcycle_resident_run_supported(n_split, L))) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
     VArgs A{};
@@ -92,6 +95,13 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.tile0 = fa >> TL;
     const unsigned grid = fb > fa ? (unsigned)((fb - fa + tm) >> TL) : 0u;
     if (grid == 0) return hipSuccess;
+    if (xc) {
+        A.ring = xc->ring;
+        A.ring_stride = xc->ring_stride;
+        A.xc_done = xc->xc_done;
+        A.xc_sig = xc->xc_sig;
+        A.xc_grid = grid;
+    }
     // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_VCYCLE_STAMPS") : nullptr;
     const int waves = coarse ? kMTc / 64 : fine_mt(n_split) / 64;
@@ -163,6 +173,19 @@ hipError_t launch_vcycle_resident(hipStream_t s, const Level *lv, int L, int U, 
                                   int keep, bool rhsf, double *send_b, int cycles, int steps) {
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, rhsn2, rhsf ? 5 : 4, keep, 0, -1,
                        send_b, cycles, steps);
+}
+
+hipError_t launch_vcycle_resident_xc(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                                     int n_coarse, double rdt, double *tov, double *tovo, double *send1,
+                                     double *rhsn2, int keep, int cycles, double *ring, int64_t ring_stride,
+                                     unsigned *xc_done, unsigned long long *xc_sig) {
+    VArgs X{};
+    X.ring = ring;
+    X.ring_stride = ring_stride;
+    X.xc_done = xc_done;
+    X.xc_sig = xc_sig;
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, rhsn2, 6, keep, 0, -1, nullptr,
+                       cycles, 1, &X);
 }
 
 // several time steps in one resident launch (k_vc_resb, or k_vc_res below n_split 5 and at L = 2)

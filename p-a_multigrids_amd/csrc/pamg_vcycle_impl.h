@@ -86,6 +86,15 @@ struct VArgs {
     int cycles;             // the resident launch: cycles of the call (of each time step)
     int steps;              // the resident launch starting time steps (RHSF): steps of the run, each
                             // told := tnew and its RHS, then `cycles` cycles; 1 otherwise
+    // the resident launch with an exchange after every cycle (part 6, halo_exchange = 1): cycle c <
+    // cycles - 1 packs the tnew words of its remote halo entries into ring + c ring_stride (3 per
+    // entry); each workgroup counts the cycle in xc_done[c] and the one that completes it adds 1 to
+    // *xc_sig, the signal the comm stream waits on (pamg_api.cpp vcycle_fused)
+    double *ring;
+    int64_t ring_stride;
+    unsigned *xc_done;
+    unsigned long long *xc_sig;
+    unsigned xc_grid;
 };
 
 }  // namespace vc
@@ -333,6 +342,32 @@ __device__ __forceinline__ void hs_write(bool uni, const HaloArgs &H, uint32_t u
     if (a) halo_face<true, false>(H, r1, 1, a, t, t);
     if (b) halo_face<true, false>(H, r2, 2, b, t, t);
     if (c) halo_face<true, false>(H, r3, 3, c, t, t);
+}
+
+// the tnew words of one sub-element's remote halo entries (mode 2) into a ring buffer of 3 words
+// per entry (the per-cycle exchange of the resident call)
+__device__ __forceinline__ void hs_ring(bool uni, const HaloArgs &H, double *ring, uint32_t u, int h,
+                                        const double t[3]) {
+    if (h == 0) return;
+    if (uni) u = __builtin_amdgcn_readfirstlane(u);
+    const int pos[3] = {h & 1023, (h >> 10) & 1023, h >> 20};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        if (!pos[f]) continue;
+        const int4 r = H.hface[3 * u + f];
+        if ((r.x & 3) != 2) continue;
+        double *o = ring + 3 * (int64_t)(r.z + pos[f] - 1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[c] = t[c];
+    }
+}
+
+// a workgroup's end of cycle c (after the barrier that follows every wave's drained ring stores):
+// count it; the workgroup that completes the cycle publishes it to the comm stream's signal
+// (release: the ring words are written back from this XCD's L2 before the count is seen)
+__device__ __forceinline__ void xc_signal(const VArgs &A, int c) {
+    const unsigned old = __hip_atomic_fetch_add(A.xc_done + c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == A.xc_grid) __hip_atomic_fetch_add(A.xc_sig, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the words of one sub-element that are constant within a time step (k_overlap_static's, from
@@ -977,7 +1012,7 @@ __device__ __forceinline__ uint32_t opaque(uint32_t u) {
     return u;
 }
 
-template <int S, int L, class ST, bool RHSF>
+template <int S, int L, class ST, bool RHSF, bool XC = false>
 __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, const double *__restrict__ sp0,
                                                                       const double *__restrict__ sp1,
                                                                       const double *__restrict__ sp2,
@@ -1151,6 +1186,11 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             store3p<PAMG_NT_TS>(V0.T(), V0.pitch, s0, p0[0], p0[1]);
             if (keep1) store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
         }
+        if constexpr (XC && !last)   // the cycle's remote halo words, exchanged while the next cycles run
+            if (v0) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k) hs_ring(G::uni(0), V0.H, A.ring + c * A.ring_stride, w0, h0[k], p0[k]);
+            }
         // ---- levels 2 .. C-1 (1-based): both smoother calls and get_residual of the cycle
         static_for<1, C>([&](auto lc) {
             constexpr int l = decltype(lc)::value;
@@ -1171,7 +1211,10 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             copy3(xs, p);
             if (last && vc) store3(V.T(), V.pitch, gxc, xs);
         });
+        if constexpr (XC && !last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring words drained
         __syncthreads();
+        if constexpr (XC && !last)
+            if (t == 0) xc_signal(A, c);
         // ---- after the call's last cycle: every coarse owner's RHSN, the restriction of the
         //      finer level's residual of that cycle (the next call's first RHS)
         if (last)
@@ -1233,7 +1276,7 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
 #define PAMG_RESB_WAVES 6
 #endif
 
-template <int S, int L, class ST, bool RHSF>
+template <int S, int L, class ST, bool RHSF, bool XC = false>
 __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) void k_vc_resb(VArgs A, const double *__restrict__ sp0,
                                                                 const double *__restrict__ sp1,
                                                                 const double *__restrict__ sp2,
@@ -1409,6 +1452,8 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
                 if (last && vc[k]) store3(V.T(), V.pitch, gc[k], xs[k]);
             });
             __syncthreads();
+            if constexpr (XC && !last)
+                if (lane_id() == 0) xc_signal(A, c);
             if (last) {
                 l2_rhsn(std::integral_constant<int, 2>{}, c, i2, g2, v2);
                 static_for<2, C>([&](auto lc) {
@@ -1539,7 +1584,16 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
                             if (keep1) store3(V0.TNN(), V0.pitch, sq, Y0[2]);
                         }
                 }
+                if constexpr (XC && !last) {   // the cycle's remote halo words, exchanged while the next cycles run
+                    double *rg = A.ring + c * A.ring_stride;
+                    if (vp)
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) hs_ring(true, V0.H, rg, w0, hs_pack(V0.H.hsub[(sp + k) & hmask]), X0[k]);
+                    if constexpr (N == 3)
+                        if (vq) hs_ring(true, V0.H, rg, w0, hs_pack(V0.H.hsub[sq & hmask]), X0[2]);
+                }
                 if constexpr (N == 2) l2_legs(std::integral_constant<int, 1>{}, lastc, c, gb, xs, bs, gc, vc);
+                if constexpr (XC && !last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring words drained
                 __syncthreads();
                 if constexpr (N == 2 && last) l2_rhsn(std::integral_constant<int, 1>{}, c, gb, gc, vc);
             };
@@ -1568,7 +1622,10 @@ template <int S, int L, class ST, bool W8>
 hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     if constexpr (std::is_same<ST, StcR>::value) {   // Richardson: the resident call only (k_vc_res)
         if constexpr (L >= 2 && fine_np(S) == 2) {
-            if (part == 5)
+            if (part == 6)
+                hipLaunchKernelGGL((k_vc_res<S, L, ST, false, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A,
+                                   A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+            else if (part == 5)
                 hipLaunchKernelGGL((k_vc_res<S, L, ST, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
                                    A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
             else if (part == 4)
@@ -1597,16 +1654,22 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
                                A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         else
             return hipErrorInvalidValue;
-    } else if (part == 4 || part == 5) {   // the resident call (5: starting a time step)
+    } else if (part >= 4 && part <= 6) {   // the resident call (5: starting a time step; 6: exchange every cycle)
         if constexpr (PAMG_RES_BALANCED && S >= 5 && L >= 3) {
-            if (part == 5)
+            if (part == 6)
+                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false, true>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
+                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+            else if (part == 5)
                 hipLaunchKernelGGL((k_vc_resb<S, L, ST, true>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
                                    A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
             else
                 hipLaunchKernelGGL((k_vc_resb<S, L, ST, false>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
                                    A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         } else if constexpr (L >= 2 && fine_np(S) == 2) {
-            if (part == 5)
+            if (part == 6)
+                hipLaunchKernelGGL((k_vc_res<S, L, ST, false, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A,
+                                   A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+            else if (part == 5)
                 hipLaunchKernelGGL((k_vc_res<S, L, ST, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
                                    A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
             else

@@ -93,6 +93,32 @@ def test_local_group_matches_single_domain(mesh, S, L, nparts, kind, fused, exch
         p.close()
 
 
+@pytest.mark.parametrize("S,L,kind,nparts,solver", [(5, 3, "strip", 8, 3), (3, 3, "block", 4, 3), (4, 2, "strip", 2, 2)])
+def test_local_group_exchange_every_cycle_inside_the_resident_call(S, L, kind, nparts, solver):
+    """halo_exchange = 1 keeps the resident call (k_vc_resb / k_vc_res with XC): every cycle but
+    the last packs its remote words into the ring and publishes the cycle on the device signal; the
+    comm stream waits on it and exchanges that cycle's words while the launch runs on. One launch,
+    one exchange per cycle, and the state is the single domain's bit for bit."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
+    kw = dict(solver=solver, arith=1)
+    full = pamg.SemiImplicitIterative(m, S, L, fused=0, **kw)
+    drive(full, "vcycle20")
+    owner = owners(m, kind, nparts)
+    parts = [pamg.SemiImplicitIterative(m, S, L, comm=(nparts, r, None, owner), fused=3, halo_exchange=1, **kw)
+             for r in range(nparts)]
+    local_group(parts)
+    for p in parts:
+        p.timing_enable(0x3F7F)
+        p.timing_reset()
+    run_ranks(parts, lambda p: drive(p, "vcycle20"))
+    check_parts(full, parts, owner)
+    for p in parts:
+        tm = p.timing()
+        assert tm["vcycle_res"]["issued"] == 1, tm["vcycle_res"]
+        assert tm["halo"]["issued"] == 20, tm["halo"]
+        p.close()
+
+
 def test_local_group_halo_mode_per_sweep():
     """halo_mode = 1 with the per-step kernels: one launch per sweep and an exchange after every
     sweep (the reference's halo schedule, :555), on 2 ranks."""
