@@ -467,10 +467,16 @@ int face_chain_check(pamg_handle *h) {
     return PAMG_OK;
 }
 
-bool face_fusable(pamg_handle *h, int l) {
+// a sweep as one launch on LDS tiles (k_face_tile / k_face_sweep) instead of the two colour
+// launches (PAMG_FACE_FUSED=0: the per-colour kernels)
+bool face_tiles_ok(pamg_handle *h, int l) {
     static const bool fuse_env = !getenv("PAMG_FACE_FUSED") || atoi(getenv("PAMG_FACE_FUSED")) != 0;
-    return fuse_env && h->p.op == 1 && h->nranks == 1 && !h->comm && face_sweep_fusable(h->lv[l]);
+    return fuse_env && h->p.op == 1 && face_sweep_fusable(h->lv[l]);
 }
+
+// ... and the whole smoother call with the halo words handed from sweep to sweep on the device
+// (face_call): a single domain (a partition exchanges them between sweeps)
+bool face_fusable(pamg_handle *h, int l) { return face_tiles_ok(h, l) && h->nranks == 1 && !h->comm; }
 
 int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) {
     Level &L = h->lv[l];
@@ -526,11 +532,18 @@ int smooth(pamg_handle *h, int l, bool src_is_T, int sweeps) {
         // single domain: one launch per sweep (PAMG_FACE_FUSED=0: the per-colour sequence)
         if (face_fusable(h, l)) return face_call(h, l, src_is_T, sweeps, false);
         if (src_is_T) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
+        // a partition: per sweep the halo refresh, the exchange, then the sweep itself -- one tile
+        // launch (both colours on the iterate in LDS, reading the exchanged t_overlap) or the two
+        // colour kernels
+        const bool tiles = face_tiles_ok(h, l);
         for (int s = 0; s < sweeps; ++s) {
             HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, true));   // tnew := tnew_nonlin (:550), :555
             CHK(halo(h, l));
-            Span sp(h, kid, bytes + 72.0 * (double)L.N);
-            if (h->p.solver == 3) {   // red-black Gauss-Seidel: up sub-elements, then down ones
+            Span sp(h, kid, tiles ? 72.0 * (double)L.N + 168.0 * h->U : bytes + 72.0 * (double)L.N);
+            if (tiles) {   // tnew_nonlin only: the refresh has copied tnew := tnew_nonlin
+                HIPCHK(h, launch_face_sweep_fused(h->stream, L, h->tov, nullptr, h->tovo, h->p.solver == 3, l == 1, rdt,
+                                                  h->p.omega, h->slots, 0, false));
+            } else if (h->p.solver == 3) {   // red-black Gauss-Seidel: up sub-elements, then down ones
                 HIPCHK(h, launch_face_sweep(h->stream, L, h->tov, 0, l == 1, rdt, h->p.omega, h->slots));
                 HIPCHK(h, launch_face_sweep(h->stream, L, h->tov, 1, l == 1, rdt, h->p.omega, h->slots));
             } else {
@@ -603,7 +616,8 @@ int face_residual(pamg_handle *h, int l, bool neg) {
     h->overlap_static_l1 = false;
     HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, false));
     CHK(halo(h, l));
-    Span sp(h, PAMG_K_RESIDUAL, 144.0 * (double)L.N + 168.0 * h->U);
+    // tnew, RHS in, residual out (the neighbours' values are the same tnew, gathered from cache)
+    Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)L.N + 168.0 * h->U);
     HIPCHK(h, launch_face_residual(h->stream, L, h->tov, neg, l == 1, 1 / h->p.dt, h->slots));
     return PAMG_OK;
 }
@@ -778,7 +792,7 @@ int vcycle_face_fused(pamg_handle *h, int n) {
             CHK(restrict_(h, l));
             Level &V = h->lv[l];
             h->rhsn_valid = false;
-            Span sp(h, PAMG_K_RESIDUAL, 144.0 * (double)V.N + 168.0 * h->U);
+            Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)V.N + 168.0 * h->U);   // tnew, RHS in, residual out
             HIPCHK(h, launch_face_residual(h->stream, V, h->tov, false, l == 1, rdt, h->slots));
         }
         CHK(face_call(h, L, true, ns * h->p.n_coarse, !last));   // :344-359
