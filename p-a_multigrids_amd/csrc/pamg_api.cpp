@@ -411,8 +411,8 @@ int sync_stream(pamg_handle *h, hipStream_t s) {
 // the persistent chain (pamg_face.hip k_face_chain) for a smoother call of level l: a single
 // domain whose level fits one workgroup per CU (face_chain_fits); PAMG_FACE_CHAIN=0 turns it off
 bool face_chain_ok(pamg_handle *h, int l) {
-    static const bool env = !getenv("PAMG_FACE_CHAIN") || atoi(getenv("PAMG_FACE_CHAIN")) != 0;
-    if (!env || h->nranks != 1 || h->comm || h->neig_local.empty()) return false;
+    const char *ev = getenv("PAMG_FACE_CHAIN");   // read per call: tests switch it within a process
+    if ((ev && atoi(ev) == 0) || h->nranks != 1 || h->comm || h->neig_local.empty()) return false;
     if (!h->cus) {
         int n = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || n <= 0) n = 1;
@@ -452,6 +452,94 @@ int face_chain_setup(pamg_handle *h, int l) {
     }
     L.chain_g = G;
     return PAMG_OK;
+}
+
+// The ticket order of the wavefront calls (k_face_wave): reverse Cuthill-McKee over the local
+// un_ele graph (BFS from a pseudo-peripheral un_ele of each component, neighbours by ascending
+// degree, reversed), and its band max |pos(u) - pos(v)| over the edges -- untitled8192: 3,754 in
+// file order, 63 in this one. A call of `run` sweeps needs (run - 1) band + 1 co-resident
+// workgroups to drain (pamg_face.hip k_face_wave).
+void rcm_order(const std::vector<int> &neig, int U, std::vector<int> &order, int &band) {
+    std::vector<int> deg(U, 0), pos(U, -1);
+    for (int u = 0; u < U; ++u)
+        for (int f = 0; f < 3; ++f) deg[u] += neig[3 * (size_t)u + f] >= 0;
+    order.clear();
+    std::vector<int> level(U, -1);
+    auto bfs = [&](int r, std::vector<int> &out) {   // breadth-first from r; returns the last level's size
+        out.clear();
+        out.push_back(r);
+        level[r] = 0;
+        for (size_t i = 0; i < out.size(); ++i) {
+            const int u = out[i];
+            int nb[3], n = 0;
+            for (int f = 0; f < 3; ++f) {
+                const int v = neig[3 * (size_t)u + f];
+                if (v >= 0 && level[v] < 0) { level[v] = level[u] + 1; nb[n++] = v; }
+            }
+            std::sort(nb, nb + n, [&](int a, int b) { return deg[a] != deg[b] ? deg[a] < deg[b] : a < b; });
+            for (int k = 0; k < n; ++k) out.push_back(nb[k]);
+        }
+    };
+    std::vector<int> comp;
+    for (int s = 0; s < U; ++s) {
+        if (pos[s] >= 0) continue;
+        // pseudo-peripheral start: repeat BFS from a minimum-degree un_ele of the farthest level
+        int r = s;
+        for (int it = 0; it < 4; ++it) {
+            bfs(r, comp);
+            const int last = level[comp.back()];
+            int best = comp.back();
+            for (int u : comp)
+                if (level[u] == last && deg[u] < deg[best]) best = u;
+            for (int u : comp) level[u] = -1;
+            if (best == r) break;
+            r = best;
+        }
+        bfs(r, comp);
+        for (int u : comp) pos[u] = 0;   // mark
+        order.insert(order.end(), comp.begin(), comp.end());
+    }
+    std::reverse(order.begin(), order.end());
+    for (int i = 0; i < U; ++i) pos[order[i]] = i;
+    band = 0;
+    for (int u = 0; u < U; ++u)
+        for (int f = 0; f < 3; ++f) {
+            const int v = neig[3 * (size_t)u + f];
+            if (v >= 0) band = std::max(band, std::abs(pos[u] - pos[v]));
+        }
+}
+
+int face_wave_setup(pamg_handle *h) {
+    if (h->wave_band >= 0) return PAMG_OK;
+    std::vector<int> order;
+    int band = 0;
+    rcm_order(h->neig_local, h->U, order, band);
+    CHK(dev_upload(h, &h->wave_order, order));
+    CHK(dev_upload(h, &h->wave_neig, h->neig_local));
+    CHK(dev_alloc(h, &h->wave_flags, (size_t)h->U + 16));
+    if (!h->chain_tmo) {
+        CHK(dev_alloc(h, &h->chain_tmo, 4));
+        HIPCHK(h, hipMemsetAsync(h->chain_tmo, 0, 4 * sizeof(unsigned), h->stream));
+    }
+    h->wave_band = band;
+    return PAMG_OK;
+}
+
+// the wavefront form for a call of `run` executed sweeps on level l (PAMG_FACE_WAVE=0: off):
+// returns its grid, 0 when the level's shape or the residency bound rules it out
+int face_wave_grid_for(pamg_handle *h, int l, int run) {
+    const char *ev = getenv("PAMG_FACE_WAVE");   // read per call: tests switch it within a process
+    if ((ev && atoi(ev) == 0) || run < 2 || h->nranks != 1 || h->comm || h->neig_local.empty() || !face_wave_shape(h->lv[l])) return 0;
+    if (!h->cus) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || n <= 0) n = 1;
+        h->cus = n;
+    }
+    if (face_wave_setup(h) != PAMG_OK) return 0;
+    const int g = face_wave_grid(h->lv[l], h->p.solver == 3, h->cus);
+    // every un_ele resident at once, or the ticket window wide enough for the call's sweeps
+    if (g <= 0 || (g < h->U && (int64_t)(run - 1) * h->wave_band + 1 > g)) return 0;
+    return g;
 }
 
 // the sticky give-up word of the chain's bounded spins: a call that hit it failed
@@ -501,6 +589,14 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags, L.chain_nb_off,
                                     L.chain_nb_list, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
                                     l == 1, rdt, h->p.omega, h->slots));
+        return PAMG_OK;
+    }
+    if (const int g = face_wave_grid_for(h, l, run)) {   // the call in one wavefront launch
+        // the state crosses HBM once per call, as the chain's
+        Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
+        HIPCHK(h, launch_face_wave(h->stream, L, h->U, g, h->tov, h->tov_b, h->tovo, h->wave_flags, h->wave_order,
+                                   h->wave_neig, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3, l == 1,
+                                   rdt, h->slots));
         return PAMG_OK;
     }
     for (int s = 0; s < run; ++s) {
@@ -1137,7 +1233,7 @@ void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
         Level &L = h->lv[l];
         dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.d_pos); dev_free(L.blocks);
-        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx);
+        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx); dev_free(L.cpos);
         dev_free(L.chain_nb_off); dev_free(L.chain_nb_list); dev_free(L.chain_flags);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
@@ -1148,6 +1244,10 @@ void free_levels(pamg_handle *h) {
     }
     dev_free(h->geo1); dev_free(h->tov); dev_free(h->tovo); dev_free(h->tov_b);
     h->geo1 = h->tov = h->tovo = h->tov_b = nullptr;
+    dev_free(h->wave_order); dev_free(h->wave_neig); dev_free(h->wave_flags);
+    h->wave_order = h->wave_neig = nullptr;
+    h->wave_flags = nullptr;
+    h->wave_band = -1;
     h->mesh_ready = false;
 }
 
@@ -1417,6 +1517,14 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
             CHK(dev_upload(h, &L.fnb, fnb));
             CHK(dev_upload(h, &L.fface, fface));
             CHK(dev_upload(h, &L.fsx, fsx));
+            std::vector<int> cpos;
+            for (int pass = 0; pass < 2; ++pass)
+                for (int j = 0; j < L.nsub; ++j)
+                    if ((fnb[j].w != 0) == (pass == 0)) cpos.push_back(j);
+            L.nup = 0;
+            for (int j = 0; j < L.nsub; ++j) L.nup += fnb[j].w != 0;
+            L.ndn = L.nsub - L.nup;
+            CHK(dev_upload(h, &L.cpos, cpos));
         }
         HaloPlan &P = L.halo;
         CHK(dev_upload(h, &P.d_local, P.local));

@@ -332,11 +332,6 @@ __device__ __forceinline__ void halo_words(const HaloArgs &H, const int4 rec[3],
     }
 }
 
-__device__ __forceinline__ void chain_halo(const HaloArgs &H, int64_t u, int h, const double t[3], bool bc) {
-    const int4 rec[3] = {H.hface[3 * u], H.hface[3 * u + 1], H.hface[3 * u + 2]};
-    halo_words<true>(H, rec, h, t, bc);
-}
-
 // ---- one sweep on a tile that is exactly one un_ele (nsub = TS: levels of 256, 1,024 or 4,096
 // sub-elements per un_ele): k_face_sweep's sweep with every input the passes read issued at the
 // start, side by side with the iterate's and RHS's streams -- the un_ele's operator record (scalar
@@ -441,7 +436,241 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
     }
 }
 
-template <bool UNI, bool RB>
+// ---- the wavefront call: every sweep of one smoother call on a level too large to stay on-chip
+// (levels 1 and 2 at n_split = 5: 8.4 M and 2.1 M sub-elements), each un_ele crossing HBM once per
+// call instead of once per sweep. A persistent cooperative grid of G workgroups takes un_eles in
+// ticket order (`order`: a reverse Cuthill-McKee numbering of the un_ele graph, host-built, band b);
+// a workgroup keeps its un_ele's iterate in LDS and its RHS in registers for the whole call and runs
+// sweep s once every neighbour has published its words for sweep s (flags[v] >= s, per un_ele), the
+// chain's hand-off (write-through halo words, drain, barrier, flag; ld_coh reads; snapshot buffers by
+// parity, safe for the chain's reason: a neighbour overwrites the buffer of sweep s - 1 only after
+// this un_ele has published sweep s, i.e. after it read that snapshot). Progress: the lowest
+// unfinished ticket t0 is resident, tickets [t0, t0 + G) are claimed, and a ticket in
+// [t0, t0 + G - k b) can always reach sweep k -- so G >= (run - 1) b + 1 (face_wave_ok) guarantees
+// the grid drains; the spins are bounded anyway (*tmo, as the chain). Every sub-element's arithmetic
+// is face_apply's on the same snapshot words, so the result is bitwise the per-sweep launches'.
+// A thread's sub-elements in the passes ("items", fixed for the whole call): red-black runs each
+// colour over its own position list (Level::cpos), so every lane of a pass has a sub-element of that
+// colour (one launch per sweep masked half the lanes of each colour pass: twice the fp64 issue);
+// Jacobi takes the positions in order. j = storage position in the tile, -1 none; nb its fnb entry,
+// b its RHS.
+template <int K>
+struct Items {
+    int j[K];
+    int4 nb[K];
+    double b[K][3];
+};
+
+// one pass (MODE 0 / 1 a colour, 2 Jacobi) of a tile's items (j: tile positions); rec(j, nb, f) calls
+// f with the item's un_ele record, un_ele, omega / D row and the un_ele's first tile position; xin reads
+// the tile; the rest as face_apply. out(k, r): the item's result --
+// stored in place at once by a colour pass (a colour reads only the other colour), held by Jacobi
+template <int MODE, int K, class XIN, class HV, class REC, class OUT>
+__device__ __forceinline__ void items_pass(const Items<K> &I, const XIN &xin, const HV &hv, const REC &rec, int level1,
+                                           double rdt, const OUT &out) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int j = I.j[k];
+        if (j < 0) continue;
+        double x[3], r[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c] = xin(c, j);
+        rec(j, I.nb[k], [&](const FaceRec &R, int64_t u, const double *wd, int jb) {
+            auto xb = [&](int c, int q) { return xin(c, jb + q); };   // un_ele-relative neighbour positions
+            face_apply<MODE>(R, xb, x, I.b[k], I.nb[k], u, hv, [&](int i) { return wd[i]; }, level1, rdt, r);
+        });
+        out(k, r);
+        asm volatile("" ::: "memory");   // one item at a time: its record's registers are not held across items
+    }
+}
+
+constexpr int kWaveStampT = 32, kWaveStampW = 19;   // tickets per workgroup, stamps per ticket
+#ifndef PAMG_WAVE_WAVES
+#define PAMG_WAVE_WAVES 4
+#endif
+template <int TS, int NT, bool RB>
+struct WaveShape {
+    static constexpr int M = TS == 256 ? 16 : TS == 1024 ? 32 : 64;
+    static constexpr int NUP = M * (M + 1) / 2, NDN = M * (M - 1) / 2;   // up / down sub-elements
+    static constexpr int KU = RB ? (NUP + NT - 1) / NT : TS / NT, KD = RB ? (NDN + NT - 1) / NT : 1;
+};
+
+template <int TS, int NT, bool RB>
+__global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_wave(
+    double *T, double *TNN, const double *__restrict__ RHS, const double *__restrict__ stc,
+    const int4 *__restrict__ fnb, const double *__restrict__ fface, const int *__restrict__ fsx,
+    const int *__restrict__ cpos, int nup, double *buf0, double *buf1, HaloArgs H, unsigned *flags,
+    const int *__restrict__ order, const int *__restrict__ neig, unsigned *tmo, int U, int run, int total,
+    int store, int64_t pitch, int slots, int level1, double rdt, long long *stamps) {
+    using WS = WaveShape<TS, NT, RB>;
+    constexpr int PER = TS / NT, M = WS::M, NH = 9 * M, KU = WS::KU, KD = WS::KD;
+    static_assert(PER % 2 == 0 && M * M == TS, "whole un_ele tiles, adjacent pairs per thread");
+    __shared__ double X[3][TS];
+    __shared__ double HI[NH];
+    __shared__ double WD[24];
+    __shared__ int s_tk;
+    const int t = threadIdx.x;
+    unsigned *ticket = flags + U;   // the claim counter sits after the per-un_ele flags
+    int hp[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {   // face positions of the thread's halo pairs (the same in every un_ele)
+        const int4 e = H.hsub[2 * (t + NT * (q / 2)) + (q & 1)];
+        hp[q] = e.x | (e.y << 10) | (e.z << 20);
+    }
+    // the thread's items: the first colour (all positions for Jacobi), then the second
+    Items<KU> IA;
+    Items<KD> IB;
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
+        const int i = t + NT * k;
+        IA.j[k] = RB ? (i < nup ? cpos[i] : -1) : i;
+        IA.nb[k] = fnb[IA.j[k] < 0 ? 0 : IA.j[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < KD; ++k) {
+        const int i = t + NT * k;
+        IB.j[k] = RB && i < TS - nup ? cpos[nup + i] : -1;
+        IB.nb[k] = fnb[IB.j[k] < 0 ? 0 : IB.j[k]];
+    }
+    // diagnostics (PAMG_WAVE_STAMPS): per ticket of workgroups 0..7 (the first kWaveStampT), wall
+    // clock at the claim, after the state's load, per sweep after the wait / snapshot / passes /
+    // publish, at the end
+    int nt_w = 0;
+    for (;;) {
+        if (t == 0) s_tk = (int)__hip_atomic_fetch_add((g_u32 *)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int tk = s_tk;
+        if (tk >= U) break;
+        long long *st = (stamps && t == 0 && blockIdx.x < 8 && nt_w < kWaveStampT)
+                            ? stamps + ((int64_t)blockIdx.x * kWaveStampT + nt_w) * kWaveStampW
+                            : nullptr;
+        ++nt_w;
+        if (st) st[0] = wall_clock64();
+        const int64_t u = __builtin_amdgcn_readfirstlane(order[tk]);
+        const int64_t s0 = u * TS;
+        int4 hf[3];
+#pragma unroll
+        for (int f = 0; f < 3; ++f) hf[f] = H.hface[3 * u + f];
+        FaceRec R;
+        load_face_rec(stc, fface, fsx, u, R);
+        if (t < 24) WD[t] = fface[u * kFaceStride + kFaceWD + t];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = t + NT * k;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) X[c][j] = TNN[c * pitch + s0 + j];
+        }
+#pragma unroll
+        for (int k = 0; k < KU; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) IA.b[k][c] = IA.j[k] < 0 ? 0.0 : RHS[c * pitch + s0 + IA.j[k]];
+#pragma unroll
+        for (int k = 0; k < KD; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) IB.b[k][c] = IB.j[k] < 0 ? 0.0 : RHS[c * pitch + s0 + IB.j[k]];
+        int nv = -1;   // lanes 0..2 of wave 0 poll the neighbours' flags
+        if (t < 3) nv = neig[3 * u + t];
+        if (st) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st[1] = wall_clock64();
+        }
+        auto xin = [&](int c, int q) { return X[c][q]; };
+        auto hv = [&](int64_t, int mf, int sp, int kk) { return HI[((mf - 1) * M + sp - 1) * 3 + kk]; };
+        auto rec = [&](int, int4 nb, auto &&f) { f(R, u, WD + 3 * face_pattern(nb), 0); };
+        for (int sw = 0; sw < run; ++sw) {
+            const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
+            double *tout = sw + 1 < total ? (((total - 2 - sw) & 1) ? buf1 : buf0) : nullptr;
+            // the items' positions and neighbour entries opaque per sweep: the LDS addresses derived
+            // from them are recomputed in each sweep instead of hoisted out of the loop (VGPRs)
+#pragma unroll
+            for (int k = 0; k < KU; ++k) asm volatile("" : "+v"(IA.j[k]), "+v"(IA.nb[k].x), "+v"(IA.nb[k].y), "+v"(IA.nb[k].z), "+v"(IA.nb[k].w));
+#pragma unroll
+            for (int k = 0; k < KD; ++k) asm volatile("" : "+v"(IB.j[k]), "+v"(IB.nb[k].x), "+v"(IB.nb[k].y), "+v"(IB.nb[k].z), "+v"(IB.nb[k].w));
+            if (sw > 0 && t < 64) {   // the neighbours' words of this sweep
+                bool ok = nv < 0;
+                for (unsigned spins = 0;; ++spins) {
+                    if (!ok)
+                        ok = __hip_atomic_load((g_u32 *)(flags + nv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                             (unsigned)sw;
+                    if (__all(ok)) break;
+                    if (spins > (1u << 22)) {
+                        if (t == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            const int sk = 2 + 4 * (sw < 4 ? sw : 3);
+            if (st) st[sk] = wall_clock64();
+            for (int i = t; i < NH; i += NT) HI[i] = ld_coh(tin + u * slots * 3 + (int64_t)(i / (3 * M)) * slots + i % (3 * M));
+            __syncthreads();
+            if (st) st[sk + 1] = wall_clock64();
+            if (store == 1 && sw + 1 == run)   // the call's last sweep: tnew := tnew_nonlin (:550)
+#pragma unroll
+                for (int k = 0; k < PER; ++k)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) T[c * pitch + s0 + t + NT * k] = X[c][t + NT * k];
+            if constexpr (RB) {   // up sub-elements, then down ones, in place (a colour reads only the other)
+                items_pass<0>(IA, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][IA.j[k]] = r[c];
+                });
+                __syncthreads();
+                items_pass<1>(IB, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][IB.j[k]] = r[c];
+                });
+            } else {   // Jacobi: every read of the old iterate before any write
+                double rj[KU][3];
+                items_pass<2>(IA, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) rj[k][c] = r[c];
+                });
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < KU; ++k)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][IA.j[k]] = rj[k][c];
+            }
+            __syncthreads();
+            if (st) st[sk + 2] = wall_clock64();
+            if (tout) {   // the next sweep's halo words (:550, :555 of sweep sw + 1), written through
+                HaloArgs Hn = H;
+                Hn.tov = tout;
+#pragma unroll
+                for (int q = 0; q < PER; ++q) {
+                    // opaque per sweep: the destinations are recomputed here instead of hoisted
+                    // out of the sweep loop (that held ~80 more VGPRs)
+                    int hq = hp[q];
+                    asm volatile("" : "+v"(hq));
+                    if (!hq) continue;
+                    const int j = 2 * (t + NT * (q / 2)) + (q & 1);
+                    const double tv[3] = {X[0][j], X[1][j], X[2][j]};
+                    halo_words<true>(Hn, hf, hq, tv, sw == 0);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (t == 0) __hip_atomic_store((g_u32 *)flags + u, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (st) st[sk + 3] = wall_clock64();
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew, the dead last sweep's :550)
+            const int j = t + NT * k;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+        }
+        if (st) st[kWaveStampW - 1] = wall_clock64();
+        __syncthreads();   // s_tk and X are rewritten by the next ticket
+    }
+}
+
+// LREC: the workgroup's un_eles' operator records (FaceRec + omega / D) sit in LDS for the whole call
+// (at most kChainRec un_eles): the passes read them there instead of fetching them from memory in
+// every pass (the dependent record fetches were most of a sweep's pass time, r03 stamps)
+constexpr int kChainRec = 32, kRecW = 48;   // un_eles, doubles per record: S 13 | w 6 | WD 24 | sx 3
+template <bool UNI, bool RB, bool LREC>
 __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *TNN, const double *__restrict__ RHS,
                                                           const double *__restrict__ stc, const int4 *__restrict__ fnb,
                                                           const double *__restrict__ fface, const int *__restrict__ fsx,
@@ -449,16 +678,71 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                                                           const int *__restrict__ nb_off, const int *__restrict__ nb_list,
                                                           unsigned *tmo, int run, int total, int store, int E,
                                                           int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
-                                                          double rdt, double omega, long long *stamps) {
+                                                          double rdt, double omega, const int *__restrict__ cpos,
+                                                          int nup, long long *stamps) {
     constexpr int NT = kChainNT, PER = kChainPer;
     __shared__ double X[3][NT * PER];
     __shared__ double HI[kChainHalo];   // this workgroup's un_eles' t_overlap(1 : 3m, 1 : 3) of the sweep
+    __shared__ double RS[LREC ? kChainRec * kRecW : 1];
     const int t = threadIdx.x, w = blockIdx.x;
     const int64_t s0 = (int64_t)w * E;
     const int64_t nsm = (1ll << nsub_log2) - 1;
     const int m = H.m, ke = E >> nsub_log2;   // positions along an un_ele face, un_eles of the workgroup
     const int64_t u0 = s0 >> nsub_log2;
     const int nhalo = ke * 9 * m;
+    if constexpr (LREC) {
+        const int kv = (int)std::min<int64_t>(ke, (N >> nsub_log2) - u0);
+        for (int i = t; i < kv * kRecW; i += NT) {
+            const int uk = i / kRecW, q = i - uk * kRecW;
+            const int64_t u = u0 + uk;
+            double v = 0.0;
+            if (q == 0) v = stc[u * kStcStride + kStcC];
+            else if (q < 10) v = stc[u * kStcStride + kStcK + q - 1];
+            else if (q < 13) v = stc[u * kStcStride + kStcW + q - 10];
+            else if (q < 19) v = fface[u * kFaceStride + q - 13];
+            else if (q < 43) v = fface[u * kFaceStride + kFaceWD + q - 19];
+            else if (q < 46) v = (double)fsx[4 * u + cFMface[q - 43] - 1];
+            RS[i] = v;
+        }
+    }
+    // with LREC the passes run over item lists (red-black: each colour over its positions, all lanes
+    // busy; Jacobi: the positions in order), as k_face_wave's
+    constexpr int KU = PER, KD = RB ? 1 : 0;
+    Items<KU> IA;
+    Items<KD == 0 ? 1 : KD> IB;
+    if constexpr (LREC) {
+        const int kv = (int)std::min<int64_t>(ke, (N >> nsub_log2) - u0), nsub = 1 << nsub_log2;
+        const int ndn = nsub - nup;
+#pragma unroll
+        for (int k = 0; k < KU; ++k) {
+            const int i = t + NT * k;
+            int j = -1;
+            if (RB) {
+                if (i < kv * nup) {
+                    const int uk = i / nup;
+                    j = (uk << nsub_log2) + cpos[i - uk * nup];
+                }
+            } else if (i < kv * nsub) {
+                j = i;
+            }
+            IA.j[k] = j;
+        }
+        IB.j[0] = -1;
+        if (RB && ndn > 0 && t < kv * ndn) {
+            const int uk = t / ndn;
+            IB.j[0] = (uk << nsub_log2) + cpos[nup + t - uk * ndn];
+        }
+        auto fill = [&](auto &I, int K) {
+            for (int k = 0; k < K; ++k) {
+                const int j = I.j[k] < 0 ? 0 : I.j[k];
+                I.nb[k] = fnb[j & nsm];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) I.b[k][c] = RHS[c * pitch + s0 + j];
+            }
+        };
+        fill(IA, KU);
+        if (KD) fill(IB, 1);
+    }
     double b[PER][3];
     int4 nbr[PER];
 #pragma unroll
@@ -520,6 +804,13 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
         }
         __syncthreads();
     };
+    // the face records of the thread's halo pair's un_ele, fetched once for the call
+    int4 hrec[3] = {};
+    if ((hp[0] | hp[1]) != 0) {
+        const int64_t u = (s0 + 2 * t) >> nsub_log2;
+#pragma unroll
+        for (int f = 0; f < 3; ++f) hrec[f] = H.hface[3 * u + f];
+    }
     const int na = nb_off[w], nn = nb_off[w + 1] - na;
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
@@ -563,7 +854,54 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 #pragma unroll
                     for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = X[c][j];
             }
-        if constexpr (RB) {
+        if constexpr (LREC) {
+#pragma unroll
+            for (int k = 0; k < KU; ++k) asm volatile("" : "+v"(IA.j[k]), "+v"(IA.nb[k].x), "+v"(IA.nb[k].y), "+v"(IA.nb[k].z), "+v"(IA.nb[k].w));
+            asm volatile("" : "+v"(IB.j[0]), "+v"(IB.nb[0].x), "+v"(IB.nb[0].y), "+v"(IB.nb[0].z), "+v"(IB.nb[0].w));
+            auto xin = [&](int c, int q) { return X[c][q]; };
+            auto hv = [&](int64_t uu, int mf, int sp, int kk) {
+                return HI[(((int)(uu - u0) * 3 + mf - 1) * m + sp - 1) * 3 + kk];
+            };
+            auto rec = [&](int j, int4 nb, auto &&f) {
+                const int uk = j >> nsub_log2;
+                const double *rs = RS + uk * kRecW;
+                FaceRec R;
+                R.S.c = rs[0];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) R.S.K[q] = rs[1 + q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) R.S.w[q] = rs[10 + q];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) R.w[q] = rs[13 + q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) R.sx[q] = (int)rs[43 + q];
+                f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
+            };
+            if constexpr (RB) {   // up sub-elements, then down ones, in place
+                items_pass<0>(IA, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][IA.j[k]] = r[c];
+                });
+                __syncthreads();
+                items_pass<1>(IB, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][IB.j[k]] = r[c];
+                });
+            } else {   // Jacobi: every read of the old iterate before any write
+                double rj[KU][3];
+                items_pass<2>(IA, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) rj[k][c] = r[c];
+                });
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < KU; ++k)
+                    if (IA.j[k] >= 0)
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) X[c][IA.j[k]] = rj[k][c];
+            }
+            __syncthreads();
+        } else if constexpr (RB) {
             pass(std::integral_constant<int, 0>{});
             pass(std::integral_constant<int, 1>{});
         } else {
@@ -574,13 +912,19 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             HaloArgs Hn = H;
             Hn.tov = tout;
             const int j = 2 * t;
-            if ((hp[0] | hp[1]) != 0) {
+            // opaque per sweep: the halo destinations are recomputed here instead of hoisted out of the
+            // sweep loop (held in registers they spilled)
+            int hq[2] = {hp[0], hp[1]};
+            int4 hr[3] = {hrec[0], hrec[1], hrec[2]};
+            asm volatile("" : "+v"(hq[0]), "+v"(hq[1]));
+#pragma unroll
+            for (int f = 0; f < 3; ++f) asm volatile("" : "+v"(hr[f].x), "+v"(hr[f].y), "+v"(hr[f].z));
+            if ((hq[0] | hq[1]) != 0) {
                 // per lane: a wave's pairs span 128 sub-elements, two un_eles when nsub = 64
-                const int64_t u = (s0 + j) >> nsub_log2;
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const double tv[3] = {X[0][j + q], X[1][j + q], X[2][j + q]};
-                    chain_halo(Hn, u, hp[q], tv, sw == 0);
+                    halo_words<true>(Hn, hr, hq[q], tv, sw == 0);
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
@@ -722,11 +1066,18 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
         e = hipMemsetAsync(stamps, 0, nst * sizeof(long long), s);
         if (e != hipSuccess) return e;
     }
+    const int *cpos = L.cpos;
+    int nup = L.nup;
     void *args[] = {&T, &TNN, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
-                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &stamps};
-    const bool uni = L.nsub >= 64;
-    const void *f = uni ? (rb ? (const void *)k_face_chain<true, true> : (const void *)k_face_chain<true, false>)
-                        : (rb ? (const void *)k_face_chain<false, true> : (const void *)k_face_chain<false, false>);
+                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &stamps};
+    // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
+    const bool uni = L.nsub >= 64,
+               lrec = k <= kChainRec && L.cpos && (int64_t)k * L.nup <= 2 * kChainNT && (int64_t)k * L.ndn <= kChainNT;
+
+#define PAMG_CHF(U_, R_) (lrec ? (const void *)k_face_chain<U_, R_, true> : (const void *)k_face_chain<U_, R_, false>)
+    const void *f = uni ? (rb ? PAMG_CHF(true, true) : PAMG_CHF(true, false))
+                        : (rb ? PAMG_CHF(false, true) : PAMG_CHF(false, false));
+#undef PAMG_CHF
     hipError_t e = hipLaunchCooperativeKernel(f, dim3(grid), dim3(kChainNT), args, 0, s);
     if (stamp_path) {
         std::vector<long long> h(nst);
@@ -737,6 +1088,80 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
             const long long hdr[4] = {run, grid, E, L.nsub};
             fwrite(hdr, sizeof hdr, 1, fp);
             fwrite(h.data(), sizeof(long long), nst, fp);
+            fclose(fp);
+        }
+    }
+    return e;
+}
+
+// the wavefront call (k_face_wave): levels whose un_eles are 256, 1,024 or 4,096 sub-elements
+bool face_wave_shape(const Level &L) {
+    const int m = L.nsub == 256 ? 16 : L.nsub == 1024 ? 32 : L.nsub == 4096 ? 64 : 0;
+    // the colour lists' sizes are the kernel's compile-time item counts
+    return m && L.N % L.nsub == 0 && L.cpos && L.nup == m * (m + 1) / 2;
+}
+
+namespace {
+const void *face_wave_fn(int nsub, bool rb, int *nt) {
+    switch (nsub) {
+        case 4096: *nt = 1024; return rb ? (const void *)k_face_wave<4096, 1024, true> : (const void *)k_face_wave<4096, 1024, false>;
+        case 1024: *nt = 512; return rb ? (const void *)k_face_wave<1024, 512, true> : (const void *)k_face_wave<1024, 512, false>;
+        case 256: *nt = 128; return rb ? (const void *)k_face_wave<256, 128, true> : (const void *)k_face_wave<256, 128, false>;
+        default: *nt = 0; return nullptr;
+    }
+}
+}  // namespace
+
+// co-resident workgroups of the wavefront kernel for this level (0: not launchable)
+int face_wave_grid(const Level &L, bool rb, int cus) {
+    int nt = 0, per = 0;
+    const void *f = face_wave_fn(L.nsub, rb, &nt);
+    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, nt, 0) != hipSuccess) return 0;
+    return per * cus;
+}
+
+hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, double *tov, double *tov_b, double *tovo,
+                            unsigned *flags, const int *order, const int *neig, unsigned *tmo, int run, int total,
+                            int store, bool rb, bool level1, double rdt, int slots) {
+    if (L.N == 0 || run <= 0) return hipSuccess;
+    int nt = 0;
+    const void *f = face_wave_fn(L.nsub, rb, &nt);
+    if (!f || !face_wave_shape(L) || !L.fnb || grid <= 0) return hipErrorInvalidValue;
+    const HaloPlan &P = L.halo;
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << L.isplit};
+    int l1 = level1 ? 1 : 0;
+    double *T = L.T, *TNN = L.TNN;
+    const double *RHS = L.RHS, *stc = L.stc, *fface = L.fface;
+    const int4 *fnb = L.fnb;
+    const int *fsx = L.fsx;
+    int64_t pitch = L.pitch;
+    hipError_t e = hipMemsetAsync(flags, 0, sizeof(unsigned) * ((size_t)U + 1), s);
+    if (e != hipSuccess) return e;
+    // PAMG_WAVE_STAMPS=<file>: append every launch's per-ticket phase stamps of workgroups 0..7
+    static const char *stamp_path = getenv("PAMG_WAVE_STAMPS");
+    long long *stamps = nullptr;
+    const size_t nst = (size_t)8 * kWaveStampT * kWaveStampW;
+    if (stamp_path) {
+        e = hipMalloc(&stamps, nst * sizeof(long long));
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(stamps, 0, nst * sizeof(long long), s);
+        if (e != hipSuccess) return e;
+    }
+    const int g = std::min(grid, U);
+    const int *cpos = L.cpos;
+    int nup = L.nup;
+    void *args[] = {&T, &TNN, &RHS, &stc, &fnb, &fface, &fsx, &cpos, &nup, &tov, &tov_b, &H, &flags, &order, &neig,
+                    &tmo, &U, &run, &total, &store, &pitch, &slots, &l1, &rdt, &stamps};
+    e = hipLaunchCooperativeKernel(f, dim3(g), dim3(nt), args, 0, s);
+    if (stamp_path) {
+        std::vector<long long> hs(nst);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpy(hs.data(), stamps, nst * sizeof(long long), hipMemcpyDeviceToHost);
+        (void)hipFree(stamps);
+        if (FILE *fp = fopen(stamp_path, "ab")) {
+            const long long hdr[4] = {run, g, U, L.nsub};
+            fwrite(hdr, sizeof hdr, 1, fp);
+            fwrite(hs.data(), sizeof(long long), nst, fp);
             fclose(fp);
         }
     }

@@ -109,6 +109,10 @@ struct Level {
     int4 *fnb = nullptr;
     double *fface = nullptr;
     int *fsx = nullptr;
+    // the colour lists of the red-black passes: the storage positions of the up sub-elements
+    // (fnb.w != 0, ascending), then of the down ones -- nup + ndn = nsub
+    int *cpos = nullptr;
+    int nup = 0, ndn = 0;
     double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
     // the persistent face chain (pamg_face.hip k_face_chain; lazy): its workgroups' neighbour lists
@@ -193,6 +197,12 @@ struct pamg_handle {
     // op = 1: the local un_eles' neighbours (0-based local ids, -1: none or another rank), 3 per un_ele
     std::vector<int> neig_local;
     unsigned *chain_tmo = nullptr;   // sticky give-up word of the face chain's bounded spins
+    // the face operator's wavefront calls (k_face_wave; lazy, single domain): the ticket order (a
+    // reverse Cuthill-McKee numbering of neig_local), its band, the neighbours on the device and the
+    // per-un_ele flags + ticket counter
+    int *wave_order = nullptr, *wave_neig = nullptr;
+    unsigned *wave_flags = nullptr;
+    int wave_band = -1;
     // the resident call's per-cycle exchange (halo_exchange = 1): per-cycle workgroup counters and
     // the signal the comm stream waits on (cycles published so far: xc_sig_base after the last call)
     unsigned *xc_done = nullptr;
@@ -325,6 +335,14 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
 // workgroups inside the launch; store 1: tnew (the last sweep's start) and tnew_nonlin, 2: tnew :=
 // the result (dead last sweep)
 bool face_chain_fits(int nsub, int U, int cus);
+// the wavefront form of one smoother call (k_face_wave, levels of 256 / 1,024 / 4,096 sub-elements
+// per un_ele): un_eles claimed in the ticket order `order`, flags = U per-un_ele words + the ticket
+// counter (zeroed here), neig = 3 local neighbours per un_ele (-1 none); grid = co-resident workgroups
+bool face_wave_shape(const Level &L);
+int face_wave_grid(const Level &L, bool rb, int cus);
+hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, double *tov, double *tov_b, double *tovo,
+                            unsigned *flags, const int *order, const int *neig, unsigned *tmo, int run, int total,
+                            int store, bool rb, bool level1, double rdt, int slots);
 int face_chain_per_wg(int nsub, int U, int cus);
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,

@@ -160,3 +160,37 @@ def test_face_fused_cycle_equals_per_step_sequence(mesh, S, L, solver, ns):
         for x, y in zip(g.overlap(), rov):
             np.testing.assert_array_equal(x, y)
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,solver,ns,n", [
+    ("untitled8192.msh", 5, 3, 3, 4, 2), ("untitled8192.msh", 5, 2, 1, 3, 1), ("untitled8192.msh", 4, 3, 3, 4, 2),
+    ("900_ele.msh", 5, 3, 3, 4, 2), ("irregular.msh", 6, 2, 3, 3, 1)])
+def test_face_wavefront_call_equals_per_sweep_launches(mesh, S, L, solver, ns, n, monkeypatch):
+    """The wavefront form of a smoother call (k_face_wave: un_eles claimed in reverse Cuthill-McKee
+    ticket order, each sweep started once the neighbours have published their words, the iterate in
+    LDS across the call) leaves the state of one launch per sweep, bit for bit -- on levels of 256,
+    1,024 and 4,096 sub-elements per un_ele, with far more un_eles than co-resident workgroups
+    (untitled8192 at S = 5: 8,192 level-1 un_eles over 512 workgroups), red-black and Jacobi."""
+    import pamg
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+
+    def run():
+        g = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, op=1)
+        g.begin_timestep()
+        g.vcycle(n)
+        g.begin_timestep()
+        g.vcycle(1)
+        st, ov = g.state(), g.overlap()
+        g.close()
+        return st, ov
+
+    monkeypatch.setenv("PAMG_FACE_WAVE", "0")
+    monkeypatch.setenv("PAMG_FACE_CHAIN", "0")
+    rs, rov = run()
+    monkeypatch.setenv("PAMG_FACE_WAVE", "1")
+    monkeypatch.setenv("PAMG_FACE_CHAIN", "1")
+    gs, gov = run()
+    assert_identical(gs, rs)
+    for x, y in zip(gov, rov):
+        np.testing.assert_array_equal(x, y)
