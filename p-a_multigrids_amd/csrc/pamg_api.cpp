@@ -515,8 +515,11 @@ int face_wave_setup(pamg_handle *h) {
     int band = 0;
     rcm_order(h->neig_local, h->U, order, band);
     CHK(dev_upload(h, &h->wave_order, order));
-    CHK(dev_upload(h, &h->wave_neig, h->neig_local));
     CHK(dev_alloc(h, &h->wave_flags, (size_t)h->U + 16));
+    const size_t ng = (size_t)h->slots * 3 * std::max(h->U, 1) * 2;   // words per granule buffer
+    CHK(dev_alloc(h, &h->wave_gran, 2 * ng));
+    HIPCHK(h, hipMemsetAsync(h->wave_gran, 0, 2 * ng * sizeof(unsigned long long), h->stream));
+    h->wave_tag = 1;
     if (!h->chain_tmo) {
         CHK(dev_alloc(h, &h->chain_tmo, 4));
         HIPCHK(h, hipMemsetAsync(h->chain_tmo, 0, 4 * sizeof(unsigned), h->stream));
@@ -525,11 +528,13 @@ int face_wave_setup(pamg_handle *h) {
     return PAMG_OK;
 }
 
-// the wavefront form for a call of `run` executed sweeps on level l (PAMG_FACE_WAVE=0: off):
-// returns its grid, 0 when the level's shape or the residency bound rules it out
+// the wavefront form for a call of `run` executed sweeps on level l, opt-in (PAMG_FACE_WAVE=1): it
+// is exact at any occupancy (tagged granules) but measured slower than one launch per sweep on the
+// bench mesh (profiles/r03_f_face_forms.txt: its hand-offs wait on memory latency, ~40 us per
+// ticket). Returns its grid, 0 when off or when the level's shape or the residency bound rules it out
 int face_wave_grid_for(pamg_handle *h, int l, int run) {
     const char *ev = getenv("PAMG_FACE_WAVE");   // read per call: tests switch it within a process
-    if ((ev && atoi(ev) == 0) || run < 2 || h->nranks != 1 || h->comm || h->neig_local.empty() || !face_wave_shape(h->lv[l])) return 0;
+    if (!ev || atoi(ev) == 0 || run < 2 || h->nranks != 1 || h->comm || h->neig_local.empty() || !face_wave_shape(h->lv[l])) return 0;
     if (!h->cus) {
         int n = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || n <= 0) n = 1;
@@ -581,6 +586,23 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         return PAMG_OK;
     }
     HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
+    // the tagged halo granules of an in-launch call (chain or wavefront): sweep s of this call carries
+    // tag wave_tag + s; the base then moves past the call's tags, so no granule is ever accepted twice
+    auto tags = [&](unsigned long long **g0, unsigned long long **g1, unsigned *tag0) -> int {
+        CHK(face_wave_setup(h));
+        const size_t ng = (size_t)h->slots * 3 * std::max(h->U, 1) * 2;
+        if ((unsigned long long)h->wave_tag + sweeps + 1 >= 0xffffffffull) {   // tags would wrap: start over
+            HIPCHK(h, hipMemsetAsync(h->wave_gran, 0, 2 * ng * sizeof(unsigned long long), h->stream));
+            h->wave_tag = 1;
+        }
+        *g0 = h->wave_gran;
+        *g1 = h->wave_gran + ng;
+        *tag0 = h->wave_tag;
+        h->wave_tag += (unsigned)sweeps + 1;
+        return PAMG_OK;
+    };
+    unsigned long long *g0 = nullptr, *g1 = nullptr;
+    unsigned tag0 = 0;
     if (run >= 2 && face_chain_ok(h, l)) {   // the whole call in one launch
         CHK(face_chain_setup(h, l));
         HIPCHK(h, hipMemsetAsync(L.chain_flags, 0, L.chain_flag_bytes, h->stream));
@@ -592,11 +614,12 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         return PAMG_OK;
     }
     if (const int g = face_wave_grid_for(h, l, run)) {   // the call in one wavefront launch
+        CHK(tags(&g0, &g1, &tag0));
         // the state crosses HBM once per call, as the chain's
         Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
-        HIPCHK(h, launch_face_wave(h->stream, L, h->U, g, h->tov, h->tov_b, h->tovo, h->wave_flags, h->wave_order,
-                                   h->wave_neig, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3, l == 1,
-                                   rdt, h->slots));
+        HIPCHK(h, launch_face_wave(h->stream, L, h->U, g, h->tov, h->tov_b, h->tovo, g0, g1, tag0, h->wave_flags,
+                                   h->wave_order, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
+                                   l == 1, rdt, h->slots));
         return PAMG_OK;
     }
     for (int s = 0; s < run; ++s) {
@@ -1244,9 +1267,10 @@ void free_levels(pamg_handle *h) {
     }
     dev_free(h->geo1); dev_free(h->tov); dev_free(h->tovo); dev_free(h->tov_b);
     h->geo1 = h->tov = h->tovo = h->tov_b = nullptr;
-    dev_free(h->wave_order); dev_free(h->wave_neig); dev_free(h->wave_flags);
+    dev_free(h->wave_order); dev_free(h->wave_neig); dev_free(h->wave_flags); dev_free(h->wave_gran);
     h->wave_order = h->wave_neig = nullptr;
     h->wave_flags = nullptr;
+    h->wave_gran = nullptr;
     h->wave_band = -1;
     h->mesh_ready = false;
 }
@@ -1424,7 +1448,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
     for (size_t q = 0; q < h->owned.size(); ++q)
         for (int c = 0; c < 6; ++c) h->Xo[6 * q + c] = X[6 * (size_t)h->owned[q] + c];
     h->neig_local.clear();
-    if (h->p.op == 1) {   // the face chain's workgroup neighbour lists (face_chain_setup)
+    if (h->p.op == 1) {   // the local neighbours: the chain's workgroup lists, the wavefront's ticket order
         std::vector<int> g2l(U, -1);
         for (size_t q = 0; q < h->owned.size(); ++q) g2l[h->owned[q]] = (int)q;
         h->neig_local.assign(3 * h->owned.size(), -1);

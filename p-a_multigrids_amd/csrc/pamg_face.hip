@@ -484,6 +484,87 @@ __device__ __forceinline__ void items_pass(const Items<K> &I, const XIN &xin, co
     }
 }
 
+// Tagged halo granules (cdna_hip_programming.md 6 Guideline 16, R2: the data is the flag). A halo
+// double d of sweep s travels as two 8-byte words {lo32(d), tag}, {hi32(d), tag}, each one aligned
+// agent-scope atomic store (single-copy atomic), tag = the launch's tag base + s. A reader re-reads
+// both words (agent-scope atomic loads) until both carry the tag it expects, then has the exact
+// double: no flag, no drain, no fence, any number of workgroups per CU, and a tear between the two
+// words is caught by the tags. Granule buffers alternate by sweep parity as the snapshot buffers.
+typedef unsigned long long u64_t;
+__device__ __forceinline__ void st_gran(u64_t *g, double d, unsigned tag) {
+    const u64_t b = (u64_t)__double_as_longlong(d);
+    __hip_atomic_store((g_u64 *)g, (b & 0xffffffffull) | ((u64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((g_u64 *)(g + 1), (b >> 32) | ((u64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// poll up to B granules at once (gi[b] < 0: none) into LDS (HI[li[b]]): every pending granule's two
+// words are requested together, so a round trip serves all of them; only the ones whose tags did not
+// match yet are re-read (bounded: *tmo set after 2^22 rounds)
+template <int B>
+__device__ __forceinline__ void gran_poll(const u64_t *gin, unsigned tag, const int64_t (&gi)[B], const int (&li)[B],
+                                          double *HI, unsigned *tmo) {
+    bool need[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) need[b] = gi[b] >= 0;
+    for (unsigned spins = 0;; ++spins) {
+        u64_t x[B], y[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (need[b]) {
+                x[b] = __hip_atomic_load((g_u64 *)const_cast<u64_t *>(gin + 2 * gi[b]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                y[b] = __hip_atomic_load((g_u64 *)const_cast<u64_t *>(gin + 2 * gi[b] + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        bool more = false;
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (need[b]) {
+                if ((unsigned)(x[b] >> 32) == tag && (unsigned)(y[b] >> 32) == tag) {
+                    HI[li[b]] = __longlong_as_double((long long)((x[b] & 0xffffffffull) | (y[b] << 32)));
+                    need[b] = false;
+                } else {
+                    more = true;
+                }
+            }
+        if (!more) return;
+        if (spins > (1u << 22)) {
+            __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// the next sweep's halo words of one sub-element as granules (update_overlaps, :555; halo_words'
+// destinations): a neighbour on this rank gets the granules of sweep `tag`, and, when fin, the plain
+// t_overlap word as well (the state the call leaves); the domain-boundary words (constant in a time
+// step) go plain into the snapshot buffer, at the call's first sweep (bc)
+__device__ __forceinline__ void halo_gran(const HaloArgs &H, const int4 rec[3], int h, const double t[3], bool bc,
+                                          u64_t *gout, unsigned tag, bool fin) {
+    const int pos[3] = {h & 1023, (h >> 10) & 1023, h >> 20};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        const int i = pos[f];
+        if (!i) continue;
+        const int4 r = rec[f];
+        const int mode = r.x & 3;
+        if (mode == 0) {
+            if (!bc) continue;
+            const int a = (i - 1) * 3 + (f == 2 ? 1 : 0);
+            const int b = (i - 1) * 3 + (f == 1 ? 1 : 2);
+            const double2 v = H.bcv[r.z + i - 1];
+            H.tov[r.y + a] = v.x;
+            H.tov[r.y + b] = v.y;
+        } else if (mode == 1) {
+            const int k = (r.x >> 2) ? (H.m - i + 1) : i;
+            const int64_t d = r.y + (int64_t)(k - 1) * 3;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                if (gout) st_gran(gout + 2 * (d + c), t[c], tag);
+                if (fin) H.tov[d + c] = t[c];
+            }
+        }
+    }
+}
+
 constexpr int kWaveStampT = 32, kWaveStampW = 19;   // tickets per workgroup, stamps per ticket
 #ifndef PAMG_WAVE_WAVES
 #define PAMG_WAVE_WAVES 4
@@ -499,8 +580,8 @@ template <int TS, int NT, bool RB>
 __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_wave(
     double *T, double *TNN, const double *__restrict__ RHS, const double *__restrict__ stc,
     const int4 *__restrict__ fnb, const double *__restrict__ fface, const int *__restrict__ fsx,
-    const int *__restrict__ cpos, int nup, double *buf0, double *buf1, HaloArgs H, unsigned *flags,
-    const int *__restrict__ order, const int *__restrict__ neig, unsigned *tmo, int U, int run, int total,
+    const int *__restrict__ cpos, int nup, double *buf0, double *buf1, u64_t *g0, u64_t *g1, unsigned tag0,
+    HaloArgs H, unsigned *flags, const int *__restrict__ order, unsigned *tmo, int U, int run, int total,
     int store, int64_t pitch, int slots, int level1, double rdt, long long *stamps) {
     using WS = WaveShape<TS, NT, RB>;
     constexpr int PER = TS / NT, M = WS::M, NH = 9 * M, KU = WS::KU, KD = WS::KD;
@@ -568,8 +649,9 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
         for (int k = 0; k < KD; ++k)
 #pragma unroll
             for (int c = 0; c < 3; ++c) IB.b[k][c] = IB.j[k] < 0 ? 0.0 : RHS[c * pitch + s0 + IB.j[k]];
-        int nv = -1;   // lanes 0..2 of wave 0 poll the neighbours' flags
-        if (t < 3) nv = neig[3 * u + t];
+        // which of the un_ele's faces have a neighbour on this rank (their words arrive as granules;
+        // a domain-boundary face's words are constant and come with the sweep-0 snapshot)
+        const int nbm = ((hf[0].x & 3) == 1) | (((hf[1].x & 3) == 1) << 1) | (((hf[2].x & 3) == 1) << 2);
         if (st) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             st[1] = wall_clock64();
@@ -580,37 +662,51 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
         for (int sw = 0; sw < run; ++sw) {
             const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
             double *tout = sw + 1 < total ? (((total - 2 - sw) & 1) ? buf1 : buf0) : nullptr;
-            // the items' positions and neighbour entries opaque per sweep: the LDS addresses derived
-            // from them are recomputed in each sweep instead of hoisted out of the loop (VGPRs)
+            // the items' positions and neighbour entries re-read in every sweep (small tables, cache
+            // hits) behind an opaque index, so that they and the LDS addresses derived from them are
+            // not held in registers across the sweep loop (VGPRs: occupancy)
 #pragma unroll
-            for (int k = 0; k < KU; ++k) asm volatile("" : "+v"(IA.j[k]), "+v"(IA.nb[k].x), "+v"(IA.nb[k].y), "+v"(IA.nb[k].z), "+v"(IA.nb[k].w));
-#pragma unroll
-            for (int k = 0; k < KD; ++k) asm volatile("" : "+v"(IB.j[k]), "+v"(IB.nb[k].x), "+v"(IB.nb[k].y), "+v"(IB.nb[k].z), "+v"(IB.nb[k].w));
-            if (sw > 0 && t < 64) {   // the neighbours' words of this sweep
-                bool ok = nv < 0;
-                for (unsigned spins = 0;; ++spins) {
-                    if (!ok)
-                        ok = __hip_atomic_load((g_u32 *)(flags + nv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                             (unsigned)sw;
-                    if (__all(ok)) break;
-                    if (spins > (1u << 22)) {
-                        if (t == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
+            for (int k = 0; k < KU; ++k) {
+                int i = t + NT * k;
+                asm volatile("" : "+v"(i));
+                IA.j[k] = RB ? (i < nup ? cpos[i] : -1) : i;
+                IA.nb[k] = fnb[IA.j[k] < 0 ? 0 : IA.j[k]];
             }
-            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KD; ++k) {
+                int i = t + NT * k;
+                asm volatile("" : "+v"(i));
+                IB.j[k] = RB && i < TS - nup ? cpos[nup + i] : -1;
+                IB.nb[k] = fnb[IB.j[k] < 0 ? 0 : IB.j[k]];
+            }
             const int sk = 2 + 4 * (sw < 4 ? sw : 3);
             if (st) st[sk] = wall_clock64();
-            for (int i = t; i < NH; i += NT) HI[i] = ld_coh(tin + u * slots * 3 + (int64_t)(i / (3 * M)) * slots + i % (3 * M));
-            __syncthreads();
-            if (st) st[sk + 1] = wall_clock64();
-            if (store == 1 && sw + 1 == run)   // the call's last sweep: tnew := tnew_nonlin (:550)
+            if (sw == 0) {   // the call's snapshot of sweep 0 (the preceding halo launch wrote it)
+                for (int i = t; i < NH; i += NT) HI[i] = tin[u * slots * 3 + (int64_t)(i / (3 * M)) * slots + i % (3 * M)];
+            } else {         // the neighbours' granules of sweep sw, polled until every tag matches
+                constexpr int QB = (NH + NT - 1) / NT;   // the thread's snapshot words, polled together
+                int64_t gi[QB];
+                int li[QB];
+#pragma unroll
+                for (int q = 0; q < QB; ++q) {
+                    const int i = t + NT * q, f = i / (3 * M);
+                    li[q] = i;
+                    gi[q] = i < NH && ((nbm >> f) & 1) ? u * slots * 3 + (int64_t)f * slots + i % (3 * M) : -1;
+                }
+                gran_poll<QB>((sw & 1) ? g1 : g0, tag0 + (unsigned)sw, gi, li, HI, tmo);
+            }
+            // the call's last sweep: tnew := tnew_nonlin (:550), before the barrier that lets the passes
+            // rewrite X (a position's item may belong to another thread)
+            if (store == 1 && sw + 1 == run) {
+                int tt = t;   // opaque: the store addresses are not held across the sweep loop
+                asm volatile("" : "+v"(tt));
 #pragma unroll
                 for (int k = 0; k < PER; ++k)
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) T[c * pitch + s0 + t + NT * k] = X[c][t + NT * k];
+                    for (int c = 0; c < 3; ++c) T[c * pitch + s0 + tt + NT * k] = X[c][tt + NT * k];
+            }
+            __syncthreads();
+            if (st) st[sk + 1] = wall_clock64();
             if constexpr (RB) {   // up sub-elements, then down ones, in place (a colour reads only the other)
                 items_pass<0>(IA, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
 #pragma unroll
@@ -635,9 +731,14 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
             }
             __syncthreads();
             if (st) st[sk + 2] = wall_clock64();
-            if (tout) {   // the next sweep's halo words (:550, :555 of sweep sw + 1), written through
+            if (tout) {   // the next sweep's halo words (:550, :555 of sweep sw + 1) as granules
                 HaloArgs Hn = H;
                 Hn.tov = tout;
+                u64_t *gout = ((sw + 1) & 1) ? g1 : g0;
+                const unsigned tag = tag0 + (unsigned)(sw + 1);
+                const bool fin = sw + 2 == total;   // the words t_overlap keeps after the call
+                // granules only for a sweep this call runs (a dead last sweep has no reader)
+                if (sw + 1 >= run) gout = nullptr;
 #pragma unroll
                 for (int q = 0; q < PER; ++q) {
                     // opaque per sweep: the destinations are recomputed here instead of hoisted
@@ -647,11 +748,8 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
                     if (!hq) continue;
                     const int j = 2 * (t + NT * (q / 2)) + (q & 1);
                     const double tv[3] = {X[0][j], X[1][j], X[2][j]};
-                    halo_words<true>(Hn, hf, hq, tv, sw == 0);
+                    halo_gran(Hn, hf, hq, tv, sw == 0, gout, tag, fin);
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (t == 0) __hip_atomic_store((g_u32 *)flags + u, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (st) st[sk + 3] = wall_clock64();
         }
@@ -844,9 +942,9 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
             HI[idx] = ld_coh(tin + (u0 + uk) * slots * 3 + (int64_t)mf * slots + off);
         }
-        __syncthreads();
-        stamp(1);
-        if (store == 1 && sw + 1 == run)   // the call's last sweep: tnew := tnew_nonlin (:550)
+        // the call's last sweep: tnew := tnew_nonlin (:550), before the barrier that lets the passes
+        // rewrite X (with item lists a position's item may belong to another thread)
+        if (store == 1 && sw + 1 == run)
 #pragma unroll
             for (int k = 0; k < PER; ++k) {
                 const int j = t + NT * k;
@@ -854,6 +952,8 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 #pragma unroll
                     for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = X[c][j];
             }
+        __syncthreads();
+        stamp(1);
         if constexpr (LREC) {
 #pragma unroll
             for (int k = 0; k < KU; ++k) asm volatile("" : "+v"(IA.j[k]), "+v"(IA.nb[k].x), "+v"(IA.nb[k].y), "+v"(IA.nb[k].z), "+v"(IA.nb[k].w));
@@ -1105,8 +1205,8 @@ namespace {
 const void *face_wave_fn(int nsub, bool rb, int *nt) {
     switch (nsub) {
         case 4096: *nt = 1024; return rb ? (const void *)k_face_wave<4096, 1024, true> : (const void *)k_face_wave<4096, 1024, false>;
-        case 1024: *nt = 512; return rb ? (const void *)k_face_wave<1024, 512, true> : (const void *)k_face_wave<1024, 512, false>;
-        case 256: *nt = 128; return rb ? (const void *)k_face_wave<256, 128, true> : (const void *)k_face_wave<256, 128, false>;
+        case 1024: *nt = 256; return rb ? (const void *)k_face_wave<1024, 256, true> : (const void *)k_face_wave<1024, 256, false>;
+        case 256: *nt = 64; return rb ? (const void *)k_face_wave<256, 64, true> : (const void *)k_face_wave<256, 64, false>;
         default: *nt = 0; return nullptr;
     }
 }
@@ -1121,8 +1221,9 @@ int face_wave_grid(const Level &L, bool rb, int cus) {
 }
 
 hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, double *tov, double *tov_b, double *tovo,
-                            unsigned *flags, const int *order, const int *neig, unsigned *tmo, int run, int total,
-                            int store, bool rb, bool level1, double rdt, int slots) {
+                            unsigned long long *g0, unsigned long long *g1, unsigned tag0, unsigned *flags,
+                            const int *order, unsigned *tmo, int run, int total, int store, bool rb, bool level1,
+                            double rdt, int slots) {
     if (L.N == 0 || run <= 0) return hipSuccess;
     int nt = 0;
     const void *f = face_wave_fn(L.nsub, rb, &nt);
@@ -1150,8 +1251,8 @@ hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, doub
     const int g = std::min(grid, U);
     const int *cpos = L.cpos;
     int nup = L.nup;
-    void *args[] = {&T, &TNN, &RHS, &stc, &fnb, &fface, &fsx, &cpos, &nup, &tov, &tov_b, &H, &flags, &order, &neig,
-                    &tmo, &U, &run, &total, &store, &pitch, &slots, &l1, &rdt, &stamps};
+    void *args[] = {&T, &TNN, &RHS, &stc, &fnb, &fface, &fsx, &cpos, &nup, &tov, &tov_b, &g0, &g1, &tag0, &H, &flags,
+                    &order, &tmo, &U, &run, &total, &store, &pitch, &slots, &l1, &rdt, &stamps};
     e = hipLaunchCooperativeKernel(f, dim3(g), dim3(nt), args, 0, s);
     if (stamp_path) {
         std::vector<long long> hs(nst);

@@ -203,6 +203,8 @@ struct pamg_handle {
     int *wave_order = nullptr, *wave_neig = nullptr;
     unsigned *wave_flags = nullptr;
     int wave_band = -1;
+    unsigned long long *wave_gran = nullptr;   // two granule buffers, 2 words per t_overlap double each
+    unsigned wave_tag = 1;                     // tag base of the next wavefront launch
     // the resident call's per-cycle exchange (halo_exchange = 1): per-cycle workgroup counters and
     // the signal the comm stream waits on (cycles published so far: xc_sig_base after the last call)
     unsigned *xc_done = nullptr;
@@ -337,12 +339,15 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
 bool face_chain_fits(int nsub, int U, int cus);
 // the wavefront form of one smoother call (k_face_wave, levels of 256 / 1,024 / 4,096 sub-elements
 // per un_ele): un_eles claimed in the ticket order `order`, flags = U per-un_ele words + the ticket
-// counter (zeroed here), neig = 3 local neighbours per un_ele (-1 none); grid = co-resident workgroups
+// counter (zeroed here); g0 / g1 the tagged halo granules of odd / even sweeps (2 words per t_overlap
+// double), tag0 + s the tag of sweep s (never reused: the host advances it past every launch's tags);
+// grid = co-resident workgroups
 bool face_wave_shape(const Level &L);
 int face_wave_grid(const Level &L, bool rb, int cus);
 hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, double *tov, double *tov_b, double *tovo,
-                            unsigned *flags, const int *order, const int *neig, unsigned *tmo, int run, int total,
-                            int store, bool rb, bool level1, double rdt, int slots);
+                            unsigned long long *g0, unsigned long long *g1, unsigned tag0, unsigned *flags,
+                            const int *order, unsigned *tmo, int run, int total, int store, bool rb, bool level1,
+                            double rdt, int slots);
 int face_chain_per_wg(int nsub, int U, int cus);
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,

@@ -345,7 +345,8 @@ __device__ __forceinline__ void hs_write(bool uni, const HaloArgs &H, uint32_t u
 }
 
 // the tnew words of one sub-element's remote halo entries (mode 2) into a ring buffer of 3 words
-// per entry (the per-cycle exchange of the resident call)
+// per entry (the per-cycle exchange of the resident call), written through (sc1: the hand-off form
+// of cdna_hip_programming.md 6 Guideline 16 R1, no release fence)
 __device__ __forceinline__ void hs_ring(bool uni, const HaloArgs &H, double *ring, uint32_t u, int h,
                                         const double t[3]) {
     if (h == 0) return;
@@ -358,16 +359,18 @@ __device__ __forceinline__ void hs_ring(bool uni, const HaloArgs &H, double *rin
         if ((r.x & 3) != 2) continue;
         double *o = ring + 3 * (int64_t)(r.z + pos[f] - 1);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) o[c] = t[c];
+        for (int c = 0; c < 3; ++c) st_coh(o + c, t[c]);
     }
 }
 
-// a workgroup's end of cycle c (after the barrier that follows every wave's drained ring stores):
-// count it; the workgroup that completes the cycle publishes it to the comm stream's signal
-// (release: the ring words are written back from this XCD's L2 before the count is seen)
+// a workgroup's end of cycle c (after the barrier that follows every wave's drained write-through
+// ring stores): count it with a relaxed agent-scope add; the workgroup whose add completes the cycle
+// publishes it to the comm stream's signal. The ring words are already at the coherence point (sc1,
+// drained), so neither add needs a fence: an acq_rel add here cost a buffer_wbl2 + buffer_inv per
+// workgroup and cycle (halo_exchange = 1 ran at 0.39 of the plain call, profiles/r03_a_mp_detached_*)
 __device__ __forceinline__ void xc_signal(const VArgs &A, int c) {
-    const unsigned old = __hip_atomic_fetch_add(A.xc_done + c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == A.xc_grid) __hip_atomic_fetch_add(A.xc_sig, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned old = __hip_atomic_fetch_add(A.xc_done + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == A.xc_grid) __hip_atomic_fetch_add(A.xc_sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the words of one sub-element that are constant within a time step (k_overlap_static's, from
@@ -1657,14 +1660,14 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     } else if (part >= 4 && part <= 6) {   // the resident call (5: starting a time step; 6: exchange every cycle)
         if constexpr (PAMG_RES_BALANCED && S >= 5 && L >= 3) {
             if (part == 6)
-                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false, true>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
-                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false, true>), dim3(grid), dim3(512), 0, s, A,
+                                   A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
             else if (part == 5)
                 hipLaunchKernelGGL((k_vc_resb<S, L, ST, true>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
                                    A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
             else
-                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
-                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false>), dim3(grid), dim3(512), 0, s, A,
+                                   A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         } else if constexpr (L >= 2 && fine_np(S) == 2) {
             if (part == 6)
                 hipLaunchKernelGGL((k_vc_res<S, L, ST, false, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A,
