@@ -332,6 +332,48 @@ __device__ __forceinline__ void halo_words(const HaloArgs &H, const int4 rec[3],
     }
 }
 
+// A thread's sub-elements in the passes ("items", fixed for the whole call): red-black runs each
+// colour over its own position list (Level::cpos), so every lane of a pass has a sub-element of that
+// colour (one launch per sweep masked half the lanes of each colour pass: twice the fp64 issue);
+// Jacobi takes the positions in order. j = storage position in the tile, -1 none; nb its fnb entry,
+// b its RHS.
+template <int K>
+struct Items {
+    int j[K];
+    int4 nb[K];
+    double b[K][3];
+};
+
+// one pass (MODE 0 / 1 a colour, 2 Jacobi) of a tile's items (j: tile positions); rec(j, nb, f) calls
+// f with the item's un_ele record, un_ele, omega / D row and the un_ele's first tile position; xin reads
+// the tile; the rest as face_apply. out(k, r): the item's result --
+// stored in place at once by a colour pass (a colour reads only the other colour), held by Jacobi
+template <int MODE, int K, class XIN, class HV, class REC, class OUT>
+__device__ __forceinline__ void items_pass(const Items<K> &I, const XIN &xin, const HV &hv, const REC &rec, int level1,
+                                           double rdt, const OUT &out) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int j = I.j[k];
+        if (j < 0) continue;
+        double x[3], r[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c] = xin(c, j);
+        rec(j, I.nb[k], [&](const FaceRec &R, int64_t u, const double *wd, int jb) {
+            auto xb = [&](int c, int q) { return xin(c, jb + q); };   // un_ele-relative neighbour positions
+            face_apply<MODE>(R, xb, x, I.b[k], I.nb[k], u, hv, [&](int i) { return wd[i]; }, level1, rdt, r);
+        });
+        out(k, r);
+        asm volatile("" ::: "memory");   // one item at a time: its record's registers are not held across items
+    }
+}
+
+template <int TS, int NT, bool RB>
+struct WaveShape {
+    static constexpr int M = TS == 256 ? 16 : TS == 1024 ? 32 : 64;
+    static constexpr int NUP = M * (M + 1) / 2, NDN = M * (M - 1) / 2;   // up / down sub-elements
+    static constexpr int KU = RB ? (NUP + NT - 1) / NT : TS / NT, KD = RB ? (NDN + NT - 1) / NT : 1;
+};
+
 // ---- one sweep on a tile that is exactly one un_ele (nsub = TS: levels of 256, 1,024 or 4,096
 // sub-elements per un_ele): k_face_sweep's sweep with every input the passes read issued at the
 // start, side by side with the iterate's and RHS's streams -- the un_ele's operator record (scalar
@@ -339,7 +381,9 @@ __device__ __forceinline__ void halo_words(const HaloArgs &H, const int4 rec[3],
 // halo pairs -- so a tile waits on memory once (k_face_sweep waited on the record, the selector and
 // the snapshot word in turn inside each colour pass, then on the halo metadata: SQ 79 % of the waves'
 // cycles waiting, r03_b_face_sq.txt). The next sweep's halo words are halo_words' (no told reads).
-// Same face_apply arithmetic per sub-element: bitwise k_face_sweep's.
+// Same face_apply arithmetic per sub-element: bitwise k_face_sweep's. (Colour item lists, as in the
+// chain, made this HBM-bound sweep slower: 0.91 -> 0.98-1.00 ms of level-1 sweeps per cycle with the
+// RHS gathered by colour position from memory or through LDS, profiles/r03_f_face_forms.txt.)
 template <int TS, int NT, bool RB>
 __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_tile(
     double *T, double *TNN, const double *__restrict__ RHS, const double *__restrict__ stc,
@@ -449,41 +493,6 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 // [t0, t0 + G - k b) can always reach sweep k -- so G >= (run - 1) b + 1 (face_wave_ok) guarantees
 // the grid drains; the spins are bounded anyway (*tmo, as the chain). Every sub-element's arithmetic
 // is face_apply's on the same snapshot words, so the result is bitwise the per-sweep launches'.
-// A thread's sub-elements in the passes ("items", fixed for the whole call): red-black runs each
-// colour over its own position list (Level::cpos), so every lane of a pass has a sub-element of that
-// colour (one launch per sweep masked half the lanes of each colour pass: twice the fp64 issue);
-// Jacobi takes the positions in order. j = storage position in the tile, -1 none; nb its fnb entry,
-// b its RHS.
-template <int K>
-struct Items {
-    int j[K];
-    int4 nb[K];
-    double b[K][3];
-};
-
-// one pass (MODE 0 / 1 a colour, 2 Jacobi) of a tile's items (j: tile positions); rec(j, nb, f) calls
-// f with the item's un_ele record, un_ele, omega / D row and the un_ele's first tile position; xin reads
-// the tile; the rest as face_apply. out(k, r): the item's result --
-// stored in place at once by a colour pass (a colour reads only the other colour), held by Jacobi
-template <int MODE, int K, class XIN, class HV, class REC, class OUT>
-__device__ __forceinline__ void items_pass(const Items<K> &I, const XIN &xin, const HV &hv, const REC &rec, int level1,
-                                           double rdt, const OUT &out) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int j = I.j[k];
-        if (j < 0) continue;
-        double x[3], r[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) x[c] = xin(c, j);
-        rec(j, I.nb[k], [&](const FaceRec &R, int64_t u, const double *wd, int jb) {
-            auto xb = [&](int c, int q) { return xin(c, jb + q); };   // un_ele-relative neighbour positions
-            face_apply<MODE>(R, xb, x, I.b[k], I.nb[k], u, hv, [&](int i) { return wd[i]; }, level1, rdt, r);
-        });
-        out(k, r);
-        asm volatile("" ::: "memory");   // one item at a time: its record's registers are not held across items
-    }
-}
-
 // Tagged halo granules (cdna_hip_programming.md 6 Guideline 16, R2: the data is the flag). A halo
 // double d of sweep s travels as two 8-byte words {lo32(d), tag}, {hi32(d), tag}, each one aligned
 // agent-scope atomic store (single-copy atomic), tag = the launch's tag base + s. A reader re-reads
@@ -569,12 +578,6 @@ constexpr int kWaveStampT = 32, kWaveStampW = 19;   // tickets per workgroup, st
 #ifndef PAMG_WAVE_WAVES
 #define PAMG_WAVE_WAVES 4
 #endif
-template <int TS, int NT, bool RB>
-struct WaveShape {
-    static constexpr int M = TS == 256 ? 16 : TS == 1024 ? 32 : 64;
-    static constexpr int NUP = M * (M + 1) / 2, NDN = M * (M - 1) / 2;   // up / down sub-elements
-    static constexpr int KU = RB ? (NUP + NT - 1) / NT : TS / NT, KD = RB ? (NDN + NT - 1) / NT : 1;
-};
 
 template <int TS, int NT, bool RB>
 __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_wave(

@@ -373,6 +373,20 @@ __device__ __forceinline__ void xc_signal(const VArgs &A, int c) {
     if (old + 1 == A.xc_grid) __hip_atomic_fetch_add(A.xc_sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// XC: does tile tb (T level-1 sub-elements from tb T) hold a face whose neighbour is on another rank?
+// Only such a tile stores ring words, so only its waves drain them before the cycle's count (an
+// x-strip rank of untitled8192 at N = 2: 64 of 4,096 tiles); the others count without waiting
+template <int S, int T>
+__device__ __forceinline__ bool tile_remote(const VArgs &A, int64_t tb) {
+    int64_t u0 = (tb * T) >> (2 * S), u1 = ((tb + 1) * T - 1) >> (2 * S);
+    if (u1 >= A.U) u1 = A.U - 1;
+    bool r = false;
+    for (int64_t u = u0; u <= u1; ++u)
+#pragma unroll
+        for (int f = 0; f < 3; ++f) r |= (A.lv[0].H.hface[3 * u + f].x & 3) == 2;
+    return r;
+}
+
 // the words of one sub-element that are constant within a time step (k_overlap_static's, from
 // its told `to`): t_overlap_old of the neighbour, the boundary values of both arrays, the told
 // half of a send entry -- into both send buffers -- and the compact told copy of the halo
@@ -1034,6 +1048,7 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
     const double rdt = A.rdt;
     const int ns = A.n_smooth, m = A.cycles;
     const int64_t tb = (int64_t)blockIdx.x + A.tile0;   // tile
+    const bool xr = XC && tile_remote<S, T>(A, tb);
     const VLevel &V0 = A.lv[0];
     const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo, keepc = A.keep & kKeepCoarse;
     bool v0;
@@ -1190,7 +1205,7 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             if (keep1) store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
         }
         if constexpr (XC && !last)   // the cycle's remote halo words, exchanged while the next cycles run
-            if (v0) {
+            if (xr && v0) {
 #pragma unroll
                 for (int k = 0; k < NP; ++k) hs_ring(G::uni(0), V0.H, A.ring + c * A.ring_stride, w0, h0[k], p0[k]);
             }
@@ -1214,7 +1229,8 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
             copy3(xs, p);
             if (last && vc) store3(V.T(), V.pitch, gxc, xs);
         });
-        if constexpr (XC && !last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring words drained
+        if constexpr (XC && !last)
+            if (xr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring words drained
         __syncthreads();
         if constexpr (XC && !last)
             if (t == 0) xc_signal(A, c);
@@ -1302,6 +1318,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     const double rdt = A.rdt;
     const int ns = A.n_smooth, m = A.cycles;
     const int64_t tb = (int64_t)blockIdx.x + A.tile0;
+    const bool xr = XC && tile_remote<S, T>(A, tb);
     const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo, keepc = A.keep & kKeepCoarse;
     const int total = A.steps * m;
     // the restrictor (:336): the RHS of coarse sub-element i of level l from the means of its
@@ -1589,14 +1606,15 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
                 }
                 if constexpr (XC && !last) {   // the cycle's remote halo words, exchanged while the next cycles run
                     double *rg = A.ring + c * A.ring_stride;
-                    if (vp)
+                    if (xr && vp)
 #pragma unroll
                         for (int k = 0; k < 2; ++k) hs_ring(true, V0.H, rg, w0, hs_pack(V0.H.hsub[(sp + k) & hmask]), X0[k]);
                     if constexpr (N == 3)
-                        if (vq) hs_ring(true, V0.H, rg, w0, hs_pack(V0.H.hsub[sq & hmask]), X0[2]);
+                        if (xr && vq) hs_ring(true, V0.H, rg, w0, hs_pack(V0.H.hsub[sq & hmask]), X0[2]);
                 }
                 if constexpr (N == 2) l2_legs(std::integral_constant<int, 1>{}, lastc, c, gb, xs, bs, gc, vc);
-                if constexpr (XC && !last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring words drained
+                if constexpr (XC && !last)
+                    if (xr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring words drained
                 __syncthreads();
                 if constexpr (N == 2 && last) l2_rhsn(std::integral_constant<int, 1>{}, c, gb, gc, vc);
             };
