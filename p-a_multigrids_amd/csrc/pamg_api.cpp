@@ -577,15 +577,20 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
     h->overlap_static_l1 = false;
     const double rdt = 1 / h->p.dt;
     const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
-    if (src_is_T) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
+    // src_is_T (the leg copy tnew_nonlin := tnew, :327 / :348 / :367): no copy launch. The call's first
+    // sweep reads its iterate from tnew, which already holds what :550 would copy into it, and writes
+    // tnew_nonlin for every sub-element; the halo refresh then only writes the words (it reads just the
+    // sub-elements that have words). A dead-last call of one executed sweep (store 2) leaves
+    // tnew_nonlin unwritten: the cycle overwrites it unread, as it does the dead sweep's.
     if (!h->tov_b) CHK(dev_alloc(h, &h->tov_b, (size_t)h->slots * 3 * std::max(h->U, 1)));
     double *buf[2] = {h->tov, h->tov_b};
     const int run = dead_last ? sweeps - 1 : sweeps;   // the sweeps that are executed
     if (run <= 0) {   // a call of one dead sweep: tnew := tnew_nonlin and its :555 words
-        if (sweeps > 0) HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, true));
+        if (src_is_T && !dead_last) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
+        if (sweeps > 0) HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, !src_is_T));
         return PAMG_OK;
     }
-    HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
+    HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, !src_is_T));   // :550, :555
     // the tagged halo granules of an in-launch call (chain or wavefront): sweep s of this call carries
     // tag wave_tag + s; the base then moves past the call's tags, so no granule is ever accepted twice
     auto tags = [&](unsigned long long **g0, unsigned long long **g1, unsigned *tag0) -> int {
@@ -610,7 +615,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
         HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags, L.chain_nb_off,
                                     L.chain_nb_list, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
-                                    l == 1, rdt, h->p.omega, h->slots));
+                                    l == 1, rdt, h->p.omega, h->slots, src_is_T));
         return PAMG_OK;
     }
     if (const int g = face_wave_grid_for(h, l, run)) {   // the call in one wavefront launch
@@ -619,7 +624,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
         HIPCHK(h, launch_face_wave(h->stream, L, h->U, g, h->tov, h->tov_b, h->tovo, g0, g1, tag0, h->wave_flags,
                                    h->wave_order, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
-                                   l == 1, rdt, h->slots));
+                                   l == 1, rdt, h->slots, src_is_T));
         return PAMG_OK;
     }
     for (int s = 0; s < run; ++s) {
@@ -629,7 +634,8 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         Span sp(h, kid, (store == 1 ? 96.0 : 72.0) * (double)L.N + 168.0 * h->U);
         HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
                                           s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
-                                          h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store, s == 0));
+                                          h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store, s == 0,
+                                          s == 0 && src_is_T));
     }
     return PAMG_OK;
 }

@@ -41,14 +41,15 @@ __global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *_
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= npairs) return;
     const int64_t s = 2 * p;
+    HaloPre hp;
+    halo_prefetch(H, s, s >> nsub_log2, nsub_log2, hp);
+    if (!copy && !hp.any) return;   // the words-only form reads just the pairs that have words
     double2 v[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         v[c] = ld2((copy ? TNN : T) + c * pitch + s);
         if (copy) st2(T + c * pitch + s, v[c]);
     }
-    HaloPre hp;
-    halo_prefetch(H, s, s >> nsub_log2, nsub_log2, hp);
     const double p0[3] = {v[0].x, v[1].x, v[2].x}, p1[3] = {v[0].y, v[1].y, v[2].y};
     halo_write(H, hp, p0, p1);
 }
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void k_face(const double *X, double *OUT, c
 #define PAMG_FACE_WAVES 6
 #endif
 template <int TS, int NT, bool UNI, bool RB>
-__global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_sweep(double *T, double *TNN, const double *__restrict__ RHS,
+__global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_sweep(double *T, double *TNN, const double *SRC, const double *__restrict__ RHS,
                                                    const double *__restrict__ stc, const int4 *__restrict__ fnb,
                                                    const double *__restrict__ fface, const int *__restrict__ fsx,
                                                    const double *__restrict__ tin, HaloArgs Hn, int next_halo, int store,
@@ -204,10 +205,10 @@ __global__ __launch_bounds__(NT, (UNI && TS <= 1024) ? PAMG_FACE_WAVES : 1) void
         nbr[k] = fnb[s & nsm];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const double v = TNN[c * pitch + s];
+            const double v = SRC[c * pitch + s];
             b[k][c] = RHS[c * pitch + s];
             X[c][j] = v;
-            if (store == 1 && s0 + j < N) T[c * pitch + s] = v;
+            if (store == 1 && SRC != T && s0 + j < N) T[c * pitch + s] = v;
         }
     }
     __syncthreads();
@@ -386,7 +387,7 @@ struct WaveShape {
 // RHS gathered by colour position from memory or through LDS, profiles/r03_f_face_forms.txt.)
 template <int TS, int NT, bool RB>
 __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_tile(
-    double *T, double *TNN, const double *__restrict__ RHS, const double *__restrict__ stc,
+    double *T, double *TNN, const double *SRC, const double *__restrict__ RHS, const double *__restrict__ stc,
     const int4 *__restrict__ fnb, const double *__restrict__ fface, const int *__restrict__ fsx,
     const double *__restrict__ tin, HaloArgs Hn, int next_halo, int bc, int store, int64_t pitch, int slots,
     int level1, double rdt) {
@@ -420,10 +421,10 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
         nbr[k] = fnb[j];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const double v = TNN[c * pitch + s0 + j];
+            const double v = SRC[c * pitch + s0 + j];
             b[k][c] = RHS[c * pitch + s0 + j];
             X[c][j] = v;
-            if (store == 1) T[c * pitch + s0 + j] = v;
+            if (store == 1 && SRC != T) T[c * pitch + s0 + j] = v;
         }
     }
     __syncthreads();
@@ -581,7 +582,7 @@ constexpr int kWaveStampT = 32, kWaveStampW = 19;   // tickets per workgroup, st
 
 template <int TS, int NT, bool RB>
 __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_wave(
-    double *T, double *TNN, const double *__restrict__ RHS, const double *__restrict__ stc,
+    double *T, double *TNN, const double *SRC, const double *__restrict__ RHS, const double *__restrict__ stc,
     const int4 *__restrict__ fnb, const double *__restrict__ fface, const int *__restrict__ fsx,
     const int *__restrict__ cpos, int nup, double *buf0, double *buf1, u64_t *g0, u64_t *g1, unsigned tag0,
     HaloArgs H, unsigned *flags, const int *__restrict__ order, unsigned *tmo, int U, int run, int total,
@@ -642,7 +643,7 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
         for (int k = 0; k < PER; ++k) {
             const int j = t + NT * k;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) X[c][j] = TNN[c * pitch + s0 + j];
+            for (int c = 0; c < 3; ++c) X[c][j] = SRC[c * pitch + s0 + j];
         }
 #pragma unroll
         for (int k = 0; k < KU; ++k)
@@ -772,7 +773,7 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
 // every pass (the dependent record fetches were most of a sweep's pass time, r03 stamps)
 constexpr int kChainRec = 32, kRecW = 48;   // un_eles, doubles per record: S 13 | w 6 | WD 24 | sx 3
 template <bool UNI, bool RB, bool LREC>
-__global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *TNN, const double *__restrict__ RHS,
+__global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *TNN, const double *SRC, const double *__restrict__ RHS,
                                                           const double *__restrict__ stc, const int4 *__restrict__ fnb,
                                                           const double *__restrict__ fface, const int *__restrict__ fsx,
                                                           double *buf0, double *buf1, HaloArgs H, unsigned *flags,
@@ -855,7 +856,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             b[k][c] = RHS[c * pitch + s];
-            X[c][j] = TNN[c * pitch + s];
+            X[c][j] = SRC[c * pitch + s];
         }
     }
     // the halo positions of the thread's pair (2t, 2t + 1), packed 10 bits per face
@@ -1086,8 +1087,10 @@ hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, i
 bool face_sweep_fusable(const Level &L) { return L.nsub <= 4096; }
 
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc) {
+                                   bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc,
+                                   bool from_T) {
     if (L.N == 0) return hipSuccess;
+    const double *src = from_T ? L.T : L.TNN;   // the sweep's iterate (from_T: tnew holds tnew_nonlin)
     if (!L.fnb || !L.fface || !L.fsx || !face_sweep_fusable(L)) return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
     HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tout, tovo, P.d_send, 1 << L.isplit};
@@ -1095,14 +1098,15 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
     const bool uni = L.nsub >= 64;
 #define PAMG_FSW(TS, NT, U, R)                                                                                      \
     hipLaunchKernelGGL((k_face_sweep<TS, NT, U, R>), dim3((unsigned)((L.N + TS - 1) / TS)), dim3(NT), 0, s, L.T,   \
-                       L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tin, H, nh, st, L.pitch, L.N, lg, slots, l1, rdt, omega)
+                       L.TNN, src, L.RHS, L.stc, L.fnb, L.fface, L.fsx, tin, H, nh, st, L.pitch, L.N, lg, slots, l1, rdt, \
+                       omega)
     // un_eles of 256, 1,024 or 4,096 sub-elements: one tile per un_ele (k_face_tile); the smaller
     // ones in tiles of 256 (more workgroups per CU for sweeps that are short and latency-bound)
     if ((L.nsub == 256 || L.nsub == 1024 || L.nsub == 4096) && L.N % L.nsub == 0) {
         const dim3 g((unsigned)(L.N / L.nsub));
         const int b = bc ? 1 : 0;
 #define PAMG_FTL(TS, NT, R)                                                                                         \
-    hipLaunchKernelGGL((k_face_tile<TS, NT, R>), g, dim3(NT), 0, s, L.T, L.TNN, L.RHS, L.stc, L.fnb, L.fface, L.fsx, \
+    hipLaunchKernelGGL((k_face_tile<TS, NT, R>), g, dim3(NT), 0, s, L.T, L.TNN, src, L.RHS, L.stc, L.fnb, L.fface, L.fsx, \
                        tin, H, nh, b, st, L.pitch, slots, l1, rdt)
         if (L.nsub == 4096) {
             if (rb) PAMG_FTL(4096, 1024, true);
@@ -1144,7 +1148,7 @@ bool face_chain_fits(int nsub, int U, int cus) {
 
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
-                             int store, bool rb, bool level1, double rdt, double omega, int slots) {
+                             int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T) {
     if (L.N == 0 || run <= 0) return hipSuccess;
     if (!face_chain_fits(L.nsub, U, cus) || !L.fnb) return hipErrorInvalidValue;
     const int g = std::max(1, std::min(cus, U));
@@ -1171,7 +1175,8 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     }
     const int *cpos = L.cpos;
     int nup = L.nup;
-    void *args[] = {&T, &TNN, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
+    const double *SRC = from_T ? L.T : L.TNN;
+    void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
                     &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &stamps};
     // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
     const bool uni = L.nsub >= 64,
@@ -1226,7 +1231,7 @@ int face_wave_grid(const Level &L, bool rb, int cus) {
 hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, double *tov, double *tov_b, double *tovo,
                             unsigned long long *g0, unsigned long long *g1, unsigned tag0, unsigned *flags,
                             const int *order, unsigned *tmo, int run, int total, int store, bool rb, bool level1,
-                            double rdt, int slots) {
+                            double rdt, int slots, bool from_T) {
     if (L.N == 0 || run <= 0) return hipSuccess;
     int nt = 0;
     const void *f = face_wave_fn(L.nsub, rb, &nt);
@@ -1254,7 +1259,8 @@ hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, doub
     const int g = std::min(grid, U);
     const int *cpos = L.cpos;
     int nup = L.nup;
-    void *args[] = {&T, &TNN, &RHS, &stc, &fnb, &fface, &fsx, &cpos, &nup, &tov, &tov_b, &g0, &g1, &tag0, &H, &flags,
+    const double *SRC = from_T ? L.T : L.TNN;
+    void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &cpos, &nup, &tov, &tov_b, &g0, &g1, &tag0, &H, &flags,
                     &order, &tmo, &U, &run, &total, &store, &pitch, &slots, &l1, &rdt, &stamps};
     e = hipLaunchCooperativeKernel(f, dim3(g), dim3(nt), args, 0, s);
     if (stamp_path) {

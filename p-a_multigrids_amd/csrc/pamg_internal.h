@@ -331,7 +331,7 @@ bool face_sweep_fusable(const Level &L);
 // last executed sweep of a call whose final sweep is dead); bc: the call's first sweep (its next-halo
 // words include the boundary words of the other snapshot buffer)
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc);
+                                   bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc, bool from_T = false);
 // the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of
 // the call's `total` sweeps in one launch, the iterate in LDS, the halo handed over between
 // workgroups inside the launch; store 1: tnew (the last sweep's start) and tnew_nonlin, 2: tnew :=
@@ -347,11 +347,11 @@ int face_wave_grid(const Level &L, bool rb, int cus);
 hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, double *tov, double *tov_b, double *tovo,
                             unsigned long long *g0, unsigned long long *g1, unsigned tag0, unsigned *flags,
                             const int *order, unsigned *tmo, int run, int total, int store, bool rb, bool level1,
-                            double rdt, int slots);
+                            double rdt, int slots, bool from_T = false);
 int face_chain_per_wg(int nsub, int U, int cus);
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
-                             int store, bool rb, bool level1, double rdt, double omega, int slots);
+                             int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T = false);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg
