@@ -571,7 +571,13 @@ bool face_tiles_ok(pamg_handle *h, int l) {
 // (face_call): a single domain (a partition exchanges them between sweeps)
 bool face_fusable(pamg_handle *h, int l) { return face_tiles_ok(h, l) && h->nranks == 1 && !h->comm; }
 
-int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) {
+int face_residual(pamg_handle *h, int l, bool neg);
+
+// res: also get_residual of level l (A tnew - RHS with the halo refreshed from tnew, :725-873) before
+// the call changes tnew -- computed by the call's first tile sweep from the iterate and snapshot it
+// loads anyway (the residual's own launch read tnew and RHS again), or by its own launch when the call
+// runs another form
+int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, bool res = false) {
     Level &L = h->lv[l];
     h->tnn_level = l;
     h->overlap_static_l1 = false;
@@ -585,6 +591,10 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
     if (!h->tov_b) CHK(dev_alloc(h, &h->tov_b, (size_t)h->slots * 3 * std::max(h->U, 1)));
     double *buf[2] = {h->tov, h->tov_b};
     const int run = dead_last ? sweeps - 1 : sweeps;   // the sweeps that are executed
+    // the residual in the first tile sweep: src_is_T (its iterate is tnew) and the tile loop below
+    const bool res_in_sweep = res && src_is_T && run >= 1 && face_tile_shape(L) && !(run >= 2 && face_chain_ok(h, l)) &&
+                              !face_wave_grid_for(h, l, run);
+    if (res && !res_in_sweep) CHK(face_residual(h, l, false));
     if (run <= 0) {   // a call of one dead sweep: tnew := tnew_nonlin and its :555 words
         if (src_is_T && !dead_last) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
         if (sweeps > 0) HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, !src_is_T));
@@ -631,11 +641,13 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last) 
         const bool fin = s + 1 == run;
         // read tnew_nonlin, RHS; write tnew_nonlin (+ tnew in the last sweep, + the next halo words)
         const int store = fin ? (dead_last ? 2 : 1) : 0;
-        Span sp(h, kid, (store == 1 ? 96.0 : 72.0) * (double)L.N + 168.0 * h->U);
+        const bool r = s == 0 && res_in_sweep;
+        if (r) h->rhsn_valid = false;
+        Span sp(h, kid, (store == 1 ? 96.0 : 72.0) * (double)L.N + (r ? 24.0 * (double)L.N : 0.0) + 168.0 * h->U);
         HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
                                           s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
                                           h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store, s == 0,
-                                          s == 0 && src_is_T));
+                                          s == 0 && src_is_T, r ? L.RES : nullptr));
     }
     return PAMG_OK;
 }
@@ -915,13 +927,16 @@ int vcycle_face_fused(pamg_handle *h, int n) {
         for (int l = 1; l <= L; ++l) {   // :323-340
             CHK(face_call(h, l, true, ns, true));
             CHK(restrict_(h, l));
+            if (l < L) continue;   // levels < L: get_residual rides on the prolongation-leg call below
             Level &V = h->lv[l];
             h->rhsn_valid = false;
             Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)V.N + 168.0 * h->U);   // tnew, RHS in, residual out
             HIPCHK(h, launch_face_residual(h->stream, V, h->tov, false, l == 1, rdt, h->slots));
         }
         CHK(face_call(h, L, true, ns * h->p.n_coarse, !last));   // :344-359
-        for (int l = L - 1; l >= 1; --l) CHK(face_call(h, l, true, ns, !last));   // :363-378
+        // :363-378; the residual of the restriction leg (:336) is due after the level's call there, and
+        // nothing changes level l's tnew, RHS or halo words until this call starts: it computes it
+        for (int l = L - 1; l >= 1; --l) CHK(face_call(h, l, true, ns, !last, true));
     }
     h->tnn_level = 1;
     return face_chain_check(h);

@@ -390,7 +390,7 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
     double *T, double *TNN, const double *SRC, const double *__restrict__ RHS, const double *__restrict__ stc,
     const int4 *__restrict__ fnb, const double *__restrict__ fface, const int *__restrict__ fsx,
     const double *__restrict__ tin, HaloArgs Hn, int next_halo, int bc, int store, int64_t pitch, int slots,
-    int level1, double rdt) {
+    int level1, double rdt, double *RESout) {
     constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
     static_assert(PER % 2 == 0 && M * M == TS, "whole un_ele tiles, adjacent pairs per thread");
     __shared__ double X[3][TS];
@@ -430,6 +430,19 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
     __syncthreads();
     auto xin = [&](int c, int q) { return X[c][q]; };
     auto hv = [&](int64_t, int mf, int sp, int kk) { return HI[((mf - 1) * M + sp - 1) * 3 + kk]; };
+    if (RESout) {   // get_residual (A x - RHS) of the iterate and snapshot the sweep starts from (:555, :869)
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = t + NT * k;
+            double x[3], r[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[c] = X[c][j];
+            face_apply<3>(R, xin, x, b[k], nbr[k], u, hv, [&](int) { return 0.0; }, level1, rdt, r);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) RESout[c * pitch + s0 + j] = r[c];
+        }
+        __syncthreads();   // every read of the start iterate before the passes rewrite it
+    }
     auto pass = [&](auto mc) {
         constexpr int MODE = decltype(mc)::value;
         double r[PER][3];
@@ -1082,13 +1095,16 @@ hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, i
     return hipGetLastError();
 }
 
+// the levels whose sweep is one tile per un_ele (k_face_tile: 256, 1,024 or 4,096 sub-elements)
+bool face_tile_shape(const Level &L) { return (L.nsub == 256 || L.nsub == 1024 || L.nsub == 4096) && L.N % L.nsub == 0; }
+
 // one fused sweep (k_face_sweep): reads the halo snapshot tin, writes the next sweep's halo words
 // into tout unless tout is null; single domain, un_eles of at most 4096 sub-elements
 bool face_sweep_fusable(const Level &L) { return L.nsub <= 4096; }
 
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
                                    bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc,
-                                   bool from_T) {
+                                   bool from_T, double *res) {
     if (L.N == 0) return hipSuccess;
     const double *src = from_T ? L.T : L.TNN;   // the sweep's iterate (from_T: tnew holds tnew_nonlin)
     if (!L.fnb || !L.fface || !L.fsx || !face_sweep_fusable(L)) return hipErrorInvalidValue;
@@ -1102,12 +1118,13 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
                        omega)
     // un_eles of 256, 1,024 or 4,096 sub-elements: one tile per un_ele (k_face_tile); the smaller
     // ones in tiles of 256 (more workgroups per CU for sweeps that are short and latency-bound)
-    if ((L.nsub == 256 || L.nsub == 1024 || L.nsub == 4096) && L.N % L.nsub == 0) {
+    if (res && !face_tile_shape(L)) return hipErrorInvalidValue;
+    if (face_tile_shape(L)) {
         const dim3 g((unsigned)(L.N / L.nsub));
         const int b = bc ? 1 : 0;
 #define PAMG_FTL(TS, NT, R)                                                                                         \
     hipLaunchKernelGGL((k_face_tile<TS, NT, R>), g, dim3(NT), 0, s, L.T, L.TNN, src, L.RHS, L.stc, L.fnb, L.fface, L.fsx, \
-                       tin, H, nh, b, st, L.pitch, slots, l1, rdt)
+                       tin, H, nh, b, st, L.pitch, slots, l1, rdt, res)
         if (L.nsub == 4096) {
             if (rb) PAMG_FTL(4096, 1024, true);
             else PAMG_FTL(4096, 1024, false);

@@ -331,7 +331,10 @@ bool face_sweep_fusable(const Level &L);
 // last executed sweep of a call whose final sweep is dead); bc: the call's first sweep (its next-halo
 // words include the boundary words of the other snapshot buffer)
 hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *tin, double *tout, double *tovo,
-                                   bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc, bool from_T = false);
+                                   bool rb, bool level1, double rdt, double omega, int slots, int store, bool bc, bool from_T = false,
+                                   double *res = nullptr);
+// k_face_tile's levels (one tile per un_ele); their first sweep can also write get_residual (res)
+bool face_tile_shape(const Level &L);
 // the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of
 // the call's `total` sweeps in one launch, the iterate in LDS, the halo handed over between
 // workgroups inside the launch; store 1: tnew (the last sweep's start) and tnew_nonlin, 2: tnew :=
