@@ -416,15 +416,18 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
     for (int i = t; i < NH; i += NT) HI[i] = tin[u * slots * 3 + (int64_t)(i / (3 * M)) * slots + i % (3 * M)];
     if (t < 24) WD[t] = fface[u * kFaceStride + kFaceWD + t];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {   // tnew := tnew_nonlin (:550); the iterate into LDS
-        const int j = t + NT * k;
+    for (int k = 0; k < PER; k += 2) {   // tnew := tnew_nonlin (:550); the iterate into LDS, pairs
+        const int j = 2 * (t + NT * (k / 2));
         nbr[k] = fnb[j];
+        nbr[k + 1] = fnb[j + 1];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const double v = SRC[c * pitch + s0 + j];
-            b[k][c] = RHS[c * pitch + s0 + j];
-            X[c][j] = v;
-            if (store == 1 && SRC != T) T[c * pitch + s0 + j] = v;
+            const double2 v = ld2(SRC + c * pitch + s0 + j), r = ld2(RHS + c * pitch + s0 + j);
+            b[k][c] = r.x;
+            b[k + 1][c] = r.y;
+            X[c][j] = v.x;
+            X[c][j + 1] = v.y;
+            if (store == 1 && SRC != T) st2(T + c * pitch + s0 + j, v);
         }
     }
     __syncthreads();
@@ -433,7 +436,7 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
     if (RESout) {   // get_residual (A x - RHS) of the iterate and snapshot the sweep starts from (:555, :869)
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int j = t + NT * k;
+            const int j = 2 * (t + NT * (k / 2)) + (k & 1);   // adjacent pairs (16-B accesses)
             double x[3], r[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) x[c] = X[c][j];
@@ -449,7 +452,7 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
         bool on[PER];
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int j = t + NT * k;
+            const int j = 2 * (t + NT * (k / 2)) + (k & 1);   // adjacent pairs (16-B accesses)
             const int4 nb = nbr[k];
             on[k] = !((MODE == 0 && !nb.w) || (MODE == 1 && nb.w));
             if (!on[k]) continue;
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
             for (int k = 0; k < PER; ++k)
                 if (on[k])
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) X[c][t + NT * k] = r[k][c];
+                    for (int c = 0; c < 3; ++c) X[c][2 * (t + NT * (k / 2)) + (k & 1)] = r[k][c];
         }
         __syncthreads();
     };
@@ -479,10 +482,10 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
         pass(std::integral_constant<int, 2>{});
     }
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew)
-        const int j = t + NT * k;
+    for (int k = 0; k < PER; k += 2) {   // tnew_nonlin (store 2: tnew), pairs
+        const int j = 2 * (t + NT * (k / 2));
 #pragma unroll
-        for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+        for (int c = 0; c < 3; ++c) st2((store == 2 ? T : TNN) + c * pitch + s0 + j, make_double2(X[c][j], X[c][j + 1]));
     }
     if (!next_halo) return;
 #pragma unroll
