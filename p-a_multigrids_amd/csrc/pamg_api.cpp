@@ -597,10 +597,14 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
     if (res && !res_in_sweep) CHK(face_residual(h, l, false));
     if (run <= 0) {   // a call of one dead sweep: tnew := tnew_nonlin and its :555 words
         if (src_is_T && !dead_last) HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
-        if (sweeps > 0) HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, !src_is_T));
+        if (sweeps > 0) {
+            if (src_is_T) HIPCHK(h, launch_face_words(h->stream, L, h->U, h->tov, h->tovo));
+            else HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, true));
+        }
         return PAMG_OK;
     }
-    HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, !src_is_T));   // :550, :555
+    if (src_is_T) HIPCHK(h, launch_face_words(h->stream, L, h->U, buf[(sweeps - 1) & 1], h->tovo));   // :555
+    else HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
     // the tagged halo granules of an in-launch call (chain or wavefront): sweep s of this call carries
     // tag wave_tag + s; the base then moves past the call's tags, so no granule is ever accepted twice
     auto tags = [&](unsigned long long **g0, unsigned long long **g1, unsigned *tag0) -> int {
@@ -751,7 +755,7 @@ int face_residual(pamg_handle *h, int l, bool neg) {
     Level &L = h->lv[l];
     h->rhsn_valid = false;
     h->overlap_static_l1 = false;
-    HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, false));
+    HIPCHK(h, launch_face_words(h->stream, L, h->U, h->tov, h->tovo));
     CHK(halo(h, l));
     // tnew, RHS in, residual out (the neighbours' values are the same tnew, gathered from cache)
     Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)L.N + 168.0 * h->U);
@@ -1282,7 +1286,7 @@ void free_levels(pamg_handle *h) {
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
         dev_free(L.halo.d_ring); dev_free(L.halo.d_recv3);
-        dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv);
+        dev_free(L.halo.d_hface); dev_free(L.halo.d_hsub); dev_free(L.halo.d_bcv); dev_free(L.halo.d_bpos);
         dev_free(L.halo.d_surf); dev_free(L.halo.d_told_halo);
         L = Level();
     }
@@ -1578,6 +1582,14 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         CHK(dev_upload(h, &P.d_recv_dst, P.recv_dst));
         CHK(dev_upload(h, &P.d_hface, P.hface));
         CHK(dev_upload(h, &P.d_hsub, P.hsub));
+        {
+            std::vector<int> bpos;
+            for (int q = 0; q < (int)P.hsub.size(); ++q)
+                if (P.hsub[q].x | P.hsub[q].y | P.hsub[q].z) bpos.push_back(q);
+            P.nbpos = (int)bpos.size();
+            if (bpos.empty()) bpos.push_back(0);
+            CHK(dev_upload(h, &P.d_bpos, bpos));
+        }
         CHK(dev_upload(h, &P.d_bcv, P.bcv));
         CHK(dev_upload(h, &P.d_surf, P.surf));
         CHK(dev_alloc(h, &P.d_told_halo, 3 * (size_t)P.n_told));

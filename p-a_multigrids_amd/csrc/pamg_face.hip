@@ -54,6 +54,34 @@ __global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *_
     halo_write(H, hp, p0, p1);
 }
 
+// the words-only refresh (launch_face_halo(copy = false)'s words) over the sub-elements that have
+// words: thread i -> un_ele i / nb, position bpos[i % nb]; the told words from the compact told halo
+// (halo_prefetch's rule), every word through halo_face as k_face_halo writes it
+__global__ __launch_bounds__(kBlock) void k_face_words(const double *__restrict__ T, int64_t pitch, HaloArgs H,
+                                                       const int *__restrict__ bpos, int nb, int64_t nwork,
+                                                       int nsub_log2) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nwork) return;
+    const int64_t u = i / nb;
+    const int p = bpos[i - u * nb];
+    const int64_t s = (u << nsub_log2) + p;
+    HaloPre P;
+    P.hs0 = H.hsub[p];
+    P.r1 = H.hface[3 * u];
+    P.r2 = H.hface[3 * u + 1];
+    P.r3 = H.hface[3 * u + 2];
+    double t[3], to[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) t[c] = T[c * pitch + s];
+    const int e = told_entry(P, P.hs0);
+    if (e >= 0)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) to[c] = H.told[3 * (int64_t)e + c];
+    if (P.hs0.x) halo_face<true, true>(H, P.r1, 1, P.hs0.x, t, to);
+    if (P.hs0.y) halo_face<true, true>(H, P.r2, 2, P.hs0.y, t, to);
+    if (P.hs0.z) halo_face<true, true>(H, P.r3, 3, P.hs0.z, t, to);
+}
+
 // The operator record of one un_ele as face_apply reads it: the element stencil, the face weights
 // w_f (inner faces 0..2 by sub-element face, then the un_ele faces 1..3) and the un_ele faces' node
 // selectors (fsx) under sub-element faces 0..2
@@ -1074,6 +1102,16 @@ hipError_t launch_face_halo(hipStream_t s, const Level &L, double *tov, double *
     HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << L.isplit};
     hipLaunchKernelGGL(k_face_halo, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.T, L.TNN, L.pitch, npairs,
                        log2i(L.nsub), H, copy ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_face_words(hipStream_t s, const Level &L, int U, double *tov, double *tovo) {
+    const HaloPlan &P = L.halo;
+    const int64_t nwork = (int64_t)U * P.nbpos;
+    if (nwork == 0 || L.N == 0) return hipSuccess;
+    HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << L.isplit};
+    hipLaunchKernelGGL(k_face_words, dim3(grid_for(nwork)), dim3(kBlock), 0, s, L.T, L.pitch, H, P.d_bpos, P.nbpos,
+                       nwork, log2i(L.nsub));
     return hipGetLastError();
 }
 

@@ -54,6 +54,10 @@ struct HaloPlan {
     std::vector<int> surf;                // surf_ele(i, f) of loc_surf_ele_multigrid, (m, 3), 1-based
     int n_told = 0;                       // entries of the told halo (3 fp64 each); hface.w = first entry
     int4 *d_hface = nullptr, *d_hsub = nullptr;
+    // the positions of the sub-elements that have halo words (any hsub face nonzero), ascending: the
+    // words-only refresh (launch_face_words) runs over U x nbpos of them instead of the whole level
+    int *d_bpos = nullptr;
+    int nbpos = 0;
     double2 *d_bcv = nullptr;
     int *d_surf = nullptr;
     double *d_told_halo = nullptr;        // told values of the copied sub-elements, refreshed when told changes
@@ -320,6 +324,8 @@ hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt);
 // red-black Gauss-Seidel in place on tnew_nonlin -- 2 Jacobi from tnew); the residual A tnew - RHS
 // (neg: RHS - A tnew); level1: the domain-boundary values enter (coarse levels: zero)
 hipError_t launch_face_halo(hipStream_t s, const Level &L, double *tov, double *tovo, bool copy);
+// the same words as launch_face_halo(copy = false), from tnew, over the sub-elements that have them
+hipError_t launch_face_words(hipStream_t s, const Level &L, int U, double *tov, double *tovo);
 hipError_t launch_face_sweep(hipStream_t s, const Level &L, const double *tov, int mode, bool level1, double rdt,
                              double omega, int slots);
 hipError_t launch_face_residual(hipStream_t s, const Level &L, const double *tov, bool neg, bool level1, double rdt,

@@ -5,6 +5,9 @@ import os
 import sys
 import time
 
+import torch  # noqa: F401  (as bench.py: the HIP runtime comes up through torch; a bare process
+#              segfaulted in its exit handlers under rocprofv3, profiles/r03_final)
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "p-a_multigrids_amd"))
 import pamg  # noqa: E402
