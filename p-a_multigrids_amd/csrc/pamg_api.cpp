@@ -1580,6 +1580,11 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
             L.nup = 0;
             for (int j = 0; j < L.nsub; ++j) L.nup += fnb[j].w != 0;
             L.ndn = L.nsub - L.nup;
+            L.words_up = true;
+            for (int j = 0; j < L.nsub && j < (int)L.halo.hsub.size(); ++j) {
+                const int4 e = L.halo.hsub[j];
+                if ((e.x | e.y | e.z) && !fnb[j].w) L.words_up = false;
+            }
             CHK(dev_upload(h, &L.cpos, cpos));
         }
         HaloPlan &P = L.halo;

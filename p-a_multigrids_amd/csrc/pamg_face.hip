@@ -825,7 +825,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                                                           unsigned *tmo, int run, int total, int store, int E,
                                                           int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                           double rdt, double omega, const int *__restrict__ cpos,
-                                                          int nup, long long *stamps) {
+                                                          int nup, int early, long long *stamps) {
     constexpr int NT = kChainNT, PER = kChainPer;
     __shared__ double X[3][NT * PER];
     __shared__ double HI[kChainHalo];   // this workgroup's un_eles' t_overlap(1 : 3m, 1 : 3) of the sweep
@@ -957,6 +957,27 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 #pragma unroll
         for (int f = 0; f < 3; ++f) hrec[f] = H.hface[3 * u + f];
     }
+    // the next sweep's halo words (:550, :555 of sweep sw + 1), written through (sc1)
+    auto words = [&](double *tout, int sw) {
+        HaloArgs Hn = H;
+        Hn.tov = tout;
+        const int j = 2 * t;
+        // opaque per sweep: the halo destinations are recomputed here instead of hoisted out of the
+        // sweep loop (held in registers they spilled)
+        int hq[2] = {hp[0], hp[1]};
+        int4 hr[3] = {hrec[0], hrec[1], hrec[2]};
+        asm volatile("" : "+v"(hq[0]), "+v"(hq[1]));
+#pragma unroll
+        for (int f = 0; f < 3; ++f) asm volatile("" : "+v"(hr[f].x), "+v"(hr[f].y), "+v"(hr[f].z));
+        if ((hq[0] | hq[1]) != 0) {
+            // per lane: a wave's pairs span 128 sub-elements, two un_eles when nsub = 64
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const double tv[3] = {X[0][j + q], X[1][j + q], X[2][j + q]};
+                halo_words<true>(Hn, hr, hq[q], tv, sw == 0);
+            }
+        }
+    };
     const int na = nb_off[w], nn = nb_off[w + 1] - na;
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
@@ -1031,6 +1052,17 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                     for (int c = 0; c < 3; ++c) X[c][IA.j[k]] = r[c];
                 });
                 __syncthreads();
+                // early: every halo sub-element is an up one (the host checked), final after the
+                // up pass -- its words go out now, their write-through latency under the down pass
+                if (early && tout) {
+                    words(tout, sw);
+                    if (early == 2) {   // and the flag too: the down pass runs while the neighbours read
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __syncthreads();
+                        if (t == 0)
+                            __hip_atomic_store((g_u32 *)flags + w, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
                 items_pass<1>(IB, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
 #pragma unroll
                     for (int c = 0; c < 3; ++c) X[c][IB.j[k]] = r[c];
@@ -1056,26 +1088,9 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             pass(std::integral_constant<int, 2>{});
         }
         stamp(2);
-        if (tout) {   // the next sweep's halo words (:550, :555 of sweep sw + 1), written through
-            HaloArgs Hn = H;
-            Hn.tov = tout;
-            const int j = 2 * t;
-            // opaque per sweep: the halo destinations are recomputed here instead of hoisted out of the
-            // sweep loop (held in registers they spilled)
-            int hq[2] = {hp[0], hp[1]};
-            int4 hr[3] = {hrec[0], hrec[1], hrec[2]};
-            asm volatile("" : "+v"(hq[0]), "+v"(hq[1]));
-#pragma unroll
-            for (int f = 0; f < 3; ++f) asm volatile("" : "+v"(hr[f].x), "+v"(hr[f].y), "+v"(hr[f].z));
-            if ((hq[0] | hq[1]) != 0) {
-                // per lane: a wave's pairs span 128 sub-elements, two un_eles when nsub = 64
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const double tv[3] = {X[0][j + q], X[1][j + q], X[2][j + q]};
-                    halo_words<true>(Hn, hr, hq[q], tv, sw == 0);
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+        if (tout && !(LREC && RB && early == 2)) {   // publish: every storing wave drains, then the workgroup's flag
+            if (!(LREC && RB && early)) words(tout, sw);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (t == 0) __hip_atomic_store((g_u32 *)flags + w, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1234,8 +1249,11 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     const int *cpos = L.cpos;
     int nup = L.nup;
     const double *SRC = from_T ? L.T : L.TNN;
+    // PAMG_CHAIN_EARLY (A/B): 0 publish after the down pass, 1 the words after the up pass, 2 (default) words and flag
+    static const int early_env = [] { const char *e = getenv("PAMG_CHAIN_EARLY"); return e ? atoi(e) : 2; }();
+    int early = L.words_up ? early_env : 0;
     void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
-                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &stamps};
+                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &early, &stamps};
     // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
     const bool uni = L.nsub >= 64,
                lrec = k <= kChainRec && L.cpos && (int64_t)k * L.nup <= 2 * kChainNT && (int64_t)k * L.ndn <= kChainNT;

@@ -117,6 +117,9 @@ struct Level {
     // (fnb.w != 0, ascending), then of the down ones -- nup + ndn = nsub
     int *cpos = nullptr;
     int nup = 0, ndn = 0;
+    // every sub-element with halo words (HaloPlan::hsub) is an up one: the chain publishes a
+    // sweep's words right after its up pass (k_face_chain, early)
+    bool words_up = false;
     double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
     // the persistent face chain (pamg_face.hip k_face_chain; lazy): its workgroups' neighbour lists
