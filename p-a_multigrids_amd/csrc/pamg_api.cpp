@@ -1573,10 +1573,21 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
             CHK(dev_upload(h, &L.fnb, fnb));
             CHK(dev_upload(h, &L.fface, fface));
             CHK(dev_upload(h, &L.fsx, fsx));
+            // the up positions without halo words, the up ones with words, then the down ones (the
+            // order inside a colour is free: a colour pass reads only the other colour)
+            auto has_words = [&](int j) {
+                if (j >= (int)L.halo.hsub.size()) return false;
+                const int4 e = L.halo.hsub[j];
+                return (e.x | e.y | e.z) != 0;
+            };
             std::vector<int> cpos;
-            for (int pass = 0; pass < 2; ++pass)
-                for (int j = 0; j < L.nsub; ++j)
-                    if ((fnb[j].w != 0) == (pass == 0)) cpos.push_back(j);
+            L.nui = 0;
+            for (int pass = 0; pass < 3; ++pass)
+                for (int j = 0; j < L.nsub; ++j) {
+                    const bool up = fnb[j].w != 0;
+                    if (pass == 0 ? up && !has_words(j) : pass == 1 ? up && has_words(j) : !up) cpos.push_back(j);
+                    if (pass == 0 && up && !has_words(j)) ++L.nui;
+                }
             L.nup = 0;
             for (int j = 0; j < L.nsub; ++j) L.nup += fnb[j].w != 0;
             L.ndn = L.nsub - L.nup;

@@ -379,11 +379,11 @@ struct Items {
 // stored in place at once by a colour pass (a colour reads only the other colour), held by Jacobi
 template <int MODE, int K, class XIN, class HV, class REC, class OUT>
 __device__ __forceinline__ void items_pass(const Items<K> &I, const XIN &xin, const HV &hv, const REC &rec, int level1,
-                                           double rdt, const OUT &out) {
+                                           double rdt, const OUT &out, int kb = 0, int ke = K) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int j = I.j[k];
-        if (j < 0) continue;
+        if (j < 0 || k < kb || k >= ke) continue;
         double x[3], r[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) x[c] = xin(c, j);
@@ -825,8 +825,13 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                                                           unsigned *tmo, int run, int total, int store, int E,
                                                           int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                           double rdt, double omega, const int *__restrict__ cpos,
-                                                          int nup, int early, long long *stamps) {
+                                                          int nup, int nui, int early, long long *stamps) {
     constexpr int NT = kChainNT, PER = kChainPer;
+    // early (LREC red-black only; the host checked that every halo sub-element is an up one):
+    // 1 a sweep's halo words go out right after its up pass, 2 and its flag, 3 as 2 with the up
+    // pass split -- item 0 the up sub-elements without halo words (Level::nui per un_ele, first in
+    // cpos), run before the wait for the neighbours; item 1 the ones with words, after it
+    const bool split = LREC && RB && early == 3;
     __shared__ double X[3][NT * PER];
     __shared__ double HI[kChainHalo];   // this workgroup's un_eles' t_overlap(1 : 3m, 1 : 3) of the sweep
     __shared__ double RS[LREC ? kChainRec * kRecW : 1];
@@ -863,7 +868,13 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
         for (int k = 0; k < KU; ++k) {
             const int i = t + NT * k;
             int j = -1;
-            if (RB) {
+            if (RB && split) {
+                const int nk = k == 0 ? nui : nup - nui, o = k == 0 ? 0 : nui;
+                if (k < 2 && t < kv * nk) {
+                    const int uk = t / nk;
+                    j = (uk << nsub_log2) + cpos[o + t - uk * nk];
+                }
+            } else if (RB) {
                 if (i < kv * nup) {
                     const int uk = i / nup;
                     j = (uk << nsub_log2) + cpos[i - uk * nup];
@@ -978,6 +989,42 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             }
         }
     };
+    // tnew := tnew_nonlin (:550) of the call's last sweep, from the tile before that sweep
+    auto tstore = [&]() {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = t + NT * k;
+            if (j < E && s0 + j < N)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = X[c][j];
+        }
+    };
+    // split: the last sweep's phase A rewrites the tile before the wait, so the store is made
+    // from the same values at the end of the sweep before it (or here, for a one-sweep call)
+    if (split && store == 1 && run == 1) {
+        tstore();
+        __syncthreads();
+    }
+    // the item passes' tile, halo snapshot and un_ele records (LREC)
+    auto ixin = [&](int c, int q) { return X[c][q]; };
+    auto ihv = [&](int64_t uu, int mf, int sp, int kk) {
+        return HI[(((int)(uu - u0) * 3 + mf - 1) * m + sp - 1) * 3 + kk];
+    };
+    auto irec = [&](int j, int4 nb, auto &&f) {
+        const int uk = j >> nsub_log2;
+        const double *rs = RS + uk * kRecW;
+        FaceRec R;
+        R.S.c = rs[0];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) R.S.K[q] = rs[1 + q];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) R.S.w[q] = rs[10 + q];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) R.w[q] = rs[13 + q];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) R.sx[q] = (int)rs[43 + q];
+        f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
+    };
     const int na = nb_off[w], nn = nb_off[w + 1] - na;
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
@@ -988,6 +1035,16 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             if (stamps && t == 0 && w < 8) stamps[((int64_t)w * run + sw) * 4 + i] = wall_clock64();
         };
         stamp(0);
+        if constexpr (LREC && RB) {
+            if (split) {   // the up sub-elements without halo words: no snapshot needed, before the wait
+                // (no face of these reads the halo: the snapshot accessor is a constant the compiler drops)
+                auto nohv = [](int64_t, int, int, int) { return 0.0; };
+                items_pass<0>(IA, ixin, nohv, irec, level1, rdt, [&](int k, const double r[3]) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][IA.j[k]] = r[c];
+                }, 0, 1);
+            }
+        }
         if (sw > 0 && t < 64) {   // wait for the neighbours' words of this sweep: one wave polls
             for (int base = 0; base < nn; base += 64) {
                 const int i = base + t;
@@ -1013,63 +1070,38 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
         }
         // the call's last sweep: tnew := tnew_nonlin (:550), before the barrier that lets the passes
         // rewrite X (with item lists a position's item may belong to another thread)
-        if (store == 1 && sw + 1 == run)
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const int j = t + NT * k;
-                if (j < E && s0 + j < N)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = X[c][j];
-            }
+        if (store == 1 && sw + 1 == run && !split) tstore();
         __syncthreads();
         stamp(1);
         if constexpr (LREC) {
 #pragma unroll
             for (int k = 0; k < KU; ++k) asm volatile("" : "+v"(IA.j[k]), "+v"(IA.nb[k].x), "+v"(IA.nb[k].y), "+v"(IA.nb[k].z), "+v"(IA.nb[k].w));
             asm volatile("" : "+v"(IB.j[0]), "+v"(IB.nb[0].x), "+v"(IB.nb[0].y), "+v"(IB.nb[0].z), "+v"(IB.nb[0].w));
-            auto xin = [&](int c, int q) { return X[c][q]; };
-            auto hv = [&](int64_t uu, int mf, int sp, int kk) {
-                return HI[(((int)(uu - u0) * 3 + mf - 1) * m + sp - 1) * 3 + kk];
-            };
-            auto rec = [&](int j, int4 nb, auto &&f) {
-                const int uk = j >> nsub_log2;
-                const double *rs = RS + uk * kRecW;
-                FaceRec R;
-                R.S.c = rs[0];
-#pragma unroll
-                for (int q = 0; q < 9; ++q) R.S.K[q] = rs[1 + q];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) R.S.w[q] = rs[10 + q];
-#pragma unroll
-                for (int q = 0; q < 6; ++q) R.w[q] = rs[13 + q];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) R.sx[q] = (int)rs[43 + q];
-                f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
-            };
             if constexpr (RB) {   // up sub-elements, then down ones, in place
-                items_pass<0>(IA, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+                auto up = [&](int k, const double r[3]) {
 #pragma unroll
                     for (int c = 0; c < 3; ++c) X[c][IA.j[k]] = r[c];
-                });
+                };
+                items_pass<0>(IA, ixin, ihv, irec, level1, rdt, up, split ? 1 : 0);   // split: the items with words
                 __syncthreads();
                 // early: every halo sub-element is an up one (the host checked), final after the
                 // up pass -- its words go out now, their write-through latency under the down pass
                 if (early && tout) {
                     words(tout, sw);
-                    if (early == 2) {   // and the flag too: the down pass runs while the neighbours read
+                    if (early >= 2) {   // and the flag too: the down pass runs while the neighbours read
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __syncthreads();
                         if (t == 0)
                             __hip_atomic_store((g_u32 *)flags + w, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
-                items_pass<1>(IB, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+                items_pass<1>(IB, ixin, ihv, irec, level1, rdt, [&](int k, const double r[3]) {
 #pragma unroll
                     for (int c = 0; c < 3; ++c) X[c][IB.j[k]] = r[c];
                 });
             } else {   // Jacobi: every read of the old iterate before any write
                 double rj[KU][3];
-                items_pass<2>(IA, xin, hv, rec, level1, rdt, [&](int k, const double r[3]) {
+                items_pass<2>(IA, ixin, ihv, irec, level1, rdt, [&](int k, const double r[3]) {
 #pragma unroll
                     for (int c = 0; c < 3; ++c) rj[k][c] = r[c];
                 });
@@ -1081,6 +1113,10 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                         for (int c = 0; c < 3; ++c) X[c][IA.j[k]] = rj[k][c];
             }
             __syncthreads();
+            if (split && store == 1 && sw + 2 == run) {   // the last sweep's tnew (see tstore)
+                tstore();
+                __syncthreads();
+            }
         } else if constexpr (RB) {
             pass(std::integral_constant<int, 0>{});
             pass(std::integral_constant<int, 1>{});
@@ -1088,7 +1124,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             pass(std::integral_constant<int, 2>{});
         }
         stamp(2);
-        if (tout && !(LREC && RB && early == 2)) {   // publish: every storing wave drains, then the workgroup's flag
+        if (tout && !(LREC && RB && early >= 2)) {   // publish: every storing wave drains, then the workgroup's flag
             if (!(LREC && RB && early)) words(tout, sw);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -1249,11 +1285,14 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     const int *cpos = L.cpos;
     int nup = L.nup;
     const double *SRC = from_T ? L.T : L.TNN;
-    // PAMG_CHAIN_EARLY (A/B): 0 publish after the down pass, 1 the words after the up pass, 2 (default) words and flag
-    static const int early_env = [] { const char *e = getenv("PAMG_CHAIN_EARLY"); return e ? atoi(e) : 2; }();
-    int early = L.words_up ? early_env : 0;
+    // PAMG_CHAIN_EARLY (A/B): 0 publish after the down pass, 1 the words after the up pass, 2 words and
+    // flag, 3 (default) as 2 with the up pass split around the wait (k_face_chain)
+    static const int early_env = [] { const char *e = getenv("PAMG_CHAIN_EARLY"); return e ? atoi(e) : 3; }();
+    int nui = L.nui, early = L.words_up ? early_env : 0;
+    // the split up pass needs each half's items in one item per thread
+    if (early == 3 && !(nui > 0 && (int64_t)k * nui <= kChainNT && (int64_t)k * (L.nup - nui) <= kChainNT)) early = 2;
     void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
-                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &early, &stamps};
+                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &stamps};
     // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
     const bool uni = L.nsub >= 64,
                lrec = k <= kChainRec && L.cpos && (int64_t)k * L.nup <= 2 * kChainNT && (int64_t)k * L.ndn <= kChainNT;

@@ -120,6 +120,7 @@ struct Level {
     // every sub-element with halo words (HaloPlan::hsub) is an up one: the chain publishes a
     // sweep's words right after its up pass (k_face_chain, early)
     bool words_up = false;
+    int nui = 0;   // up sub-elements without halo words per un_ele: cpos lists them first among the ups
     double *Ainv = nullptr;           // U_local * 9: FINDInv of (1/dt) M + Kd (coarse_solver = 1)
     double *blocks = nullptr;         // assembled per-sub-element operator (lazy, pamg_sweep_bench)
     // the persistent face chain (pamg_face.hip k_face_chain; lazy): its workgroups' neighbour lists
