@@ -815,7 +815,9 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
 // LREC: the workgroup's un_eles' operator records (FaceRec + omega / D) sit in LDS for the whole call
 // (at most kChainRec un_eles): the passes read them there instead of fetching them from memory in
 // every pass (the dependent record fetches were most of a sweep's pass time, r03 stamps)
-constexpr int kChainRec = 32, kRecW = 48;   // un_eles, doubles per record: S 13 | w 6 | WD 24 | sx 3
+constexpr int kChainRec = 32, kRecW = 48;
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+constexpr int kAuxSc1 = 16;   // buffer instruction cache policy: sc1 (through to the coherent level)   // un_eles, doubles per record: S 13 | w 6 | WD 24 | sx 3
 template <bool UNI, bool RB, bool LREC>
 __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *TNN, const double *SRC, const double *__restrict__ RHS,
                                                           const double *__restrict__ stc, const int4 *__restrict__ fnb,
@@ -1025,6 +1027,9 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
         for (int q = 0; q < 3; ++q) R.sx[q] = (int)rs[43 + q];
         f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
     };
+    // the snapshot's 16-byte loads: a face's 3m words and the slot pitch even (16-byte aligned pairs)
+    const bool snap16 = ((3 * m) & 1) == 0 && (slots & 1) == 0;
+    const int tin_bytes = (int)((N >> nsub_log2) * slots * 3 * 8);
     const int na = nb_off[w], nn = nb_off[w + 1] - na;
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
@@ -1063,10 +1068,23 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             }
         }
         __syncthreads();
-        // the snapshot of this workgroup's un_eles into LDS (every load of the handed-over words: ld_coh)
-        for (int idx = t; idx < nhalo; idx += NT) {
-            const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
-            HI[idx] = ld_coh(tin + (u0 + uk) * slots * 3 + (int64_t)mf * slots + off);
+        // the snapshot of this workgroup's un_eles into LDS (every load of the handed-over words
+        // through to the coherent level, sc1): 16 bytes a lane where a face's 3m words pair up
+        if (snap16) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(tin), (short)0, tin_bytes, 0x00020000);
+            for (int i2 = t; 2 * i2 < nhalo; i2 += NT) {
+                const int idx = 2 * i2;
+                const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
+                const int o = (int)(((u0 + uk) * slots * 3 + (int64_t)mf * slots + off) * 8);
+                const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kAuxSc1);
+                HI[idx] = __longlong_as_double(((long long)v.y << 32) | v.x);
+                HI[idx + 1] = __longlong_as_double(((long long)v.w << 32) | v.z);
+            }
+        } else {
+            for (int idx = t; idx < nhalo; idx += NT) {
+                const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
+                HI[idx] = ld_coh(tin + (u0 + uk) * slots * 3 + (int64_t)mf * slots + off);
+            }
         }
         // the call's last sweep: tnew := tnew_nonlin (:550), before the barrier that lets the passes
         // rewrite X (with item lists a position's item may belong to another thread)
