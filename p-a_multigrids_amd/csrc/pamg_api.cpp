@@ -453,6 +453,8 @@ int face_chain_setup(pamg_handle *h, int l) {
     // the polled words in one block of their own, a multiple of 16 bytes from the allocation's start
     L.chain_flag_bytes = ((size_t)G * sizeof(unsigned) + 15) / 16 * 16;
     CHK(dev_alloc(h, &L.chain_flags, L.chain_flag_bytes / sizeof(unsigned)));
+    HIPCHK(h, hipMemsetAsync(L.chain_flags, 0, L.chain_flag_bytes, h->stream));
+    L.chain_epoch = 0;
     if (!h->chain_tmo) {
         CHK(dev_alloc(h, &h->chain_tmo, 4));
         HIPCHK(h, hipMemsetAsync(h->chain_tmo, 0, 4 * sizeof(unsigned), h->stream));
@@ -631,12 +633,17 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
     unsigned tag0 = 0;
     if (run >= 2 && face_chain_ok(h, l)) {   // the whole call in one launch
         CHK(face_chain_setup(h, l));
-        HIPCHK(h, hipMemsetAsync(L.chain_flags, 0, L.chain_flag_bytes, h->stream));
+        if ((unsigned long long)L.chain_epoch + run + 2 >= 0xffffffffull) {   // the epoch would wrap: start over
+            HIPCHK(h, hipMemsetAsync(L.chain_flags, 0, L.chain_flag_bytes, h->stream));
+            L.chain_epoch = 0;
+        }
+        const unsigned f0 = L.chain_epoch;
+        L.chain_epoch += (unsigned)run + 1;
         // the state crosses HBM once per call: tnew_nonlin and RHS in, tnew (+ tnew_nonlin) out
         Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
         HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags, L.chain_nb_off,
                                     L.chain_nb_list, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
-                                    l == 1, rdt, h->p.omega, h->slots, src_is_T));
+                                    l == 1, rdt, h->p.omega, h->slots, src_is_T, f0));
         return PAMG_OK;
     }
     if (const int g = face_wave_grid_for(h, l, run)) {   // the call in one wavefront launch

@@ -827,7 +827,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                                                           unsigned *tmo, int run, int total, int store, int E,
                                                           int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                           double rdt, double omega, const int *__restrict__ cpos,
-                                                          int nup, int nui, int early, long long *stamps) {
+                                                          int nup, int nui, int early, unsigned f0, long long *stamps) {
     constexpr int NT = kChainNT, PER = kChainPer;
     // early (LREC red-black only; the host checked that every halo sub-element is an up one):
     // 1 a sweep's halo words go out right after its up pass, 2 and its flag, 3 as 2 with the up
@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                 bool ok = f == nullptr;
                 for (unsigned spins = 0;; ++spins) {
                     if (!ok) ok = __hip_atomic_load((g_u32 *)const_cast<unsigned *>(f), __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)sw;
+                                                    __HIP_MEMORY_SCOPE_AGENT) >= f0 + (unsigned)sw;
                     if (__all(ok)) break;
                     if (spins > (1u << 22)) {
                         if (t == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1110,7 +1110,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __syncthreads();
                         if (t == 0)
-                            __hip_atomic_store((g_u32 *)flags + w, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store((g_u32 *)flags + w, f0 + (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
                 items_pass<1>(IB, ixin, ihv, irec, level1, rdt, [&](int k, const double r[3]) {
@@ -1146,7 +1146,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             if (!(LREC && RB && early)) words(tout, sw);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (t == 0) __hip_atomic_store((g_u32 *)flags + w, (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0) __hip_atomic_store((g_u32 *)flags + w, f0 + (unsigned)(sw + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         stamp(3);
     }
@@ -1275,7 +1275,8 @@ bool face_chain_fits(int nsub, int U, int cus) {
 
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
-                             int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T) {
+                             int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T,
+                             unsigned f0) {
     if (L.N == 0 || run <= 0) return hipSuccess;
     if (!face_chain_fits(L.nsub, U, cus) || !L.fnb) return hipErrorInvalidValue;
     const int g = std::max(1, std::min(cus, U));
@@ -1310,7 +1311,7 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     // the split up pass needs each half's items in one item per thread
     if (early == 3 && !(nui > 0 && (int64_t)k * nui <= kChainNT && (int64_t)k * (L.nup - nui) <= kChainNT)) early = 2;
     void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
-                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &stamps};
+                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &f0, &stamps};
     // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
     const bool uni = L.nsub >= 64,
                lrec = k <= kChainRec && L.cpos && (int64_t)k * L.nup <= 2 * kChainNT && (int64_t)k * L.ndn <= kChainNT;

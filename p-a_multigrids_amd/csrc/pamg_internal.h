@@ -129,6 +129,9 @@ struct Level {
     int *chain_nb_off = nullptr, *chain_nb_list = nullptr;
     unsigned *chain_flags = nullptr;
     size_t chain_flag_bytes = 0;
+    // the flags' epoch: a chain call publishes epoch + s + 1 for its sweep s and the next call starts
+    // past every value published, so the flags are zeroed only at setup and on wrap
+    unsigned chain_epoch = 0;
     int arith = 0;                    // operator arithmetic of this level's kernels (pamg_params.arith)
     bool richardson = false;          // solver 2: the Richardson update (solve_Richardson, :511-518)
     HaloPlan halo;
@@ -364,7 +367,8 @@ hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, doub
 int face_chain_per_wg(int nsub, int U, int cus);
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
-                             int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T = false);
+                             int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T = false,
+                             unsigned f0 = 0);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg
