@@ -1028,8 +1028,10 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
         f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
     };
     // the snapshot's 16-byte loads: a face's 3m words and the slot pitch even (16-byte aligned pairs)
-    const bool snap16 = ((3 * m) & 1) == 0 && (slots & 1) == 0;
-    const int tin_bytes = (int)((N >> nsub_log2) * slots * 3 * 8);
+    // (and the snapshot buffer within a buffer resource's 32-bit range)
+    const int64_t tin_bytes64 = (N >> nsub_log2) * slots * 3 * 8;
+    const bool snap16 = ((3 * m) & 1) == 0 && (slots & 1) == 0 && tin_bytes64 < (1ll << 31);
+    const int tin_bytes = (int)std::min<int64_t>(tin_bytes64, (1ll << 31) - 1);
     const int na = nb_off[w], nn = nb_off[w + 1] - na;
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
