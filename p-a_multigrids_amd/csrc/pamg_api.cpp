@@ -376,31 +376,40 @@ int comm_error(pamg_handle *h) {
 
 // stream synchronisation that keeps polling RCCL's error state: a rank whose peer failed
 // returns PAMG_ERR_COMM (communicator aborted) instead of waiting on a receive that never
-// completes; PAMG_COMM_TIMEOUT_S, when set, also bounds the wait. The poll spins on the
-// stream's completion (hipStreamQuery) for its first 20 ms and checks the communicator every
-// 256th query, then sleeps 20 us between polls (the N = 8 rank's 20-cycle call: blocking
-// hipStreamSynchronize 150.3 us, this spin 154.2, a 20 us sleeping poll 155.3 -- within noise
-// of each other, profiles/r03_m_sync_probe.txt; the spin only removes the sleep's granularity)
+// completes; PAMG_COMM_TIMEOUT_S, when set, also bounds the wait. The device-copy transport
+// (pamg_comm_local_group) is polled the same way with its exchange bound (PAMG_COMM_TIMEOUT_S,
+// default 120 s): its resident call's comm stream waits on a device signal (hipStreamWaitValue64)
+// that a faulted or stopped launch would never raise. The poll sleeps 20 us between queries and
+// checks the communicator every 16th; PAMG_SYNC_SPIN_MS=<ms> spins on hipStreamQuery first (the
+// N = 8 rank's 20-cycle call: blocking hipStreamSynchronize 150.3 us, a 20 ms spin 154.2, the
+// sleeping poll 155.3 -- within noise of each other, profiles/r03_m_sync_probe.txt; a spin keeps a
+// core busy per rank for no measured gain, so it is off by default)
 int sync_stream(pamg_handle *h, hipStream_t s) {
-    if (!h->comm || !h->comm->nccl) {
+    if (!h->comm || (!h->comm->nccl && !h->comm->local)) {
         HIPCHK(h, hipStreamSynchronize(s));
         return PAMG_OK;
     }
     const char *env = getenv("PAMG_COMM_TIMEOUT_S");
-    const int limit = env ? atoi(env) : 0;   // unset: no limit, only the error polling
+    // unset: no limit on an RCCL rank (only the error polling), the exchange bound on a local group
+    const int limit = env ? atoi(env) : h->comm->local ? local_timeout_s() : 0;
+    static const int spin_ms = getenv("PAMG_SYNC_SPIN_MS") ? std::max(0, atoi(getenv("PAMG_SYNC_SPIN_MS"))) : 0;
     const auto t0 = std::chrono::steady_clock::now();
-    const auto spin_end = t0 + std::chrono::milliseconds(20);
+    const auto spin_end = t0 + std::chrono::milliseconds(spin_ms);
     for (unsigned i = 0;; ++i) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) return PAMG_OK;
         if (e != hipErrorNotReady) HIPCHK(h, e);
         const auto now = std::chrono::steady_clock::now();
-        if ((i & 255) != 255 && now < spin_end) continue;
-        CHK(comm_error(h));
+        if (now < spin_end && (i & 255) != 255) continue;
+        if ((i & 15) == 15 || now < spin_end) CHK(comm_error(h));
         if (limit > 0 && now - t0 > std::chrono::seconds(limit)) {
-            h->err = "stream did not drain within PAMG_COMM_TIMEOUT_S; RCCL communicator aborted";
-            (void)ncclCommAbort(h->comm->nccl);
-            h->comm->nccl = nullptr;
+            if (h->comm->nccl) {
+                h->err = "stream did not drain within PAMG_COMM_TIMEOUT_S; RCCL communicator aborted";
+                (void)ncclCommAbort(h->comm->nccl);
+                h->comm->nccl = nullptr;
+            } else {
+                h->err = "stream did not drain within PAMG_COMM_TIMEOUT_S (local-group transport)";
+            }
             return PAMG_ERR_COMM;
         }
         if (now >= spin_end) std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -556,14 +565,20 @@ int face_wave_grid_for(pamg_handle *h, int l, int run) {
     return g;
 }
 
-// the sticky give-up word of the chain's bounded spins: a call that hit it failed
+// the give-up word of the chain's and the wavefront's bounded spins: a call that hit it failed, and
+// the state it left was computed from halo words that had not all arrived -- the handle's fields are
+// invalid after the error (set them again, or start a new time step from a known tnew). Checked only
+// when such a launch ran since the last check (the other op = 1 calls stay asynchronous); the word is
+// cleared once reported, so the next call on the handle runs again.
 int face_chain_check(pamg_handle *h) {
-    if (!h->chain_tmo) return PAMG_OK;
+    if (!h->chain_tmo || !h->chain_pending) return PAMG_OK;
+    h->chain_pending = false;
     unsigned v = 0;
     HIPCHK(h, hipMemcpyAsync(&v, h->chain_tmo, sizeof v, hipMemcpyDeviceToHost, h->stream));
     CHK(sync_stream(h, h->stream));
     if (v) {
-        h->err = "face chain: a workgroup gave up waiting for its neighbours' halo words";
+        HIPCHK(h, hipMemsetAsync(h->chain_tmo, 0, sizeof v, h->stream));
+        h->err = "face chain: a workgroup gave up waiting for its neighbours' halo words (the state is invalid)";
         return PAMG_ERR_HIP;
     }
     return PAMG_OK;
@@ -641,6 +656,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
         L.chain_epoch += (unsigned)run + 1;
         // the state crosses HBM once per call: tnew_nonlin and RHS in, tnew (+ tnew_nonlin) out
         Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
+        h->chain_pending = true;
         HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags, L.chain_nb_off,
                                     L.chain_nb_list, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
                                     l == 1, rdt, h->p.omega, h->slots, src_is_T, f0));
@@ -650,6 +666,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
         CHK(tags(&g0, &g1, &tag0));
         // the state crosses HBM once per call, as the chain's
         Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
+        h->chain_pending = true;
         HIPCHK(h, launch_face_wave(h->stream, L, h->U, g, h->tov, h->tov_b, h->tovo, g0, g1, tag0, h->wave_flags,
                                    h->wave_order, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
                                    l == 1, rdt, h->slots, src_is_T));
@@ -1384,11 +1401,16 @@ int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int
     h->rank = rank;
     h->owner.assign(owner, owner + U);
     if (nranks > 1 && id) {   // id == NULL: detached partition (pamg_halo_loopback exchanges)
+        if (h->comm) { h->err = "communicator already bound"; return PAMG_ERR_STATE; }
         HIPCHK(h, hipSetDevice(h->device));
         ncclUniqueId uid;
         std::memcpy(&uid, id, 128);
+        // bound to the handle only once RCCL has initialised it (a failure leaves no half-bound
+        // communicator behind, so a retry can bind again)
+        ncclComm_t nc = nullptr;
+        NCCLCHK(h, ncclCommInitRank(&nc, nranks, uid, rank));
         h->comm = new Comm;
-        NCCLCHK(h, ncclCommInitRank(&h->comm->nccl, nranks, uid, rank));
+        h->comm->nccl = nc;
     }
     return PAMG_OK;
 }
@@ -1397,15 +1419,19 @@ int pamg_comm_init_self(pamg_handle *h, const char id[128], int U, const int *pa
     if (!h || !id || !part || U < 1) return PAMG_ERR_ARG;
     if (h->mesh_ready) { h->err = "pamg_comm_init_self must precede pamg_upload_mesh"; return PAMG_ERR_STATE; }
     if (h->comm) { h->err = "communicator already bound"; return PAMG_ERR_STATE; }
+    HIPCHK(h, hipSetDevice(h->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    // the plan and the communicator are bound only once RCCL has initialised it: a failure leaves
+    // the handle as it was (no half-bound communicator, no self-peer parts), so a retry can bind
+    ncclComm_t nc = nullptr;
+    NCCLCHK(h, ncclCommInitRank(&nc, 1, uid, 0));
     h->nranks = 1;
     h->rank = 0;
     h->owner.assign(U, 0);
     h->vpart.assign(part, part + U);
-    HIPCHK(h, hipSetDevice(h->device));
-    ncclUniqueId uid;
-    std::memcpy(&uid, id, 128);
     h->comm = new Comm;
-    NCCLCHK(h, ncclCommInitRank(&h->comm->nccl, 1, uid, 0));
+    h->comm->nccl = nc;
     return PAMG_OK;
 }
 

@@ -827,7 +827,8 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                                                           unsigned *tmo, int run, int total, int store, int E,
                                                           int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                           double rdt, double omega, const int *__restrict__ cpos,
-                                                          int nup, int nui, int early, unsigned f0, long long *stamps) {
+                                                          int nup, int nui, int early, unsigned f0, int snap_ok,
+                                                          long long *stamps) {
     constexpr int NT = kChainNT, PER = kChainPer;
     // early (LREC red-black only; the host checked that every halo sub-element is an up one):
     // 1 a sweep's halo words go out right after its up pass, 2 and its flag, 3 as 2 with the up
@@ -1028,9 +1029,10 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
         f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
     };
     // the snapshot's 16-byte loads: a face's 3m words and the slot pitch even (16-byte aligned pairs)
-    // (and the snapshot buffer within a buffer resource's 32-bit range)
+    // (and the snapshot buffer within a buffer resource's 32-bit range; snap_ok = 0 forces the 8-byte
+    // form, the path of a larger buffer -- PAMG_CHAIN_SNAP16=0, tests/test_face_operator.py)
     const int64_t tin_bytes64 = (N >> nsub_log2) * slots * 3 * 8;
-    const bool snap16 = ((3 * m) & 1) == 0 && (slots & 1) == 0 && tin_bytes64 < (1ll << 31);
+    const bool snap16 = snap_ok && ((3 * m) & 1) == 0 && (slots & 1) == 0 && tin_bytes64 < (1ll << 31);
     const int tin_bytes = (int)std::min<int64_t>(tin_bytes64, (1ll << 31) - 1);
     const int na = nb_off[w], nn = nb_off[w + 1] - na;
     for (int sw = 0; sw < run; ++sw) {
@@ -1312,8 +1314,13 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     int nui = L.nui, early = L.words_up ? early_env : 0;
     // the split up pass needs each half's items in one item per thread
     if (early == 3 && !(nui > 0 && (int64_t)k * nui <= kChainNT && (int64_t)k * (L.nup - nui) <= kChainNT)) early = 2;
+    // PAMG_CHAIN_SNAP16=0: the snapshot's 8-byte loads, the form a snapshot buffer beyond a buffer
+    // resource's 32-bit range takes (read per launch: a test switches it within a process)
+    const char *snap_env = getenv("PAMG_CHAIN_SNAP16");
+    int snap_ok = !(snap_env && atoi(snap_env) == 0);
     void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
-                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &f0, &stamps};
+                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &f0,
+                    &snap_ok, &stamps};
     // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
     const bool uni = L.nsub >= 64,
                lrec = k <= kChainRec && L.cpos && (int64_t)k * L.nup <= 2 * kChainNT && (int64_t)k * L.ndn <= kChainNT;

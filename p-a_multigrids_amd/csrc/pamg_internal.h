@@ -207,7 +207,8 @@ struct pamg_handle {
     double *scratch = nullptr; size_t scratch_bytes = 0;
     // op = 1: the local un_eles' neighbours (0-based local ids, -1: none or another rank), 3 per un_ele
     std::vector<int> neig_local;
-    unsigned *chain_tmo = nullptr;   // sticky give-up word of the face chain's bounded spins
+    unsigned *chain_tmo = nullptr;   // give-up word of the face chain's / wavefront's bounded spins
+    bool chain_pending = false;      // a chain or wavefront launch ran since face_chain_check last read it
     // the face operator's wavefront calls (k_face_wave; lazy, single domain): the ticket order (a
     // reverse Cuthill-McKee numbering of neig_local), its band, the neighbours on the device and the
     // per-un_ele flags + ticket counter

@@ -5,8 +5,8 @@ import os
 import sys
 import time
 
-import torch  # noqa: F401  (as bench.py: the HIP runtime comes up through torch; a bare process
-#              segfaulted in its exit handlers under rocprofv3, profiles/r03_final)
+if os.environ.get("PAMG_PROBE_TORCH", "1") != "0":
+    import torch  # noqa: F401  (as bench.py: the HIP runtime comes up through torch)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "p-a_multigrids_amd"))
@@ -38,3 +38,7 @@ for cycle in CYCLES:
             print(f"   {k:14s} {v['launches'] // n:4d} launches/cycle {ms:.4f} ms/cycle "
                   f"{v['bytes'] / (v['ms'] * 1e-3) / 1e9 if v['ms'] else 0:.0f} GB/s (algorithmic)", flush=True)
     s.close()
+# PAMG_PROBE_MAPS=<path>: the process's mappings at the end (resolves the PCs of a crash at exit)
+if os.environ.get("PAMG_PROBE_MAPS"):
+    with open("/proc/self/maps") as f, open(os.environ["PAMG_PROBE_MAPS"], "w") as o:
+        o.write(f.read())

@@ -99,12 +99,33 @@ def assert_identical(sg, so):
     # the fused single-domain sweep's tiles of 1,024 and 4,096 sub-elements
     ("irregular.msh", 5, 3, 3, 2), ("irregular.msh", 6, 2, 3, 1), ("irregular.msh", 6, 2, 1, 1),
     # one sweep per call (every sweep of the fused cycle's non-final calls is dead), one level
-    ("irregular.msh", 4, 3, 3, 1), ("untitled8.msh", 3, 1, 3, 2)])
+    ("irregular.msh", 4, 3, 3, 1), ("untitled8.msh", 3, 1, 3, 2),
+    # bench.py's extra.op1 configuration (untitled8192, n_split 5, L 3, n_smooth 4, solver 3): level 3
+    # (64 sub-elements per un_ele, m = 8 face positions) runs as the persistent chain -- 256 cooperating
+    # workgroups handing the halo words over inside the launch, the split up pass and the 16-byte
+    # write-through snapshot loads (buffer_load_dwordx4 sc1) -- and Jacobi on the same chain
+    ("untitled8192.msh", 5, 3, 3, 4), ("untitled8192.msh", 5, 3, 1, 4)])
 @pytest.mark.parametrize("cycle", [0, 1])
 def test_face_operator_is_bitwise_the_oracle(mesh, S, L, solver, ns, cycle):
     g, o = gpu_pair(mesh, S, L, solver, cycle, ns)
     drive(g, False, cycle)
     drive(o, True, cycle)
+    sg, so = g.state(), o.state()
+    sg["t_overlap"], sg["t_overlap_old"] = g.overlap()
+    so["t_overlap"], so["t_overlap_old"] = o.overlap()
+    assert_identical(sg, so)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("solver", [3, 1])
+def test_face_chain_8byte_snapshot_is_bitwise_the_oracle(solver, monkeypatch):
+    """The chain's snapshot falls back to 8-byte write-through loads when the snapshot buffer exceeds a
+    buffer resource's 32-bit range (pamg_face.hip k_face_chain, snap16); PAMG_CHAIN_SNAP16=0 forces that
+    form on bench.py's extra.op1 configuration, which must stay bitwise the oracle."""
+    monkeypatch.setenv("PAMG_CHAIN_SNAP16", "0")
+    g, o = gpu_pair("untitled8192.msh", 5, 3, solver, 0, 4)
+    drive(g, False, 0)
+    drive(o, True, 0)
     sg, so = g.state(), o.state()
     sg["t_overlap"], sg["t_overlap_old"] = g.overlap()
     so["t_overlap"], so["t_overlap_old"] = o.overlap()
