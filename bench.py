@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # lanes x 2 flops x 2.4 GHz)
 FP64_PEAK_TFLOPS = 78.6
 EVENT_STRIDE = 10
-ALL_CLASSES = 0x3F7F   # every timing class (PAMG_K_*) but sweep_bench
+ALL_CLASSES = 0x7F7F   # every timing class (PAMG_K_*) but sweep_bench
 
 
 def parse():
@@ -284,6 +284,48 @@ def measure_face(pamg, m, S, L, device, cycles=20):
                                             frac=round(gbs / HBM_PEAK_GBS, 4),
                                             ms_per_sweep=round(k1["ms"] / k1["launches"], 4))
     s.close()
+    return out
+
+
+def measure_corrected(pamg, m, S, L, ns, arith, device, cycles=200):
+    """the corrected V-cycle (cycle = 1: the fresh residual restricted, coarse
+    levels from zero, the interpolated coarse correction added) on the benchmarked workload. A
+    pamg_vcycle call runs as one resident launch (k_vc_corr, every level of a tile on-chip between the
+    cycles; bitwise the per-step sequence, tests/test_corrected.py): V-cycles/s of a `cycles`-cycle
+    call after a warm-up call, the launch's fp64 roofline from an evented pass, and the per-step
+    kernel sequence beside it (fused = 0, 20 cycles)"""
+    s = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=3, device=device, arith=arith, cycle=1)
+    s.begin_timestep()
+    s.vcycle(cycles)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.vcycle(cycles)
+    s.synchronize()
+    v = cycles / (time.perf_counter() - t0)
+    s.timing_enable(1 << 14)   # PAMG_K_VCYCLE_CORR
+    s.timing_stride(1)
+    s.timing_reset()
+    s.vcycle(cycles)
+    s.synchronize()
+    k = s.timing()["vcycle_corr"]
+    out = dict(workload=f"corrected V-cycle (cycle=1), n_split={S} L={L} n_smooth={ns} GS, one pamg_vcycle({cycles}) "
+                        "call = one resident launch", vcycles_per_s=round(v, 1))
+    if k["launches"]:
+        ms = k["ms"] / k["launches"]
+        fl = s.vcycle_flops() * cycles
+        out.update(launch_ms=round(ms, 4), fp64_flops_per_cycle=s.vcycle_flops(),
+                   fp64_tflops=round(fl / (ms * 1e-3) / 1e12, 2),
+                   fp64_frac=round(fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4))
+    s.close()
+    s0 = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=3, device=device, arith=arith, cycle=1, fused=0)
+    s0.begin_timestep()
+    s0.vcycle(3)
+    s0.synchronize()
+    t0 = time.perf_counter()
+    s0.vcycle(20)
+    s0.synchronize()
+    out["per_step_vcycles_per_s"] = round(20 / (time.perf_counter() - t0), 1)
+    s0.close()
     return out
 
 
@@ -529,6 +571,7 @@ def main():
             extra[tag] = measure_workload(pamg, m_, S_, a.levels, a.nsmooth, a.arith, device)
         # the face-coupled operator on the benchmarked mesh, n_split 5, 3 levels
         extra["op1"] = measure_face(pamg, mesh, a.nsplit, 3, device)
+        extra["cycle1"] = measure_corrected(pamg, mesh, a.nsplit, a.levels, a.nsmooth, a.arith, device)
     if world > 1 and not a.no_extra:
         # the other exchange mode on the same partition (timed region the same shape): halo words
         # exchanged after every cycle, overlapped with the next one

@@ -63,7 +63,8 @@ extern "C" {
 #define PAMG_K_VCYCLE_RHSF 11    /* the pipelined launch that starts a pamg_run step (told, RHS) */
 #define PAMG_K_VCYCLE_RES 12     /* resident V-cycle call: every cycle of a pamg_vcycle call in one launch */
 #define PAMG_K_VCYCLE_RES_RHSF 13 /* the resident launch that starts a pamg_run step */
-#define PAMG_K_COUNT 14
+#define PAMG_K_VCYCLE_CORR 14    /* the corrected V-cycle's resident call (cycle = 1): a pamg_vcycle call in one launch */
+#define PAMG_K_COUNT 15
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;
@@ -108,8 +109,10 @@ typedef struct {
                          1: the corrected V-cycle of SURVEY.md 8(f) rank 2 -- the restrictor acts on
                          the fresh residual b - A x, coarse levels start from zero, the prolonged
                          correction (P1 interpolation of the coarse iterate) is added to the iterate
-                         the next smoother call starts from; per-step kernels; no reference output
-                         exists, pinned to the oracle's restatement */
+                         the next smoother call starts from; a pamg_vcycle call runs as one resident
+                         launch (every level of a tile on-chip between the cycles; op 0, coarse_solver 0,
+                         fused != 0, halo_exchange 0), else as the per-step kernels -- the state is the
+                         same bit for bit; no reference output exists, pinned to the oracle's restatement */
     int op;           /* 0 (default): the reference's mode-9 operator, block diagonal (its surface terms are
                          commented out, transport_tri_semi.F90:619-688); 1: the face-coupled interior-penalty
                          diffusion operator of SURVEY.md 8(f) rank 1 -- the surface terms with

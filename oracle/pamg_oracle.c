@@ -1196,8 +1196,16 @@ static void residual_corrected(orc_state *s, int l) {
     for (int u = 0; u < s->U; ++u) {
         double M[3][3], Kd[3][3], ml[3];
         stencil(s->detwei[l - 1] + 3 * u, (double (*)[2][NLOC])(s->nx[l - 1] + 18 * (size_t)u), s->c.k, M, Kd, ml);
+        double Ae[3][3], w[3];
+        if (s->c.arith == 1) contracted_ops(M, Kd, ml, rdt, s->c.omega, Ae, w);
         for (int se = 1; se <= nsub; ++se) {
             size_t o = (size_t)3 * ((size_t)u * nsub + se - 1);
+            if (s->c.arith == 1) {   /* the build's contracted arithmetic: -(A x - b) of the fma rows */
+                double r[3];
+                contracted_residual(Ae, T + o, R + o, r);
+                for (int i = 0; i < 3; ++i) s->res[l - 1][o + i] = -r[i];
+                continue;
+            }
             double A[3], mo[3];
             get_A_x(s, M, Kd, rdt, T + o, To + o, A, mo);
             for (int i = 0; i < 3; ++i) s->res[l - 1][o + i] = R[o + i] - A[i];

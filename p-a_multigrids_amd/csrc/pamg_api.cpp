@@ -872,12 +872,26 @@ double vcycle_res_bytes(pamg_handle *h, int keep, bool rhsf) {
 // the coarsest n_smooth (1 + n_coarse) - 2; only a call's last cycle also runs level 1's final
 // sweep, whose tnew_nonlin it stores (not counted here)
 int call_schedule(pamg_handle *h);
+bool corrected_resident_ok(pamg_handle *h);
 double vcycle_flops(pamg_handle *h) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth, nc = h->p.n_coarse;
     const bool f = h->p.arith == 1 && h->p.solver != 2;
     // Richardson's update is x + omega b (a multiply and an add per component), its residual the
     // reference's order
     const double sw = h->p.solver == 2 ? 6.0 : f ? 24.0 : 42.0, rs = f ? 18.0 : 36.0;
+    if (h->p.cycle == 1) {
+        // the corrected cycle: every sweep is live -- a level l < L runs two calls of n_smooth sweeps, the
+        // fresh residual and its mean (3), and takes the interpolated correction (3 adds per sub-element,
+        // the three midpoints, 9 flops, per coarse parent); the coarsest n_coarse calls from zero; the fine
+        // residual after the cycle only in a call's last cycle (not counted)
+        double fl = 0.0;
+        for (int l = 1; l <= L; ++l) {
+            const double n = (double)h->lv[l].N;
+            if (l < L) fl += n * (2.0 * ns * sw + rs + 3.0 + 3.0) + 9.0 * (double)h->lv[l + 1].N;
+            else fl += n * ((double)ns * (L > 1 ? nc : 1) * sw + (L > 1 ? 0.0 : rs));
+        }
+        return fl;
+    }
     // the resident kernels (call schedule 3) do not compute the dead prolongator (pamg_vcycle.hip
     // k_vc_res, k_vc_resb); every other fused form executes its cascade
     const bool prolong = !(call_schedule(h) == 3 && vcycle_resident_supported(h->p.n_split, L));
@@ -1028,6 +1042,53 @@ int vcycle_corrected(pamg_handle *h) {
     return PAMG_OK;
 }
 
+// the corrected cycle as one resident launch per pamg_vcycle call (pamg_vcycle_impl.h k_vc_corr): the
+// call's cycles with every level of a tile on-chip, the state stored once at the end -- bitwise the
+// per-step sequence above (tests/test_corrected.py). The halo words of the state are the last smoother
+// call's, level 1's post-smoothing call of the last cycle (every coarser level writes a subset of its
+// slots before it): its tnew words are written by the launch, the words constant within a time step by
+// k_overlap_static, the remote ones exchanged after the call (halo_exchange = 0). PAMG_NO_CORR_RESIDENT
+// (A/B) keeps the per-step sequence.
+int call_schedule(pamg_handle *h);
+bool corrected_resident_ok(pamg_handle *h) {
+    static const bool off = getenv("PAMG_NO_CORR_RESIDENT") != nullptr;
+    return !off && h->p.cycle == 1 && h->p.fused != 0 && h->p.op == 0 && h->p.coarse_solver == 0 && h->p.solver != 2 &&
+           h->p.halo_exchange == 0 && h->p.n_smooth > 0 && call_schedule(h) == 3 &&
+           vcycle_corrected_supported(h->p.n_split, h->p.multi_levels);
+}
+
+// algorithmic HBM bytes of the corrected resident call: level 1 reads tnew and RHS and writes tnew,
+// tnew_nonlin and the residual (120 B); a level between writes RHS, residual, tnew, tnew_nonlin (96 B);
+// the coarsest RHS, tnew, tnew_nonlin (72 B); the operator words (104 B per un_ele and level)
+double vcycle_corr_bytes(pamg_handle *h) {
+    const int L = h->p.multi_levels;
+    double b = 120.0 * h->lv[1].N;
+    for (int l = 2; l <= L; ++l) b += (l < L ? 96.0 : 72.0) * h->lv[l].N;
+    return b + 104.0 * h->U * L;
+}
+
+int overlap_static_once(pamg_handle *h);
+int vcycle_corrected_resident(pamg_handle *h, int n) {
+    if (n <= 0) return PAMG_OK;
+    const int L = h->p.multi_levels;
+    HaloPlan &P1 = h->lv[1].halo;
+    CHK(overlap_static_once(h));
+    const int buf = P1.d_send_b ? 1 - P1.send_cur : 0;
+    if (h->sent_pending[buf]) {   // the exchange that read this buffer
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_sent[buf], 0));
+        h->sent_pending[buf] = false;
+    }
+    h->rhsn_valid = false;   // residuals and coarse RHS rewritten (RHSN does not follow them)
+    {
+        Span sp(h, PAMG_K_VCYCLE_CORR, vcycle_corr_bytes(h));
+        HIPCHK(h, launch_vcycle_corrected(h->stream, h->lv, L, h->U, h->p.n_split, h->p.n_smooth, h->p.n_coarse,
+                                          1 / h->p.dt, h->tov, h->tovo, P1.send_buf(buf), h->lv[2].RHSN, PAMG_KEEP_ALL, n));
+    }
+    h->tnn_level = 1;
+    CHK(halo_async(h, buf));
+    return join_comm(h);
+}
+
 // n V-cycles as two fused launches each (pamg_vcycle.hip)
 // pipelined-call schedule (pamg_set_call_schedule; PAMG_CALL_SCHEDULE=<s> overrides for A/B runs)
 // 0 automatic: the resident form where it applies (two levels or more, the halo words exchanged
@@ -1052,6 +1113,19 @@ bool fused_ok(pamg_handle *h) {
 }
 
 
+// once per time step: the level-1 halo words the cycle's last smoother call leaves constant
+// (t_overlap_old, the boundary words, the told halves of the send entries -- into both send buffers)
+int overlap_static_once(pamg_handle *h) {
+    if (h->overlap_static_l1) return PAMG_OK;
+    HaloPlan &P1 = h->lv[1].halo;
+    CHK(join_comm(h));
+    HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, nullptr, h->told_halo_stale_l1));
+    h->told_halo_stale_l1 = false;
+    if (P1.d_send_b) HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, P1.d_send_b));
+    h->overlap_static_l1 = true;
+    return PAMG_OK;
+}
+
 // dead_after (pamg_run, every step but the last): the next call rewrites the fields this one
 // leaves for an observer -- level 1's residual and tnew_nonlin, the coarse levels' RHS and
 // residual, the halo words -- before any read (nothing reads t_overlap, the next step's first
@@ -1072,15 +1146,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
     // once per time step: the halo words the cycle's last smoother leaves constant (into both
     // send buffers); when this call starts a pamg_run step whose told and RHS its first level-1
     // launch computes (rhs_pending), after that launch, as it reads told
-    auto overlap_static = [&]() -> int {
-        if (h->overlap_static_l1) return PAMG_OK;
-        CHK(join_comm(h));
-        HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, nullptr, h->told_halo_stale_l1));
-        h->told_halo_stale_l1 = false;
-        if (two) HIPCHK(h, launch_overlap_static(h->stream, h->lv[1], h->U, h->tov, h->tovo, P1.d_send_b));
-        h->overlap_static_l1 = true;
-        return PAMG_OK;
-    };
+    auto overlap_static = [&]() -> int { return overlap_static_once(h); };
     const bool rhs_first = h->rhs_pending;
     h->rhs_pending = false;
     if (!rhs_first) CHK(overlap_static());
@@ -1814,6 +1880,7 @@ int pamg_prolongator(pamg_handle *h, int level) {
 int vcycle(pamg_handle *h, int n, bool dead_after) {
     CHK(check_level(h, 1));
     if (h->p.cycle == 1) {
+        if (corrected_resident_ok(h)) return vcycle_corrected_resident(h, n);
         for (int c = 0; c < n; ++c) CHK(vcycle_corrected(h));
         return PAMG_OK;
     }

@@ -19,6 +19,9 @@
 // dropped (profiles/r03_c_face_ab.txt).
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
 #include "pamg_device.h"
 #include "pamg_internal.h"
 
@@ -1264,6 +1267,38 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
     return hipGetLastError();
 }
 
+// Launch of a grid whose workgroups wait on each other (k_face_chain, k_face_wave): it must be resident
+// at once. hipLaunchCooperativeKernel checks that, but a process that used it crashed at exit under
+// rocprofv3's kernel trace -- SIGSEGV inside libhsa-runtime64, called from libamdhip64's exit-time
+// teardown, on a GPU mapping already gone (profiles/r04_a_face_exit.txt; the same probe without the
+// chain exits cleanly). So the grid is checked against the same occupancy bound the cooperative launch
+// checks (workgroups per CU x CUs) and launched as a plain kernel: on the stream's turn every workgroup
+// of such a grid is dispatched at once, and every in-kernel wait is bounded (the give-up word tmo), so a
+// grid that did not become resident ends in PAMG_ERR_HIP, never in a hang. PAMG_CHAIN_COOP=1 restores
+// the cooperative launch (A/B).
+static hipError_t launch_coresident(const void *f, int grid, int nt, void **args, hipStream_t s) {
+    static const bool coop = getenv("PAMG_CHAIN_COOP") && atoi(getenv("PAMG_CHAIN_COOP")) != 0;
+    if (coop) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(nt), args, 0, s);
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, int> cap;   // co-resident workgroups per (kernel, block)
+    int n = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cap.find({f, nt});
+        if (it == cap.end()) {
+            int dev = 0, cus = 0, per = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, nt, 0);
+            if (e != hipSuccess) return e;
+            it = cap.emplace(std::make_pair(f, nt), per * cus).first;
+        }
+        n = it->second;
+    }
+    if (grid > n) return hipErrorCooperativeLaunchTooLarge;
+    return hipLaunchKernel(f, dim3(grid), dim3(nt), args, 0, s);
+}
+
 int face_chain_per_wg(int nsub, int U, int cus) {
     const int g = std::max(1, std::min(cus, U));
     const int k = (U + g - 1) / g;
@@ -1329,7 +1364,7 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     const void *f = uni ? (rb ? PAMG_CHF(true, true) : PAMG_CHF(true, false))
                         : (rb ? PAMG_CHF(false, true) : PAMG_CHF(false, false));
 #undef PAMG_CHF
-    hipError_t e = hipLaunchCooperativeKernel(f, dim3(grid), dim3(kChainNT), args, 0, s);
+    hipError_t e = launch_coresident(f, grid, kChainNT, args, s);
     if (stamp_path) {
         std::vector<long long> h(nst);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -1405,7 +1440,7 @@ hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, doub
     const double *SRC = from_T ? L.T : L.TNN;
     void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &cpos, &nup, &tov, &tov_b, &g0, &g1, &tag0, &H, &flags,
                     &order, &tmo, &U, &run, &total, &store, &pitch, &slots, &l1, &rdt, &stamps};
-    e = hipLaunchCooperativeKernel(f, dim3(g), dim3(nt), args, 0, s);
+    e = launch_coresident(f, g, nt, args, s);
     if (stamp_path) {
         std::vector<long long> hs(nst);
         if (e == hipSuccess) e = hipStreamSynchronize(s);

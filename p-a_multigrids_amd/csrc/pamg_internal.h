@@ -316,6 +316,13 @@ hipError_t launch_vcycle_resident_xc(hipStream_t s, const Level *lv, int L, int 
                                      double *rhsn2, int keep, int cycles, double *ring, int64_t ring_stride,
                                      unsigned *xc_done, unsigned long long *xc_sig);
 bool vcycle_resident_supported(int n_split, int L);
+// the corrected V-cycle (pamg_params.cycle = 1) as one resident launch per call (k_vc_corr): `cycles`
+// cycles, every level of a tile on-chip, the final state and level 1's halo words stored at the end
+// (keep & PAMG_KEEP_HALO; remote words packed into send1); the state is the per-step sequence's
+hipError_t launch_vcycle_corrected(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                                   int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
+                                   int keep, int cycles);
+bool vcycle_corrected_supported(int n_split, int L);
 bool vcycle_resident_run_supported(int n_split, int L);
 hipError_t launch_restrict_residual(hipStream_t s, const Level &fine, const Level &coarse, double rdt);
 hipError_t launch_to_soa(hipStream_t s, const Level &L, const double *aos, double *soa);

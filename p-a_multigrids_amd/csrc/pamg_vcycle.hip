@@ -188,6 +188,20 @@ hipError_t launch_vcycle_resident_xc(hipStream_t s, const Level *lv, int L, int 
                        cycles, 1, &X);
 }
 
+// the resident corrected call (k_vc_corr): `cycles` corrected V-cycles in one launch
+hipError_t launch_vcycle_corrected(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
+                                   int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
+                                   int keep, int cycles) {
+    if (!vcycle_corrected_supported(n_split, L)) return hipErrorInvalidValue;
+    return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, rhsn2, 7, keep, 0, -1, nullptr,
+                       cycles, 1);
+}
+
+bool vcycle_corrected_supported(int n_split, int L) {
+    return L >= 2 && L <= kMaxFusedLevels && n_split >= L && n_split <= kMaxFusedSplit && fine_np(n_split) == 2 &&
+           fine_tl(n_split) == 10;
+}
+
 // several time steps in one resident launch (k_vc_resb, or k_vc_res below n_split 5 and at L = 2)
 bool vcycle_resident_run_supported(int n_split, int L) {
     return L >= 2 && L <= kMaxFusedLevels && n_split <= kMaxFusedSplit && fine_np(n_split) == 2;

@@ -1638,6 +1638,250 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     }
 }
 
+// ===================================================================== resident corrected call
+// The corrected V-cycle (pamg_params.cycle = 1; pamg_api.cpp vcycle_corrected,
+// oracle orc_vcycle_corrected): the reference's levels, smoother (transport_tri_semi.F90:491-507),
+// residual (:725-873, with the b - A x sign), restrictor (splitting.F90:10-32, 146-151) and the P1
+// interpolation its prolongator cascade encodes (splitting.F90:59-88), with the defects of the
+// reference's cycle (SURVEY.md A3 iii/iv) fixed: the restrictor acts on the fresh residual, coarse
+// levels start from zero, the interpolated coarse correction is added to the iterate the next smoother
+// call starts from. Unlike the reference's cycle every step depends on the one before it -- level l's
+// post-smoothing needs level l+1's result of the same cycle -- so a tile cannot run its levels at once.
+// It can still keep the whole cycle on-chip: every operation stays inside a tile (an un_ele's
+// sub-elements of every level), so one workgroup carries its tile through all the cycles
+// of a pamg_vcycle call, the state in registers, and only the values that cross threads go through LDS:
+//   step 0          level 0 (the reference's level 1): n_smooth sweeps from tnew, the fresh residual
+//                   b - A x, its means (the restrictor's input) into LDS;
+//   step l < C      level l: RHS := restrictor of level l-1's means, tnew := 0, n_smooth sweeps, the
+//                   residual's means into LDS;
+//   step C          the coarsest level: RHS, tnew := 0, n_coarse smoother calls; tnew into LDS;
+//   step 2C - l     level l (C > l >= 1): tnew += P tnew_{l+1} (from LDS), n_smooth sweeps, tnew into LDS;
+//   step 2C         level 0: tnew += P tnew_1, n_smooth sweeps; the call's last cycle stores the state,
+//                   the halo words of the last smoother call and the fine residual after the cycle.
+// One barrier closes each step but the last (2C per cycle); a step's LDS buffer is rewritten only one
+// cycle later, behind the barriers its readers passed. Threads: level 0 on all 512 (an adjacent pair
+// each), level 1 on waves 4-7 (one sub-element per thread, one wave per SIMD: waves w and w + 4 share
+// one), level l >= 2 on wave l - 2 -- no thread holds two coarse levels, and each role runs its own
+// cycle loop (unswitched, so one role's loop-carried registers are not reserved in another's).
+// Every sweep, residual, mean and interpolation is the per-step kernels' device code on the same
+// values in the same order (pamg_kernels.hip k_smooth, k_residual<.., NEG>, k_restrict_tile,
+// k_interp_add): the state after the call is bitwise the per-step sequence's (tests/test_corrected.py).
+#ifndef PAMG_CORR_WAVES
+#define PAMG_CORR_WAVES 6
+#endif
+template <int S, int L>
+struct KGeo {
+    using G = Geo<S, L>;
+    static constexpr int C = G::C;
+    // LDS: the residual means of levels 0 .. C-1, then the iterates of levels 1 .. C (3 planes each)
+    static constexpr int MO(int l) { int o = 0; for (int i = 0; i < l; ++i) o += G::nt(i); return o; }
+    static constexpr int TO(int l) { int o = MO(C); for (int i = 1; i < l; ++i) o += 3 * G::nt(i); return o; }
+    static constexpr int SIZE = TO(C + 1);
+};
+
+// negated residual (the corrected cycle's b - A x, k_residual<.., NEG>) and the restrictor's mean of it
+template <class ST>
+__device__ __forceinline__ double neg_resid_mean(const ST &St, double rdt, const double x[3], const double b[3],
+                                                 double n[3]) {
+    double r[3];
+    resid(St, rdt, x, b, r);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) n[c] = -r[c];
+    return div3(n[0] + n[1] + n[2]);
+}
+
+// tnew += P y for child q (0..3, element_conversion's order) of the coarse sub-element whose tnew is y
+// (k_interp_add, the P1 interpolation of the prolongator cascade, splitting.F90:59-88)
+__device__ __forceinline__ void interp_add(double x[3], int q, const double y[3]) {
+    const double m20 = 0.5 * y[2] + 0.5 * y[0], m12 = 0.5 * y[1] + 0.5 * y[2], m01 = 0.5 * y[0] + 0.5 * y[1];
+    double a0, a1, a2;
+    switch (q) {
+        case 0: a0 = m20; a1 = m12; a2 = y[2]; break;
+        case 1: a0 = m12; a1 = m20; a2 = m01; break;
+        case 2: a0 = y[0]; a1 = m01; a2 = m20; break;
+        default: a0 = m01; a1 = y[1]; a2 = m12; break;
+    }
+    x[0] = x[0] + a0;
+    x[1] = x[1] + a1;
+    x[2] = x[2] + a2;
+}
+
+template <int S, int L, class ST>
+__global__ __launch_bounds__(512, PAMG_CORR_WAVES) void k_vc_corr(VArgs A, const double *__restrict__ sp0,
+                                                                  const double *__restrict__ sp1,
+                                                                  const double *__restrict__ sp2,
+                                                                  const double *__restrict__ sp3,
+                                                                  const double *__restrict__ sp4) {
+    using G = Geo<S, L>;
+    using K = KGeo<S, L>;
+    constexpr int C = G::C, T = G::T;
+    static_assert(C >= 1 && C <= 4 && T == 1024 && G::MT == 512 && G::NP == 2, "corrected resident call: 1024-element tiles, L 2..5");
+    __shared__ __attribute__((aligned(16))) double LB[K::SIZE];
+    const double *__restrict__ SP[kMaxFusedLevels] = {sp0, sp1, sp2, sp3, sp4};
+    const int t = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    auto lane_id = [] { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); };
+    const double rdt = A.rdt;
+    const int ns = A.n_smooth, m = A.cycles;
+    const int64_t tb = (int64_t)blockIdx.x + A.tile0;
+    const bool keeph = A.keep & kKeepHalo;
+    const VLevel &V0 = A.lv[0];
+    constexpr int hmask = (1 << G::lg(0)) - 1;
+    // level 0: the thread's adjacent pair (tile-local 2t, 2t + 1): tnew and the RHS, for the whole call
+    bool v0;
+    const uint32_t s0 = tile_index<S>(A, tb, T, 0, 2 * t, v0);
+    const uint32_t w0 = s0 >> G::lg(0);
+    double x0[2][3], b0[2][3];
+    load3p<PAMG_NT_TL>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
+    load3p<PAMG_NT_RL>(V0.RHS(), V0.pitch, s0, b0[0], b0[1]);
+    // the role: the coarse level lo the thread owns (0: none) -- level 1 on waves 4-7, level l >= 2 on wave l-2
+    auto role = [&](auto loc) {
+        constexpr int lo = decltype(loc)::value;
+        bool vs = false;
+        uint32_t gs = 0;
+        int is = 0;
+        if constexpr (lo > 0) {
+            is = lo == 1 ? t - 256 : lane_id();
+            gs = tile_index<S>(A, tb, G::nt(lo), lo, is, vs);
+        }
+        double xs[3], bs[3];
+        auto cycle = [&](auto lastc) {
+            constexpr bool last = decltype(lastc)::value;
+            // ---- step 0: level 0's pre-smoothing call (:331) from tnew, its fresh residual, the means
+            {
+                ST St;
+                stencil(G::uni(0), sp0, opaque(w0), St);
+                for (int it = 0; it < ns; ++it) {
+                    sweep(St, rdt, b0[0], x0[0]);
+                    sweep(St, rdt, b0[1], x0[1]);
+                }
+                double n[3];
+                const double a = neg_resid_mean(St, rdt, x0[0], b0[0], n);
+                const double b = neg_resid_mean(St, rdt, x0[1], b0[1], n);
+                if (v0) *reinterpret_cast<double2 *>(LB + K::MO(0) + 2 * t) = make_double2(a, b);
+            }
+            __syncthreads();
+            // ---- steps 1 .. C-1: level l from zero, RHS the restriction of level l-1's residual
+            static_for<1, C>([&](auto lc) {
+                constexpr int l = decltype(lc)::value;
+                if constexpr (lo == l) {
+                    const double *Mf = LB + K::MO(l - 1);
+                    bs[0] = Mf[4 * is + 2];
+                    bs[1] = Mf[4 * is + 3];
+                    bs[2] = Mf[4 * is];
+                    xs[0] = xs[1] = xs[2] = 0.0;
+                    ST St;
+                    stencil(G::uni(l), SP[l], opaque(gs >> G::lg(l)), St);
+                    for (int it = 0; it < ns; ++it) sweep(St, rdt, bs, xs);
+                    double n[3];
+                    const double mn = neg_resid_mean(St, rdt, xs, bs, n);
+                    if (vs) {
+                        LB[K::MO(l) + is] = mn;
+                        if (last) {
+                            const VLevel &V = A.lv[l];
+                            store3(V.RHS(), V.pitch, gs, bs);
+                            store3(V.RES(), V.pitch, gs, n);
+                        }
+                    }
+                }
+                __syncthreads();
+            });
+            // ---- step C: the coarsest level from zero, its n_coarse smoother calls (:351-353)
+            if constexpr (lo == C) {
+                const double *Mf = LB + K::MO(C - 1);
+                bs[0] = Mf[4 * is + 2];
+                bs[1] = Mf[4 * is + 3];
+                bs[2] = Mf[4 * is];
+                xs[0] = xs[1] = xs[2] = 0.0;
+                ST St;
+                stencil(G::uni(C), SP[C], opaque(gs >> G::lg(C)), St);
+                constexpr int prio = std::is_same<ST, StcF>::value ? PAMG_CHAIN_PRIO : 0;
+                if (prio) __builtin_amdgcn_s_setprio(prio);
+                const int nB = ns * A.n_coarse;
+                for (int it = 0; it < nB; ++it) sweep(St, rdt, bs, xs);
+                if (prio) __builtin_amdgcn_s_setprio(0);
+                if (vs) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) LB[K::TO(C) + c * G::nt(C) + is] = xs[c];
+                    if (last) {
+                        const VLevel &V = A.lv[C];
+                        store3(V.RHS(), V.pitch, gs, bs);
+                        store3(V.T(), V.pitch, gs, xs);
+                        store3(V.TNN(), V.pitch, gs, xs);
+                    }
+                }
+            }
+            __syncthreads();
+            // ---- steps C+1 .. 2C-1: level l = C-1 .. 1, the interpolated correction, n_smooth sweeps
+            static_for<1, C>([&](auto jc) {
+                constexpr int l = C - decltype(jc)::value;
+                if constexpr (lo == l) {
+                    const double *Y = LB + K::TO(l + 1);
+                    const int pc = is >> 2;
+                    const double y[3] = {Y[pc], Y[G::nt(l + 1) + pc], Y[2 * G::nt(l + 1) + pc]};
+                    interp_add(xs, is & 3, y);
+                    ST St;
+                    stencil(G::uni(l), SP[l], opaque(gs >> G::lg(l)), St);
+                    for (int it = 0; it < ns; ++it) sweep(St, rdt, bs, xs);
+                    if (vs) {
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) LB[K::TO(l) + c * G::nt(l) + is] = xs[c];
+                        if (last) {
+                            const VLevel &V = A.lv[l];
+                            store3(V.T(), V.pitch, gs, xs);
+                            store3(V.TNN(), V.pitch, gs, xs);
+                        }
+                    }
+                }
+                __syncthreads();
+            });
+            // ---- step 2C: level 0, the interpolated correction of level 1, the post-smoothing call (:376)
+            {
+                const double *Y = LB + K::TO(1);
+                const int pc = t >> 1;   // the pair's coarse parent; children 2t & 3, 2t & 3 + 1
+                const double y[3] = {Y[pc], Y[G::nt(1) + pc], Y[2 * G::nt(1) + pc]};
+                interp_add(x0[0], (2 * t) & 3, y);
+                interp_add(x0[1], ((2 * t) & 3) + 1, y);
+                ST St;
+                stencil(G::uni(0), sp0, opaque(w0), St);
+                if constexpr (!last) {
+                    for (int it = 0; it < ns; ++it) {
+                        sweep(St, rdt, b0[0], x0[0]);
+                        sweep(St, rdt, b0[1], x0[1]);
+                    }
+                } else {
+                    // the call's last cycle: the halo words of the last smoother call (:555 of its last
+                    // sweep: the iterate before it), tnew = tnew_nonlin, and the fine residual after the cycle
+                    for (int it = 1; it < ns; ++it) {
+                        sweep(St, rdt, b0[0], x0[0]);
+                        sweep(St, rdt, b0[1], x0[1]);
+                    }
+                    if (v0 && keeph)
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) hs_write(G::uni(0), V0.H, w0, hs_pack(V0.H.hsub[(s0 + k) & hmask]), x0[k]);
+                    sweep(St, rdt, b0[0], x0[0]);
+                    sweep(St, rdt, b0[1], x0[1]);
+                    double n[2][3];
+                    (void)neg_resid_mean(St, rdt, x0[0], b0[0], n[0]);
+                    (void)neg_resid_mean(St, rdt, x0[1], b0[1], n[1]);
+                    if (v0) {
+                        store3p<PAMG_NT_TS>(V0.T(), V0.pitch, s0, x0[0], x0[1]);
+                        store3p(V0.TNN(), V0.pitch, s0, x0[0], x0[1]);
+                        store3p(V0.RES(), V0.pitch, s0, n[0], n[1]);
+                    }
+                }
+            }
+        };
+        for (int c = 0; c + 1 < m; ++c) cycle(std::false_type{});
+        cycle(std::true_type{});
+    };
+    if (t >= 256) role(std::integral_constant<int, 1>{});
+    else if (C >= 2 && wv == 0) role(std::integral_constant<int, (C >= 2 ? 2 : 0)>{});
+    else if (C >= 3 && wv == 1) role(std::integral_constant<int, (C >= 3 ? 3 : 0)>{});
+    else if (C >= 4 && wv == 2) role(std::integral_constant<int, (C >= 4 ? 4 : 0)>{});
+    else role(std::integral_constant<int, 0>{});
+}
+
 // part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
 template <int S, int L, class ST, bool W8>
 hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
@@ -1673,6 +1917,12 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
         if constexpr (L >= 2 && fine_np(S) == 2)
             hipLaunchKernelGGL((k_vc_fine<S, L, ST, true, W8, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A,
                                A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+        else
+            return hipErrorInvalidValue;
+    } else if (part == 7) {   // the resident corrected call (k_vc_corr)
+        if constexpr (L >= 2 && fine_np(S) == 2 && fine_tl(S) == 10)
+            hipLaunchKernelGGL((k_vc_corr<S, L, ST>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc, A.lv[1].stc,
+                               A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         else
             return hipErrorInvalidValue;
     } else if (part >= 4 && part <= 6) {   // the resident call (5: starting a time step; 6: exchange every cycle)

@@ -21,7 +21,7 @@ TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN, SOURCE = 0, 1, 2, 3, 4, 5
 (K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH, K_VCYCLE,
  K_VCYCLE_COARSE) = range(10)
 K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle",
-           "vcycle_coarse", "vcycle_pipe", "vcycle_rhsf", "vcycle_res", "vcycle_res_rhsf"]
+           "vcycle_coarse", "vcycle_pipe", "vcycle_rhsf", "vcycle_res", "vcycle_res_rhsf", "vcycle_corr"]
 
 
 class PamgParams(C.Structure):

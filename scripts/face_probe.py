@@ -25,7 +25,7 @@ for cycle in CYCLES:
     s.vcycle(n)
     s.synchronize()
     dt = (time.perf_counter() - t0) / n
-    s.timing_enable(0x3F7F)
+    s.timing_enable(0x7F7F)
     s.timing_stride(1)
     s.timing_reset()
     s.vcycle(n)

@@ -101,3 +101,69 @@ def test_corrected_cycle_time_loop_and_schedules():
         s = pamg.SemiImplicitIterative(m, 4, 3, cycle=1, fused=fused)
         s.run(2, 2)
         check_corrected(s.state(), o.state())
+
+
+# ---------------------------------------------------------------- the resident corrected call
+def corr_pair(mesh, S, L, arith, solver=3, ns=4, fused=3):
+    """the HIP path (cycle = 1) and the oracle in the same arithmetic, the oracle taking the device's
+    source term s' (the one operation the two sides cannot share, tests/test_contracted_oracle.py)"""
+    import pamg
+    path = os.path.join(goldens.MESHES, mesh)
+    g = pamg.SemiImplicitIterative(pamg.Mesh.read(path), S, L, n_smooth=ns, solver=solver, fused=fused, arith=arith,
+                                   cycle=1)
+    o = O.Oracle(O.read_msh(path), S, L, n_smooth=ns, solver=solver, arith=arith)
+    o.set_source(g.get(pamg.SOURCE, 1))
+    return g, o
+
+
+def assert_identical(g, o):
+    sg, so = g.state(), o.state()
+    for k in so:
+        np.testing.assert_array_equal(sg[k], so[k], err_msg=k)
+    for x, y in zip(g.overlap(), o.overlap()):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arith", [1, 0])
+def test_corrected_resident_call_is_bitwise_the_oracle_at_the_bench_config(arith):
+    """bench.py's extra.cycle1 workload -- untitled8192, n_split 5, L 3, n_smooth 4, solver 3, one
+    time step and a pamg_vcycle(4) call, i.e. ONE resident launch (k_vc_corr) -- is every field of
+    every level, t_overlap and t_overlap_old of orc_vcycle_corrected's four cycles, bit for bit."""
+    g, o = corr_pair("untitled8192.msh", 5, 3, arith)
+    g.timing_enable(1 << 14)   # PAMG_K_VCYCLE_CORR
+    g.timing_reset()
+    g.begin_timestep()
+    g.vcycle(4)
+    o.begin_timestep()
+    for _ in range(4):
+        o.vcycle_corrected()
+    assert g.timing()["vcycle_corr"]["issued"] == 1
+    assert_identical(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,solver,ns", [
+    ("untitled8.msh", 3, 3, 3, 4), ("irregular.msh", 6, 3, 1, 2), ("900_ele.msh", 2, 2, 3, 3),
+    ("test_sn2.msh", 4, 4, 3, 2), ("untitled2048.msh", 5, 5, 3, 1), ("irregular.msh", 7, 4, 3, 2),
+    ("untitled8192.msh", 3, 3, 1, 4), ("untitled8.msh", 1, 1, 3, 2)])
+@pytest.mark.parametrize("arith", [1, 0])
+def test_corrected_resident_call_equals_per_step_and_oracle(mesh, S, L, solver, ns, arith):
+    """The resident call (fused = 3: whole-un_ele tiles below n_split 5, parts of one at 6 and 7, two to
+    five levels, Jacobi and GS, calls split 2 + 1 over two time steps) and the per-step sequence
+    (fused = 0) leave the oracle's state, bit for bit."""
+    o = None
+    for fused in (3, 0):
+        g, o1 = corr_pair(mesh, S, L, arith, solver, ns, fused)
+        for _ in range(2):
+            g.begin_timestep()
+            g.vcycle(2)
+            g.vcycle(1)
+        if o is None:
+            o = o1
+            for _ in range(2):
+                o.begin_timestep()
+                for _ in range(3):
+                    o.vcycle_corrected()
+        assert_identical(g, o)
+        g.close()

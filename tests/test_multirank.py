@@ -108,7 +108,7 @@ def test_local_group_exchange_every_cycle_inside_the_resident_call(S, L, kind, n
              for r in range(nparts)]
     local_group(parts)
     for p in parts:
-        p.timing_enable(0x3F7F)
+        p.timing_enable(0x7F7F)
         p.timing_reset()
     run_ranks(parts, lambda p: drive(p, "vcycle20"))
     check_parts(full, parts, owner)
@@ -116,6 +116,31 @@ def test_local_group_exchange_every_cycle_inside_the_resident_call(S, L, kind, n
         tm = p.timing()
         assert tm["vcycle_res"]["issued"] == 1, tm["vcycle_res"]
         assert tm["halo"]["issued"] == 20, tm["halo"]
+        p.close()
+
+
+@pytest.mark.parametrize("S,L,kind,nparts,solver", [(5, 3, "strip", 8, 3), (3, 3, "block", 4, 1), (6, 3, "strip", 8, 3)])
+def test_local_group_corrected_resident_call(S, L, kind, nparts, solver):
+    """The corrected cycle's resident call (k_vc_corr) on partitions: the level-1 halo words of the
+    call's last smoother call packed by the launch and exchanged once after it; every field and both
+    halo arrays of every rank equal the single domain's per-step sequence, bit for bit."""
+    mesh = "irregular.msh" if S == 6 else "untitled8192.msh"
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    kw = dict(solver=solver, arith=1, cycle=1)
+    full = pamg.SemiImplicitIterative(m, S, L, fused=0, **kw)
+    drive(full, "calls")
+    owner = owners(m, kind, nparts)
+    parts = [pamg.SemiImplicitIterative(m, S, L, comm=(nparts, r, None, owner), fused=3, **kw) for r in range(nparts)]
+    local_group(parts)
+    for p in parts:
+        p.timing_enable(0x7F7F)
+        p.timing_reset()
+    run_ranks(parts, lambda p: drive(p, "calls"))
+    check_parts(full, parts, owner)
+    for p in parts:
+        tm = p.timing()
+        if p.U:
+            assert tm["vcycle_corr"]["issued"] == 3, tm["vcycle_corr"]
         p.close()
 
 
