@@ -12,7 +12,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-LIB_PATH = os.path.join(ORACLE_DIR, "_build", "liborc.so")
+# ORACLE_LIB: another build of the same checker (the host sanitizer build, scripts/asan_cpu_tests.sh)
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(ORACLE_DIR, "_build", "liborc.so")
 
 TNEW, TOLD, RHS, RES, TNN, SOURCE = 0, 1, 2, 3, 4, 5
 
