@@ -968,7 +968,147 @@ bool face_cycle_fusable(pamg_handle *h) {
     return true;
 }
 
+// ---- the face V-cycle with two sweeps per HBM pass (k_face_pp) on the levels below the coarsest
+// The fused cycle's level-l work, for l < L, is a stream of sweeps on one RHS: its restriction-leg call's
+// executed sweeps and its prolongation-leg call's, which starts from the restriction-leg tnew (:367; the
+// prolongated values are overwritten unread, :550), with get_residual between them -- and level 1's RHS
+// is the time step's, so level 1's streams of all the call's cycles are ONE stream (its coarse levels
+// never feed back into it). Such a stream runs as launches of two sweeps (the halo of the second sweep
+// computed in the launch, k_face_pp), the residual inside the launch that passes its point, and the
+// state rotating through tnew, tnew_nonlin and RHSN (op = 1 has no use for RHSN) -- a launch never writes
+// the iterate its neighbours read. The restrictor of level l (:336, the PREVIOUS residual) runs before the
+// launch that writes the new one; a coarse level's whole cycle runs before the next level's (nothing of
+// the next level reaches it). The halo words (:555) are no longer published between sweeps (the launches
+// read the iterate itself): t_overlap, t_overlap_old and the boundary words are written from level 1's
+// tnew once, after the call -- what the per-step sequence's last writer, level 1's last smoother call,
+// leaves (every coarser level writes a subset of its slots). Bitwise the per-step sequence
+// (tests/test_face_operator.py). PAMG_FACE_PP=0 keeps the one-sweep launches (A/B).
+bool face_pp_ok(pamg_handle *h, int l) {
+    const char *ev = getenv("PAMG_FACE_PP");   // read per call: tests switch it within a process
+    if (ev && atoi(ev) == 0) return false;
+    const Level &L = h->lv[l];
+    return face_fusable(h, l) && face_tile_shape(L) && L.gface && L.gpos && (h->p.solver != 3 || L.words_up);
+}
+
+struct PPPass { int K, res; double *in, *pre, *mid, *end; };
+
+// the passes of a stream of `total` sweeps from src with get_residual after sweep r for each r in res_at
+// (0 < r < total), ending with the final stores fin (1: tnew = the iterate before the last sweep,
+// tnew_nonlin = after it; 2: tnew = the last result, the dead sweep's :550)
+int face_pp_plan(pamg_handle *h, int l, int total, double *src, const std::vector<int> &res_at, int fin,
+                 std::vector<PPPass> &plan) {
+    Level &L = h->lv[l];
+    plan.clear();
+    for (int s = 0; s < total; s += 2) plan.push_back(PPPass{std::min(2, total - s), 0, nullptr, nullptr, nullptr, nullptr});
+    for (int r : res_at) {
+        if (r <= 0 || r >= total) { h->err = "internal: face stream residual point"; return PAMG_ERR_STATE; }
+        PPPass &q = plan[r / 2];
+        if (q.res) { h->err = "internal: two residuals in one face pass"; return PAMG_ERR_STATE; }
+        q.res = (r & 1) ? 2 : 1;   // after the pass's first sweep, or at its start
+    }
+    const int P = (int)plan.size();
+    PPPass &z = plan[P - 1];
+    if (fin == 1) {
+        if (z.K == 2) z.mid = L.T; else z.pre = L.T;
+        z.end = L.TNN;
+    } else {
+        z.end = L.T;
+    }
+    double *const buf[3] = {L.RHSN, L.TNN, L.T};
+    // inputs, last to first: the last pass reads RHSN (neither of its outputs); every other pass writes the
+    // next one's input, which is not its own; the first reads src
+    std::vector<double *> in(P);
+    in[P - 1] = P == 1 ? src : L.RHSN;
+    for (int p = P - 2; p >= 1; --p)
+        for (double *b : buf)
+            if (b != in[p + 1] && (p != 1 || b != src)) { in[p] = b; break; }
+    if (P >= 2) in[0] = src;
+    for (int p = 0; p < P; ++p) {
+        plan[p].in = in[p];
+        if (p + 1 < P) plan[p].end = in[p + 1];
+        if (plan[p].in == plan[p].end || plan[p].in == plan[p].mid || plan[p].in == plan[p].pre) {
+            h->err = "internal: a face pass writes its own input";
+            return PAMG_ERR_STATE;
+        }
+    }
+    return PAMG_OK;
+}
+
+int face_pp_emit(pamg_handle *h, int l, const PPPass &q) {
+    Level &L = h->lv[l];
+    const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
+    // iterate and RHS in, the outputs and the residual out (the halo gathers of the neighbours' boundary
+    // sub-elements are overhead, not counted)
+    const double by = (48.0 + 24.0 * ((q.pre != nullptr) + (q.mid != nullptr) + (q.end != nullptr) + (q.res != 0))) *
+                      (double)L.N + 168.0 * h->U;
+    if (q.res) h->rhsn_valid = false;
+    Span sp(h, kid, by);
+    HIPCHK(h, launch_face_pp(h->stream, L, q.K, q.in, q.pre, q.mid, q.end, h->p.solver == 3, l == 1, 1 / h->p.dt, q.res));
+    return PAMG_OK;
+}
+
+// level l's part of cycle c of the fused face cycle (levels l .. L): the coarsest level's calls; a level
+// below it as a two-sweep stream (its restrictor before the launch that writes its new residual, then the
+// next level), or as its two calls around the next level (vcycle_face_fused's order)
+int face_pp_level(pamg_handle *h, int l, bool last) {
+    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    const double rdt = 1 / h->p.dt;
+    if (l == L) {
+        CHK(face_call(h, l, true, ns, true));   // :331 via :351
+        Level &V = h->lv[l];
+        h->rhsn_valid = false;
+        {
+            Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)V.N + 168.0 * h->U);
+            HIPCHK(h, launch_face_residual(h->stream, V, h->tov, false, l == 1, rdt, h->slots));
+        }
+        return face_call(h, L, true, ns * h->p.n_coarse, !last);   // :344-359
+    }
+    if (!face_pp_ok(h, l) || 2 * (ns - 1) + (last ? 1 : 0) < 3) {   // (one pass could not rotate its buffers)
+        CHK(face_call(h, l, true, ns, true));
+        CHK(restrict_(h, l));
+        CHK(face_pp_level(h, l + 1, last));
+        return face_call(h, l, true, ns, !last, true);
+    }
+    h->tnn_level = l;
+    h->overlap_static_l1 = false;
+    std::vector<PPPass> plan;
+    CHK(face_pp_plan(h, l, 2 * (ns - 1) + (last ? 1 : 0), h->lv[l].T, {ns - 1}, last ? 1 : 2, plan));
+    bool restricted = false;
+    for (const PPPass &q : plan) {
+        if (q.res && !restricted) { CHK(restrict_(h, l)); restricted = true; }   // :336, the previous residual
+        CHK(face_pp_emit(h, l, q));
+    }
+    if (!restricted) CHK(restrict_(h, l));
+    return face_pp_level(h, l + 1, last);
+}
+
+int vcycle_face_pp(pamg_handle *h, int n) {
+    const int ns = h->p.n_smooth;
+    if (n <= 0) return PAMG_OK;
+    // level 1: one stream over the call's cycles, get_residual after each cycle's restriction leg
+    const int per = 2 * (ns - 1);
+    std::vector<int> res_at;
+    for (int c = 0; c < n; ++c) res_at.push_back(ns - 1 + per * c);
+    std::vector<PPPass> plan;
+    CHK(face_pp_plan(h, 1, per * n + 1, h->lv[1].T, res_at, 1, plan));
+    h->overlap_static_l1 = false;
+    size_t p = 0;
+    for (int c = 0; c < n; ++c) {
+        h->tnn_level = 1;
+        CHK(restrict_(h, 1));   // :336 -- level 1's residual of the previous cycle, before this cycle's is written
+        const size_t pr = (size_t)res_at[c] / 2;   // the pass that writes this cycle's residual
+        for (; p <= pr; ++p) CHK(face_pp_emit(h, 1, plan[p]));
+        CHK(face_pp_level(h, 2, c + 1 == n));
+    }
+    for (; p < plan.size(); ++p) CHK(face_pp_emit(h, 1, plan[p]));
+    // the halo the per-step sequence leaves: level 1's last smoother call's words, from its tnew (:555)
+    HIPCHK(h, launch_face_words(h->stream, h->lv[1], h->U, h->tov, h->tovo));
+    h->tnn_level = 1;
+    return face_chain_check(h);
+}
+
 int vcycle_face_fused(pamg_handle *h, int n) {
+    if (h->p.multi_levels >= 2 && h->p.n_smooth >= 2 && face_pp_ok(h, 1)) return vcycle_face_pp(h, n);
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     const double rdt = 1 / h->p.dt;
     for (int c = 0; c < n; ++c) {
@@ -1378,7 +1518,7 @@ void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
         Level &L = h->lv[l];
         dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.d_pos); dev_free(L.blocks);
-        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx); dev_free(L.cpos);
+        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx); dev_free(L.cpos); dev_free(L.gface); dev_free(L.gpos);
         dev_free(L.chain_nb_off); dev_free(L.chain_nb_list); dev_free(L.chain_flags);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
@@ -1696,6 +1836,38 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
                 if ((e.x | e.y | e.z) && !fnb[j].w) L.words_up = false;
             }
             CHK(dev_upload(h, &L.cpos, cpos));
+            // the two-sweep passes' tables (k_face_pp): each face's neighbour as the halo words travel
+            // (hface: this un_ele's words into it; its record for the face back: its words into this one),
+            // and the boundary sub-elements by face and position (hsub)
+            if (face_tile_shape(L)) {
+                const int m = 1 << L.isplit, sl = h->slots;
+                std::vector<int4> gf((size_t)std::max(Ul, 1) * 3, make_int4(-1, 0, 0, 0));
+                for (int q = 0; q < Ul; ++q)
+                    for (int f = 1; f <= 3; ++f) {
+                        const int4 r = L.halo.hface[3 * (size_t)q + f - 1];
+                        const int mode = r.x & 3;
+                        if (mode == 0) continue;
+                        if (mode == 2) { gf[3 * (size_t)q + f - 1] = make_int4(-2, 0, 0, 0); continue; }
+                        const int v = r.y / (3 * sl), fv = (r.y - v * 3 * sl) / sl + 1;
+                        const int4 rv = L.halo.hface[3 * (size_t)v + fv - 1];
+                        if ((rv.x & 3) != 1 || rv.y != q * 3 * sl + (f - 1) * sl) {
+                            h->err = "face operator: asymmetric halo records between un_eles " + std::to_string(q) + " and " + std::to_string(v);
+                            return PAMG_ERR_STATE;
+                        }
+                        gf[3 * (size_t)q + f - 1] = make_int4(v, fv, rv.x >> 2, r.x >> 2);
+                    }
+                std::vector<int> gp(3 * (size_t)m, -1);
+                for (int j = 0; j < L.nsub && j < (int)L.halo.hsub.size(); ++j) {
+                    const int4 e = L.halo.hsub[j];
+                    if (e.x) gp[e.x - 1] = j;
+                    if (e.y) gp[m + e.y - 1] = j;
+                    if (e.z) gp[2 * m + e.z - 1] = j;
+                }
+                for (int v : gp)
+                    if (v < 0) { h->err = "face operator: a face position without its boundary sub-element"; return PAMG_ERR_STATE; }
+                CHK(dev_upload(h, &L.gface, gf));
+                CHK(dev_upload(h, &L.gpos, gp));
+            }
         }
         HaloPlan &P = L.halo;
         CHK(dev_upload(h, &P.d_local, P.local));

@@ -528,6 +528,203 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
     }
 }
 
+// ---- two sweeps per HBM pass (temporal blocking) of a level whose tile is one un_ele (k_face_tile's
+// levels: 256, 1,024, 4,096 sub-elements; single domain). Every sweep reads its cross-un_ele values from
+// a snapshot of the neighbours' iterate at the sweep's start (:555, Jacobi across un_ele faces, red-black
+// or Jacobi inside). Here the snapshot is not published through t_overlap: the launch reads its input
+// iterate A (written by the previous launch, read-only in this one -- its output goes to another buffer)
+// and takes the neighbours' boundary values straight from it. For a second sweep in the same launch the
+// tile needs the neighbours' boundary values after the FIRST sweep -- which their own workgroups are
+// computing -- so it computes them itself: every sub-element with halo words is an up one (words_up), an
+// up sub-element's sweep reads only its down neighbours (unchanged since the previous sweep) and the
+// snapshot across its un_ele faces, so the neighbour v's boundary sub-element e after the sweep is
+// face_apply of e's value, its two down neighbours, its RHS and v's operator record -- all in A or in
+// memory that does not change -- and the snapshot values across e's faces: this tile's own boundary
+// values at the sweep's start, or (corners) those of v's other neighbour w, in A. The same face_apply on
+// the same operands as v's own workgroup: bitwise the per-sweep launches (tests/test_face_operator.py).
+// A pass: K = 1 or 2 sweeps; res 1: get_residual of the start iterate, 2: of the iterate after the first
+// sweep (the residual point of a smoother stream, with the snapshot the second sweep reads); outputs:
+// out_pre the start iterate, out_mid the iterate after sweep 1 (K = 2), out_end the iterate after the
+// last sweep (none of them aliases A).
+// gface (U x 3): per un_ele face {neighbour v (-1 boundary, -2 another rank), v's face toward it, the rev
+// flag of v's words into it, the rev flag of its words into v}; E (3 m): the storage position of the
+// boundary sub-element at position i of face f.
+template <int TS, int NT, bool RB, int K>
+__global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_pp(
+    const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, const double *__restrict__ RHS,
+    const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
+    const int *__restrict__ fsx, const int4 *__restrict__ gface, const int *__restrict__ E,
+    const int4 *__restrict__ hface, const double2 *__restrict__ bcv, int64_t pitch, int level1, double rdt, int res,
+    double *RESout) {
+    constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
+    static_assert(PER % 2 == 0 && M * M == TS && 3 * M <= NT && (NT < 192 || M <= 64), "whole un_ele tiles, adjacent pairs per thread");
+    __shared__ double X[3][TS];
+    __shared__ double HI[K][NH];
+    __shared__ double WD[24];
+    const int t = threadIdx.x;
+    const int64_t u = blockIdx.x, s0 = u * TS;
+    int4 nbr[PER];
+    double b[PER][3];
+    FaceRec R;
+    load_face_rec(stc, fface, fsx, u, R);
+    if (t < 24) WD[t] = fface[u * kFaceStride + kFaceWD + t];
+    // the boundary words of face f (1..3) at position sp (1..m) of a domain-boundary face: update_overlaps'
+    // boundary values at the two face nodes (halo_words' placement; the third word is never read)
+    auto bcword = [&](int64_t uu, int f, int sp, int kk) -> double {
+        const double2 v = bcv[hface[3 * uu + f - 1].z + sp - 1];
+        return kk == (f == 3 ? 1 : 0) ? v.x : kk == (f == 2 ? 1 : 2) ? v.y : 0.0;
+    };
+    // the value of A at the boundary sub-element of neighbour g (gface entry) that faces slot sp
+    auto across = [&](int4 g, int sp, int kk) -> double {
+        const int i = g.z ? M - sp + 1 : sp;
+        return A[kk * pitch + (int64_t)g.x * TS + E[(g.y - 1) * M + i - 1]];
+    };
+    // the snapshot of the first sweep (:555 at its start): the neighbours' boundary values in A. Thread ->
+    // (face fu, slot spu): a face per wave where the workgroup has three waves or more (the neighbour's
+    // records then come through the scalar unit), else packed
+    constexpr bool WAVEF = NT >= 192;
+    int4 gu = make_int4(-1, 0, 0, 0);
+    const int fu = WAVEF ? t / 64 + 1 : t / M + 1;
+    const int spu = WAVEF ? (t & 63) + 1 : t - (fu - 1) * M + 1;
+    const bool gon = fu <= 3 && spu <= M;
+    const int hq = 3 * ((fu - 1) * M + spu - 1);   // the slot's first word in HI
+    if (fu <= 3) {
+        gu = gface[3 * u + fu - 1];
+        if (WAVEF) {
+            gu.x = __builtin_amdgcn_readfirstlane(gu.x);
+            gu.y = __builtin_amdgcn_readfirstlane(gu.y);
+            gu.z = __builtin_amdgcn_readfirstlane(gu.z);
+            gu.w = __builtin_amdgcn_readfirstlane(gu.w);
+        }
+    }
+    if (gon)
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk)
+            HI[0][hq + kk] = gu.x >= 0 ? across(gu, spu, kk) : gu.x == -1 ? bcword(u, fu, spu, kk) : 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; k += 2) {   // the iterate into LDS, pairs
+        const int j = 2 * (t + NT * (k / 2));
+        nbr[k] = fnb[j];
+        nbr[k + 1] = fnb[j + 1];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double2 v = ld2(A + c * pitch + s0 + j), r = ld2(RHS + c * pitch + s0 + j);
+            b[k][c] = r.x;
+            b[k + 1][c] = r.y;
+            X[c][j] = v.x;
+            X[c][j + 1] = v.y;
+            if (out_pre) st2(out_pre + c * pitch + s0 + j, v);
+        }
+    }
+    __syncthreads();
+    if constexpr (K == 2) {
+        // the neighbours' boundary sub-elements after the first sweep: the second sweep's snapshot
+        if (gon) {
+            if (gu.x >= 0) {
+                const int64_t v = gu.x;
+                const int fv = gu.y;
+                const int i = gu.z ? M - spu + 1 : spu;   // v's boundary position facing this slot
+                const int e = E[(fv - 1) * M + i - 1];
+                const int4 nb = fnb[e];
+                FaceRec Rv;
+                load_face_rec(stc, fface, fsx, v, Rv);
+                const double *wd = fface + v * kFaceStride + kFaceWD + 3 * face_pattern(nb);
+                double x[3], be[3], r[3];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    x[c] = HI[0][hq + c];   // = A at v's e
+                    be[c] = RHS[c * pitch + v * TS + e];
+                }
+                auto xv = [&](int c, int q) { return A[c * pitch + v * TS + q]; };
+                auto hvv = [&](int64_t, int mf, int sp, int kk) -> double {
+                    if (mf == fv) {   // this tile's own boundary value at the sweep's start
+                        const int iu = gu.w ? M - sp + 1 : sp;
+                        return X[kk][E[(fu - 1) * M + iu - 1]];
+                    }
+                    const int4 g2 = gface[3 * v + mf - 1];   // a corner: v's other neighbour w, or the boundary
+                    return g2.x >= 0 ? across(g2, sp, kk) : g2.x == -1 ? bcword(v, mf, sp, kk) : 0.0;
+                };
+                face_apply<RB ? 0 : 2>(Rv, xv, x, be, nb, v, hvv, [&](int q) { return wd[q]; }, level1, rdt, r);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) HI[1][hq + c] = r[c];
+            } else {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) HI[1][hq + c] = HI[0][hq + c];   // boundary words: constant
+            }
+        }
+        __syncthreads();   // the ghost updates read the start iterate (X) before the sweeps rewrite it
+    }
+    auto xin = [&](int c, int q) { return X[c][q]; };
+    auto residual = [&](int snap) {   // get_residual (A x - RHS) of the tile's iterate with snapshot snap
+        auto hv = [&](int64_t, int mf, int sp, int kk) { return HI[snap][((mf - 1) * M + sp - 1) * 3 + kk]; };
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = 2 * (t + NT * (k / 2)) + (k & 1);
+            double x[3], r[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[c] = X[c][j];
+            face_apply<3>(R, xin, x, b[k], nbr[k], u, hv, [&](int) { return 0.0; }, level1, rdt, r);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) RESout[c * pitch + s0 + j] = r[c];
+        }
+        __syncthreads();   // every read of the iterate before the passes rewrite it
+    };
+    auto sweep = [&](int snap) {
+        auto hv = [&](int64_t, int mf, int sp, int kk) { return HI[snap][((mf - 1) * M + sp - 1) * 3 + kk]; };
+        auto pass = [&](auto mc) {
+            constexpr int MODE = decltype(mc)::value;
+            double r[PER][3];
+            bool on[PER];
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                const int j = 2 * (t + NT * (k / 2)) + (k & 1);
+                const int4 nb = nbr[k];
+                on[k] = !((MODE == 0 && !nb.w) || (MODE == 1 && nb.w));
+                if (!on[k]) continue;
+                double x[3];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) x[c] = X[c][j];
+                const int wb = 3 * face_pattern(nb);
+                face_apply<MODE>(R, xin, x, b[k], nb, u, hv, [&](int i) { return WD[wb + i]; }, level1, rdt, r[k]);
+                if (MODE != 2)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) X[c][j] = r[k][c];
+            }
+            if (MODE == 2) {
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < PER; ++k)
+                    if (on[k])
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) X[c][2 * (t + NT * (k / 2)) + (k & 1)] = r[k][c];
+            }
+            __syncthreads();
+        };
+        if constexpr (RB) {
+            pass(std::integral_constant<int, 0>{});
+            pass(std::integral_constant<int, 1>{});
+        } else {
+            pass(std::integral_constant<int, 2>{});
+        }
+    };
+    auto store = [&](double *o) {
+#pragma unroll
+        for (int k = 0; k < PER; k += 2) {
+            const int j = 2 * (t + NT * (k / 2));
+#pragma unroll
+            for (int c = 0; c < 3; ++c) st2(o + c * pitch + s0 + j, make_double2(X[c][j], X[c][j + 1]));
+        }
+    };
+    if (res == 1) residual(0);
+    sweep(0);
+    if constexpr (K == 2) {
+        if (out_mid) store(out_mid);
+        if (res == 2) residual(1);
+        sweep(1);
+    }
+    if (out_end) store(out_end);
+}
+
 // ---- the wavefront call: every sweep of one smoother call on a level too large to stay on-chip
 // (levels 1 and 2 at n_split = 5: 8.4 M and 2.1 M sub-elements), each un_ele crossing HBM once per
 // call instead of once per sweep. A persistent cooperative grid of G workgroups takes un_eles in
@@ -1297,6 +1494,30 @@ static hipError_t launch_coresident(const void *f, int grid, int nt, void **args
     }
     if (grid > n) return hipErrorCooperativeLaunchTooLarge;
     return hipLaunchKernel(f, dim3(grid), dim3(nt), args, 0, s);
+}
+
+// k_face_pp: K sweeps of a whole-un_ele-tile level in one launch (face_tile_shape; single domain)
+hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
+                          double *out_end, bool rb, bool level1, double rdt, int res) {
+    if (L.N == 0) return hipSuccess;
+    if (!face_tile_shape(L) || !L.fnb || !L.gface || !L.gpos || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)))
+        return hipErrorInvalidValue;
+    const HaloPlan &P = L.halo;
+    const dim3 g((unsigned)(L.N / L.nsub));
+    const int l1 = level1 ? 1 : 0;
+    double *R = res ? L.RES : nullptr;
+#define PAMG_FPP(TS, NT, RB_, K_)                                                                                    \
+    hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, L.RHS, L.stc,  \
+                       L.fnb, L.fface, L.fsx, L.gface, L.gpos, P.d_hface, P.d_bcv, L.pitch, l1, rdt, res, R)
+#define PAMG_FPPK(TS, NT)                                          \
+    if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \
+    else { if (K == 2) PAMG_FPP(TS, NT, false, 2); else PAMG_FPP(TS, NT, false, 1); }
+    if (L.nsub == 4096) { PAMG_FPPK(4096, 1024) }
+    else if (L.nsub == 1024) { PAMG_FPPK(1024, 512) }
+    else { PAMG_FPPK(256, 128) }
+#undef PAMG_FPPK
+#undef PAMG_FPP
+    return hipGetLastError();
 }
 
 int face_chain_per_wg(int nsub, int U, int cus) {

@@ -117,6 +117,11 @@ struct Level {
     // (fnb.w != 0, ascending), then of the down ones -- nup + ndn = nsub
     int *cpos = nullptr;
     int nup = 0, ndn = 0;
+    // the two-sweep passes (k_face_pp): per local un_ele face {neighbour (-1 boundary, -2 another rank), its
+    // face toward this one, rev of its words into this one, rev of this one's words into it}, and the storage
+    // positions of the boundary sub-elements by face and position along it (3 m)
+    int4 *gface = nullptr;
+    int *gpos = nullptr;
     // every sub-element with halo words (HaloPlan::hsub) is an up one: the chain publishes a
     // sweep's words right after its up pass (k_face_chain, early)
     bool words_up = false;
@@ -356,6 +361,12 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
                                    double *res = nullptr);
 // k_face_tile's levels (one tile per un_ele); their first sweep can also write get_residual (res)
 bool face_tile_shape(const Level &L);
+// K = 1 or 2 sweeps in one launch from the iterate `in` (read-only: the neighbours' halo values are read
+// from it, the second sweep's computed in the launch); res 1 / 2: get_residual into L.RES of the start
+// iterate / the iterate after the first sweep; out_pre / out_mid / out_end (any may be null, none `in`):
+// the start iterate, the iterate after sweep 1, after the last sweep
+hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
+                          double *out_end, bool rb, bool level1, double rdt, int res);
 // the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of
 // the call's `total` sweeps in one launch, the iterate in LDS, the halo handed over between
 // workgroups inside the launch; store 1: tnew (the last sweep's start) and tnew_nonlin, 2: tnew :=

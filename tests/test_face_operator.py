@@ -206,6 +206,7 @@ def test_face_wavefront_call_equals_per_sweep_launches(mesh, S, L, solver, ns, n
         g.close()
         return st, ov
 
+    monkeypatch.setenv("PAMG_FACE_PP", "0")   # the fused cycle's one-sweep calls, where the wavefront form applies
     monkeypatch.setenv("PAMG_FACE_WAVE", "0")
     monkeypatch.setenv("PAMG_FACE_CHAIN", "0")
     rs, rov = run()
@@ -215,3 +216,36 @@ def test_face_wavefront_call_equals_per_sweep_launches(mesh, S, L, solver, ns, n
     assert_identical(gs, rs)
     for x, y in zip(gov, rov):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,solver,ns,splits", [
+    ("untitled8192.msh", 5, 3, 3, 4, ([3], [1, 2])), ("untitled8192.msh", 5, 3, 1, 4, ([2],)),
+    ("untitled8192.msh", 4, 3, 3, 3, ([3], [2, 1])), ("irregular.msh", 6, 3, 3, 2, ([3], [1, 1, 1])),
+    ("irregular.msh", 6, 3, 1, 5, ([2],)), ("test_sn2.msh", 4, 4, 3, 3, ([2, 1],)), ("900_ele.msh", 5, 3, 3, 4, ([2],))])
+def test_face_two_sweep_passes_equal_one_sweep_launches(mesh, S, L, solver, ns, splits, monkeypatch):
+    """The fused face cycle with two sweeps per HBM pass on the levels below the coarsest (k_face_pp: the
+    second sweep's halo computed in the launch from the neighbours' boundary sub-elements and their down
+    neighbours; level 1 one stream over the call's cycles) leaves the state of the one-sweep launches, bit
+    for bit -- levels of 256, 1,024 and 4,096 sub-elements per un_ele, red-black and Jacobi, odd and even
+    stream lengths, residuals at a pass's start and in its middle, calls split over time steps."""
+    import pamg
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+
+    def run(split):
+        g = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, op=1)
+        for n in split:
+            g.begin_timestep()
+            g.vcycle(n)
+        st, ov = g.state(), g.overlap()
+        g.close()
+        return st, ov
+
+    for split in splits:
+        monkeypatch.setenv("PAMG_FACE_PP", "0")
+        rs, rov = run(split)
+        monkeypatch.setenv("PAMG_FACE_PP", "1")
+        gs, gov = run(split)
+        assert_identical(gs, rs)
+        for x, y in zip(gov, rov):
+            np.testing.assert_array_equal(x, y)
