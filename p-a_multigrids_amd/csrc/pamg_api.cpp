@@ -987,7 +987,7 @@ bool face_pp_ok(pamg_handle *h, int l) {
     const char *ev = getenv("PAMG_FACE_PP");   // read per call: tests switch it within a process
     if (ev && atoi(ev) == 0) return false;
     const Level &L = h->lv[l];
-    return face_fusable(h, l) && face_tile_shape(L) && L.gface && L.gpos && (h->p.solver != 3 || L.words_up);
+    return face_fusable(h, l) && face_tile_shape(L) && L.gtab && (h->p.solver != 3 || L.words_up);
 }
 
 struct PPPass { int K, res; double *in, *pre, *mid, *end; };
@@ -1518,7 +1518,7 @@ void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
         Level &L = h->lv[l];
         dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.d_pos); dev_free(L.blocks);
-        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx); dev_free(L.cpos); dev_free(L.gface); dev_free(L.gpos);
+        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx); dev_free(L.cpos); dev_free(L.gtab);
         dev_free(L.chain_nb_off); dev_free(L.chain_nb_list); dev_free(L.chain_flags);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
@@ -1836,12 +1836,13 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
                 if ((e.x | e.y | e.z) && !fnb[j].w) L.words_up = false;
             }
             CHK(dev_upload(h, &L.cpos, cpos));
-            // the two-sweep passes' tables (k_face_pp): each face's neighbour as the halo words travel
-            // (hface: this un_ele's words into it; its record for the face back: its words into this one),
-            // and the boundary sub-elements by face and position (hsub)
+            // the two-sweep passes' gather table (k_face_pp, Level::gtab): for every halo slot of every local
+            // un_ele, the neighbour's boundary sub-element e whose words fill it (hface: this un_ele's words
+            // into the neighbour; the neighbour's record back: its words into this one, reversed or not) and,
+            // for each face of e, where the value across it lives
             if (face_tile_shape(L)) {
-                const int m = 1 << L.isplit, sl = h->slots;
-                std::vector<int4> gf((size_t)std::max(Ul, 1) * 3, make_int4(-1, 0, 0, 0));
+                const int m = 1 << L.isplit, sl = h->slots, ns = L.nsub;
+                std::vector<int4> gf((size_t)std::max(Ul, 1) * 3, make_int4(-1, 0, 0, 0));   // {v, fv, rev v->u, rev u->v}
                 for (int q = 0; q < Ul; ++q)
                     for (int f = 1; f <= 3; ++f) {
                         const int4 r = L.halo.hface[3 * (size_t)q + f - 1];
@@ -1856,17 +1857,44 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
                         }
                         gf[3 * (size_t)q + f - 1] = make_int4(v, fv, rv.x >> 2, r.x >> 2);
                     }
-                std::vector<int> gp(3 * (size_t)m, -1);
-                for (int j = 0; j < L.nsub && j < (int)L.halo.hsub.size(); ++j) {
+                std::vector<int> E(3 * (size_t)m, -1);   // boundary sub-element at position i of face f
+                for (int j = 0; j < ns && j < (int)L.halo.hsub.size(); ++j) {
                     const int4 e = L.halo.hsub[j];
-                    if (e.x) gp[e.x - 1] = j;
-                    if (e.y) gp[m + e.y - 1] = j;
-                    if (e.z) gp[2 * m + e.z - 1] = j;
+                    if (e.x) E[e.x - 1] = j;
+                    if (e.y) E[m + e.y - 1] = j;
+                    if (e.z) E[2 * m + e.z - 1] = j;
                 }
-                for (int v : gp)
+                for (int v : E)
                     if (v < 0) { h->err = "face operator: a face position without its boundary sub-element"; return PAMG_ERR_STATE; }
-                CHK(dev_upload(h, &L.gface, gf));
-                CHK(dev_upload(h, &L.gpos, gp));
+                static const int fmface[3] = {1, 3, 2};   // un_ele face under sub-element face fi (pamg_face.hip cFMface)
+                std::vector<int4> gt((size_t)std::max(Ul, 1) * 3 * m, make_int4(-1, 0, 0, 0));
+                for (int q = 0; q < Ul; ++q)
+                    for (int f = 1; f <= 3; ++f) {
+                        const int4 g = gf[3 * (size_t)q + f - 1];
+                        for (int sp = 1; sp <= m; ++sp) {
+                            int4 &o = gt[(3 * (size_t)q + f - 1) * m + sp - 1];
+                            if (g.x < 0) { o = make_int4(g.x, 0, 0, 0); continue; }
+                            const int e = E[(g.y - 1) * m + (g.z ? m - sp + 1 : sp) - 1];
+                            const int4 nb = fnb[e];
+                            const int nbf[3] = {nb.x, nb.y, nb.z};
+                            int y[3];
+                            for (int fi = 0; fi < 3; ++fi) {
+                                if (nbf[fi] >= 0) { y[fi] = g.x * ns + nbf[fi]; continue; }
+                                const int mf = fmface[fi], spp = -nbf[fi];
+                                if (mf == g.y) {   // across to this un_ele: its own boundary sub-element
+                                    y[fi] = -1 - E[(f - 1) * m + (g.w ? m - spp + 1 : spp) - 1];
+                                    continue;
+                                }
+                                const int4 g2 = gf[3 * (size_t)g.x + mf - 1];   // a corner: the neighbour's other face
+                                if (g2.x >= 0) y[fi] = g2.x * ns + E[(g2.y - 1) * m + (g2.z ? m - spp + 1 : spp) - 1];
+                                else if (g2.x == -1)
+                                    y[fi] = -(1 + ns + 3 * (L.halo.hface[3 * (size_t)g.x + mf - 1].z + spp - 1) + mf - 1);
+                                else y[fi] = -1 - e;   // another rank: k_face_pp is single-domain (never read)
+                            }
+                            o = make_int4(g.x * ns + e, y[0], y[1], y[2]);
+                        }
+                    }
+                CHK(dev_upload(h, &L.gtab, gt));
             }
         }
         HaloPlan &P = L.halo;

@@ -106,11 +106,12 @@ __device__ __forceinline__ void load_face_rec(const double *__restrict__ stc, co
 // the sub-element's pattern of inner faces (selects omega / D_i, kFaceWD)
 __device__ __forceinline__ int face_pattern(int4 nb) { return (nb.x >= 0) | ((nb.y >= 0) << 1) | ((nb.z >= 0) << 2); }
 
-// face_point's arithmetic from a loaded record; wd(i): omega / D_i of the sub-element's pattern
-template <int MODE, class XIN, class HV, class WD>
-__device__ __forceinline__ void face_apply(const FaceRec &R, const XIN &xin, const double x[3], const double b[3],
-                                           int4 nb, int64_t u, const HV &hv, const WD &wd, int level1, double rdt,
-                                           double out[3]) {
+// face_point's arithmetic from a loaded record and the neighbours' values: yf(fi, c) = component c of the
+// neighbour across sub-element face fi (the inner neighbour's value, or slot -nb of the halo snapshot of
+// un_ele face cFMface[fi]); wd(i): omega / D_i of the sub-element's pattern
+template <int MODE, class YF, class WD>
+__device__ __forceinline__ void face_core(const FaceRec &R, const double x[3], const double b[3], int4 nb, const YF &yf,
+                                          const WD &wd, int level1, double rdt, double out[3]) {
     double A[3];
     apply_A(R.S, rdt, x, A);
     double ds[3] = {0.0, 0.0, 0.0};
@@ -120,8 +121,8 @@ __device__ __forceinline__ void face_apply(const FaceRec &R, const XIN &xin, con
         const int a = cFNode[fi][0], bb = cFNode[fi][1];
         double ya, yb, wf;
         if (nbf[fi] >= 0) {   // inner neighbour: its nodes at my face nodes a, b are its b, a
-            ya = xin(bb, nbf[fi]);
-            yb = xin(a, nbf[fi]);
+            ya = yf(fi, bb);
+            yb = yf(fi, a);
             wf = R.w[fi];
         } else {              // across the un_ele face: the halo (t_overlap slot sp)
             const int mface = cFMface[fi], sx = R.sx[fi];
@@ -129,8 +130,8 @@ __device__ __forceinline__ void face_apply(const FaceRec &R, const XIN &xin, con
                 ya = 0.0;     // coarse levels carry the error equation: homogeneous boundary data
                 yb = 0.0;
             } else {
-                ya = hv(u, mface, -nbf[fi], (sx & 3) - 1);
-                yb = hv(u, mface, -nbf[fi], ((sx >> 2) & 3) - 1);
+                ya = yf(fi, (sx & 3) - 1);
+                yb = yf(fi, ((sx >> 2) & 3) - 1);
             }
             wf = R.w[3 + mface - 1];
         }
@@ -146,6 +147,18 @@ __device__ __forceinline__ void face_apply(const FaceRec &R, const XIN &xin, con
         else if (MODE == 3) out[i] = ai - b[i];
         else out[i] = b[i] - ai;
     }
+}
+
+// face_core with the neighbours read from the tile (xin(c, q): component c at un_ele position q) and the
+// halo snapshot (hv(u, mface, sp, c))
+template <int MODE, class XIN, class HV, class WD>
+__device__ __forceinline__ void face_apply(const FaceRec &R, const XIN &xin, const double x[3], const double b[3],
+                                           int4 nb, int64_t u, const HV &hv, const WD &wd, int level1, double rdt,
+                                           double out[3]) {
+    const int nbf[3] = {nb.x, nb.y, nb.z};
+    face_core<MODE>(R, x, b, nb, [&](int fi, int c) {
+        return nbf[fi] >= 0 ? xin(c, nbf[fi]) : hv(u, cFMface[fi], -nbf[fi], c);
+    }, wd, level1, rdt, out);
 }
 
 // One sub-element of the face-coupled operator (the oracle's face_terms / face_sweep order):
@@ -546,16 +559,16 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 // sweep (the residual point of a smoother stream, with the snapshot the second sweep reads); outputs:
 // out_pre the start iterate, out_mid the iterate after sweep 1 (K = 2), out_end the iterate after the
 // last sweep (none of them aliases A).
-// gface (U x 3): per un_ele face {neighbour v (-1 boundary, -2 another rank), v's face toward it, the rev
-// flag of v's words into it, the rev flag of its words into v}; E (3 m): the storage position of the
-// boundary sub-element at position i of face f.
+// gtab (U x 3 x m, Level::gtab): the gather entry of every halo slot (see the prologue).
+#ifndef PAMG_FACE_PP_WAVES
+#define PAMG_FACE_PP_WAVES 6
+#endif
 template <int TS, int NT, bool RB, int K>
-__global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void k_face_pp(
+__global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
-    const int *__restrict__ fsx, const int4 *__restrict__ gface, const int *__restrict__ E,
-    const int4 *__restrict__ hface, const double2 *__restrict__ bcv, int64_t pitch, int level1, double rdt, int res,
-    double *RESout) {
+    const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
+    const double2 *__restrict__ bcv, int64_t pitch, int level1, double rdt, int res, double *RESout) {
     constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
     static_assert(PER % 2 == 0 && M * M == TS && 3 * M <= NT && (NT < 192 || M <= 64), "whole un_ele tiles, adjacent pairs per thread");
     __shared__ double X[3][TS];
@@ -568,39 +581,46 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
     FaceRec R;
     load_face_rec(stc, fface, fsx, u, R);
     if (t < 24) WD[t] = fface[u * kFaceStride + kFaceWD + t];
-    // the boundary words of face f (1..3) at position sp (1..m) of a domain-boundary face: update_overlaps'
+    // the boundary words of a domain-boundary face mf (1..3) of un_ele uu at slot sp (1..m): update_overlaps'
     // boundary values at the two face nodes (halo_words' placement; the third word is never read)
-    auto bcword = [&](int64_t uu, int f, int sp, int kk) -> double {
-        const double2 v = bcv[hface[3 * uu + f - 1].z + sp - 1];
-        return kk == (f == 3 ? 1 : 0) ? v.x : kk == (f == 2 ? 1 : 2) ? v.y : 0.0;
+    auto bcpair = [&](int bci, int mf, int kk) -> double {
+        const double2 v = bcv[bci];
+        return kk == (mf == 3 ? 1 : 0) ? v.x : kk == (mf == 2 ? 1 : 2) ? v.y : 0.0;
     };
-    // the value of A at the boundary sub-element of neighbour g (gface entry) that faces slot sp
-    auto across = [&](int4 g, int sp, int kk) -> double {
-        const int i = g.z ? M - sp + 1 : sp;
-        return A[kk * pitch + (int64_t)g.x * TS + E[(g.y - 1) * M + i - 1]];
-    };
-    // the snapshot of the first sweep (:555 at its start): the neighbours' boundary values in A. Thread ->
-    // (face fu, slot spu): a face per wave where the workgroup has three waves or more (the neighbour's
-    // records then come through the scalar unit), else packed
+    // halo slot (fu, spu) of this tile: thread t -- a face per wave where the workgroup has three waves or
+    // more (the neighbour's operator record then comes through the scalar unit), else packed. Its gather
+    // entry (Level::gtab) names, for the neighbour's boundary sub-element e facing the slot, e's global
+    // index and, per face of e, the global index of the value across it (>= 0), this tile's own position
+    // p as -1 - p, or a boundary word as -(1 + TS + 3 bcv index + face - 1): every operand load of the
+    // ghost update below is issued here, at the launch's start, beside the tile's own loads
     constexpr bool WAVEF = NT >= 192;
-    int4 gu = make_int4(-1, 0, 0, 0);
     const int fu = WAVEF ? t / 64 + 1 : t / M + 1;
     const int spu = WAVEF ? (t & 63) + 1 : t - (fu - 1) * M + 1;
     const bool gon = fu <= 3 && spu <= M;
     const int hq = 3 * ((fu - 1) * M + spu - 1);   // the slot's first word in HI
-    if (fu <= 3) {
-        gu = gface[3 * u + fu - 1];
-        if (WAVEF) {
-            gu.x = __builtin_amdgcn_readfirstlane(gu.x);
-            gu.y = __builtin_amdgcn_readfirstlane(gu.y);
-            gu.z = __builtin_amdgcn_readfirstlane(gu.z);
-            gu.w = __builtin_amdgcn_readfirstlane(gu.w);
+    int4 ge = make_int4(-1, -1, -1, -1);
+    if (gon) ge = gtab[(u * 3 + fu - 1) * M + spu - 1];
+    double xe[3] = {0.0, 0.0, 0.0}, be[3] = {0.0, 0.0, 0.0}, yv[3][3];
+    int4 nbe = make_int4(0, 0, 0, 0);
+    if (gon && ge.x >= 0) {
+        const int e = ge.x & (TS - 1);
+        nbe = fnb[e];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            xe[c] = A[c * pitch + ge.x];
+            if (K == 2) be[c] = RHS[c * pitch + ge.x];
+        }
+        if constexpr (K == 2) {
+            const int yy[3] = {ge.y, ge.z, ge.w};
+#pragma unroll
+            for (int fi = 0; fi < 3; ++fi)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    yv[fi][c] = yy[fi] >= 0 ? A[c * pitch + yy[fi]]
+                                : yy[fi] <= -(1 + TS) ? bcpair((-(yy[fi] + 1 + TS)) / 3, (-(yy[fi] + 1 + TS)) % 3 + 1, c)
+                                                      : 0.0;   // this tile's own value: from LDS below
         }
     }
-    if (gon)
-#pragma unroll
-        for (int kk = 0; kk < 3; ++kk)
-            HI[0][hq + kk] = gu.x >= 0 ? across(gu, spu, kk) : gu.x == -1 ? bcword(u, fu, spu, kk) : 0.0;
 #pragma unroll
     for (int k = 0; k < PER; k += 2) {   // the iterate into LDS, pairs
         const int j = 2 * (t + NT * (k / 2));
@@ -616,35 +636,32 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
             if (out_pre) st2(out_pre + c * pitch + s0 + j, v);
         }
     }
+    // the snapshot of the first sweep (:555 at its start): the neighbours' boundary values in A, or this
+    // tile's boundary words
+    if (gon)
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk)
+            HI[0][hq + kk] = ge.x >= 0 ? xe[kk] : ge.x == -1 ? bcpair(hface[3 * u + fu - 1].z + spu - 1, fu, kk) : 0.0;
     __syncthreads();
     if constexpr (K == 2) {
-        // the neighbours' boundary sub-elements after the first sweep: the second sweep's snapshot
+        // the neighbour's boundary sub-element e after the first sweep (an up one: its sweep reads its down
+        // neighbours, unchanged since the previous sweep, and the snapshot across its faces): the second
+        // sweep's snapshot -- face_core on v's record and the values gathered above
         if (gon) {
-            if (gu.x >= 0) {
-                const int64_t v = gu.x;
-                const int fv = gu.y;
-                const int i = gu.z ? M - spu + 1 : spu;   // v's boundary position facing this slot
-                const int e = E[(fv - 1) * M + i - 1];
-                const int4 nb = fnb[e];
+            if (ge.x >= 0) {
+                const int64_t v = WAVEF ? __builtin_amdgcn_readfirstlane(ge.x / TS) : ge.x / TS;   // one face a wave
                 FaceRec Rv;
                 load_face_rec(stc, fface, fsx, v, Rv);
-                const double *wd = fface + v * kFaceStride + kFaceWD + 3 * face_pattern(nb);
-                double x[3], be[3], r[3];
+                const double *wd = fface + v * kFaceStride + kFaceWD + 3 * face_pattern(nbe);
+                const int yy[3] = {ge.y, ge.z, ge.w};
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    x[c] = HI[0][hq + c];   // = A at v's e
-                    be[c] = RHS[c * pitch + v * TS + e];
-                }
-                auto xv = [&](int c, int q) { return A[c * pitch + v * TS + q]; };
-                auto hvv = [&](int64_t, int mf, int sp, int kk) -> double {
-                    if (mf == fv) {   // this tile's own boundary value at the sweep's start
-                        const int iu = gu.w ? M - sp + 1 : sp;
-                        return X[kk][E[(fu - 1) * M + iu - 1]];
-                    }
-                    const int4 g2 = gface[3 * v + mf - 1];   // a corner: v's other neighbour w, or the boundary
-                    return g2.x >= 0 ? across(g2, sp, kk) : g2.x == -1 ? bcword(v, mf, sp, kk) : 0.0;
-                };
-                face_apply<RB ? 0 : 2>(Rv, xv, x, be, nb, v, hvv, [&](int q) { return wd[q]; }, level1, rdt, r);
+                for (int fi = 0; fi < 3; ++fi)
+                    if (yy[fi] < 0 && yy[fi] > -(1 + TS))
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) yv[fi][c] = X[c][-1 - yy[fi]];
+                double r[3];
+                face_core<RB ? 0 : 2>(Rv, xe, be, nbe, [&](int fi, int c) { return yv[fi][c]; },
+                                      [&](int q) { return wd[q]; }, level1, rdt, r);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) HI[1][hq + c] = r[c];
             } else {
@@ -1500,7 +1517,7 @@ static hipError_t launch_coresident(const void *f, int grid, int nt, void **args
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
                           double *out_end, bool rb, bool level1, double rdt, int res) {
     if (L.N == 0) return hipSuccess;
-    if (!face_tile_shape(L) || !L.fnb || !L.gface || !L.gpos || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)))
+    if (!face_tile_shape(L) || !L.fnb || !L.gtab || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)))
         return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
     const dim3 g((unsigned)(L.N / L.nsub));
@@ -1508,7 +1525,7 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
     double *R = res ? L.RES : nullptr;
 #define PAMG_FPP(TS, NT, RB_, K_)                                                                                    \
     hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, L.RHS, L.stc,  \
-                       L.fnb, L.fface, L.fsx, L.gface, L.gpos, P.d_hface, P.d_bcv, L.pitch, l1, rdt, res, R)
+                       L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.pitch, l1, rdt, res, R)
 #define PAMG_FPPK(TS, NT)                                          \
     if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \
     else { if (K == 2) PAMG_FPP(TS, NT, false, 2); else PAMG_FPP(TS, NT, false, 1); }

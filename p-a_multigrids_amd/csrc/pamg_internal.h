@@ -117,11 +117,11 @@ struct Level {
     // (fnb.w != 0, ascending), then of the down ones -- nup + ndn = nsub
     int *cpos = nullptr;
     int nup = 0, ndn = 0;
-    // the two-sweep passes (k_face_pp): per local un_ele face {neighbour (-1 boundary, -2 another rank), its
-    // face toward this one, rev of its words into this one, rev of this one's words into it}, and the storage
-    // positions of the boundary sub-elements by face and position along it (3 m)
-    int4 *gface = nullptr;
-    int *gpos = nullptr;
+    // the two-sweep passes (k_face_pp): per (local un_ele, face, halo slot) the gather entry of the
+    // neighbour's boundary sub-element e facing the slot -- {e's global index (-1 boundary face, -2 another
+    // rank), then per face of e the global index of the value across it, -1 - p for this un_ele's own
+    // position p, or -(1 + nsub + 3 bcv index + face - 1) for a boundary word}
+    int4 *gtab = nullptr;
     // every sub-element with halo words (HaloPlan::hsub) is an up one: the chain publishes a
     // sweep's words right after its up pass (k_face_chain, early)
     bool words_up = false;
