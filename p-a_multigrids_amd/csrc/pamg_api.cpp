@@ -987,7 +987,7 @@ bool face_pp_ok(pamg_handle *h, int l) {
     const char *ev = getenv("PAMG_FACE_PP");   // read per call: tests switch it within a process
     if (ev && atoi(ev) == 0) return false;
     const Level &L = h->lv[l];
-    return face_fusable(h, l) && face_tile_shape(L) && L.gtab && (h->p.solver != 3 || L.words_up);
+    return face_fusable(h, l) && face_tile_shape(L) && L.nsub <= 1024 && L.gtab && (h->p.solver != 3 || L.words_up);
 }
 
 struct PPPass { int K, res; double *in, *pre, *mid, *end; };
@@ -1085,6 +1085,11 @@ int face_pp_level(pamg_handle *h, int l, bool last) {
 int vcycle_face_pp(pamg_handle *h, int n) {
     const int ns = h->p.n_smooth;
     if (n <= 0) return PAMG_OK;
+    if (!face_pp_ok(h, 1)) {   // level 1 as its two calls per cycle, a coarser level as a stream
+        for (int c = 0; c < n; ++c) CHK(face_pp_level(h, 1, c + 1 == n));
+        h->tnn_level = 1;
+        return face_chain_check(h);
+    }
     // level 1: one stream over the call's cycles, get_residual after each cycle's restriction leg
     const int per = 2 * (ns - 1);
     std::vector<int> res_at;
@@ -1108,7 +1113,9 @@ int vcycle_face_pp(pamg_handle *h, int n) {
 }
 
 int vcycle_face_fused(pamg_handle *h, int n) {
-    if (h->p.multi_levels >= 2 && h->p.n_smooth >= 2 && face_pp_ok(h, 1)) return vcycle_face_pp(h, n);
+    if (h->p.multi_levels >= 2 && h->p.n_smooth >= 2)
+        for (int l = 1; l < h->p.multi_levels; ++l)
+            if (face_pp_ok(h, l)) return vcycle_face_pp(h, n);
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     const double rdt = 1 / h->p.dt;
     for (int c = 0; c < n; ++c) {

@@ -542,7 +542,7 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 }
 
 // ---- two sweeps per HBM pass (temporal blocking) of a level whose tile is one un_ele (k_face_tile's
-// levels: 256, 1,024, 4,096 sub-elements; single domain). Every sweep reads its cross-un_ele values from
+// levels of 256 and 1,024 sub-elements; single domain). Every sweep reads its cross-un_ele values from
 // a snapshot of the neighbours' iterate at the sweep's start (:555, Jacobi across un_ele faces, red-black
 // or Jacobi inside). Here the snapshot is not published through t_overlap: the launch reads its input
 // iterate A (written by the previous launch, read-only in this one -- its output goes to another buffer)
@@ -564,25 +564,30 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #define PAMG_FACE_PP_WAVES 6
 #endif
 template <int TS, int NT, bool RB, int K>
-__global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
+__global__ __launch_bounds__(NT, RB ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
     const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
-    const double2 *__restrict__ bcv, int64_t pitch, int level1, double rdt, int res, double *RESout) {
+    const double2 *__restrict__ bcv, const int *__restrict__ cpos, int nup, int64_t pitch, int level1, double rdt,
+    int res, double *RESout) {
     constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
-    static_assert(PER % 2 == 0 && M * M == TS && 3 * M <= NT && (NT < 192 || M <= 64), "whole un_ele tiles, adjacent pairs per thread");
-    __shared__ double X[3][TS];
-    __shared__ double HI[K][NH];
-    __shared__ double WD[24];
+    // red-black: the colour passes run over colour lists (Level::cpos), every lane with an item of the colour
+    constexpr int NUP = M * (M + 1) / 2, KU = RB ? (NUP + NT - 1) / NT : PER, KD = RB ? (TS - NUP + NT - 1) / NT : 0;
+    static_assert(PER % 2 == 0 && M * M == TS && 3 * M <= NT && TS <= 1024, "whole un_ele tiles of <= 1,024, adjacent pairs per thread");
+    // one LDS array: the iterate, the RHS, the halo snapshot of each sweep, omega / D
+    constexpr int OX = 0, OB = 3 * TS, OH = 6 * TS, OW = 6 * TS + K * NH;
+    __shared__ double LDSM[OW + 24];
+    double (*X)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OX);
+    double (*B)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OB);
+    double *WD = LDSM + OW;
+    auto HI = [&](int snap) { return LDSM + OH + snap * NH; };
     const int t = threadIdx.x;
     const int64_t u = blockIdx.x, s0 = u * TS;
-    int4 nbr[PER];
-    double b[PER][3];
     FaceRec R;
     load_face_rec(stc, fface, fsx, u, R);
     if (t < 24) WD[t] = fface[u * kFaceStride + kFaceWD + t];
-    // the boundary words of a domain-boundary face mf (1..3) of un_ele uu at slot sp (1..m): update_overlaps'
-    // boundary values at the two face nodes (halo_words' placement; the third word is never read)
+    // the boundary words of a domain-boundary face mf (1..3) at bcv index bci: update_overlaps' boundary values
+    // at the two face nodes (halo_words' placement; the third word is never read)
     auto bcpair = [&](int bci, int mf, int kk) -> double {
         const double2 v = bcv[bci];
         return kk == (mf == 3 ? 1 : 0) ? v.x : kk == (mf == 2 ? 1 : 2) ? v.y : 0.0;
@@ -597,14 +602,13 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_PP_WAVES : 1) vo
     const int fu = WAVEF ? t / 64 + 1 : t / M + 1;
     const int spu = WAVEF ? (t & 63) + 1 : t - (fu - 1) * M + 1;
     const bool gon = fu <= 3 && spu <= M;
-    const int hq = 3 * ((fu - 1) * M + spu - 1);   // the slot's first word in HI
+    const int hq = 3 * ((fu - 1) * M + spu - 1);   // the slot's first word in a snapshot
     int4 ge = make_int4(-1, -1, -1, -1);
     if (gon) ge = gtab[(u * 3 + fu - 1) * M + spu - 1];
     double xe[3] = {0.0, 0.0, 0.0}, be[3] = {0.0, 0.0, 0.0}, yv[3][3];
     int4 nbe = make_int4(0, 0, 0, 0);
     if (gon && ge.x >= 0) {
-        const int e = ge.x & (TS - 1);
-        nbe = fnb[e];
+        nbe = fnb[ge.x & (TS - 1)];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             xe[c] = A[c * pitch + ge.x];
@@ -621,18 +625,31 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_PP_WAVES : 1) vo
                                                       : 0.0;   // this tile's own value: from LDS below
         }
     }
+    // the thread's items: red-black -- KU up and KD down positions from the colour lists; Jacobi -- its PER
+    // positions (adjacent pairs)
+    int ij[KU + KD];
+    int4 inb[KU + KD];
 #pragma unroll
-    for (int k = 0; k < PER; k += 2) {   // the iterate into LDS, pairs
+    for (int k = 0; k < KU + KD; ++k) {
+        if constexpr (RB) {
+            const int i = k < KU ? t + NT * k : NUP + t + NT * (k - KU);
+            ij[k] = (k < KU ? i < NUP : i < TS) ? cpos[i] : -1;
+        } else {
+            ij[k] = 2 * (t + NT * (k / 2)) + (k & 1);
+        }
+        inb[k] = fnb[ij[k] < 0 ? 0 : ij[k]];
+    }
+    (void)nup;
+#pragma unroll
+    for (int k = 0; k < PER; k += 2) {   // the iterate and the RHS into LDS, adjacent pairs
         const int j = 2 * (t + NT * (k / 2));
-        nbr[k] = fnb[j];
-        nbr[k + 1] = fnb[j + 1];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const double2 v = ld2(A + c * pitch + s0 + j), r = ld2(RHS + c * pitch + s0 + j);
-            b[k][c] = r.x;
-            b[k + 1][c] = r.y;
             X[c][j] = v.x;
             X[c][j + 1] = v.y;
+            B[c][j] = r.x;
+            B[c][j + 1] = r.y;
             if (out_pre) st2(out_pre + c * pitch + s0 + j, v);
         }
     }
@@ -641,7 +658,15 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_PP_WAVES : 1) vo
     if (gon)
 #pragma unroll
         for (int kk = 0; kk < 3; ++kk)
-            HI[0][hq + kk] = ge.x >= 0 ? xe[kk] : ge.x == -1 ? bcpair(hface[3 * u + fu - 1].z + spu - 1, fu, kk) : 0.0;
+            HI(0)[hq + kk] = ge.x >= 0 ? xe[kk] : ge.x == -1 ? bcpair(hface[3 * u + fu - 1].z + spu - 1, fu, kk) : 0.0;
+    // the neighbour's operator record for the ghost update (scalar loads, in flight across the barrier)
+    FaceRec Rv;
+    const double *wdv = nullptr;
+    if (K == 2 && gon && ge.x >= 0) {
+        const int64_t v = WAVEF ? __builtin_amdgcn_readfirstlane(ge.x / TS) : ge.x / TS;   // one face a wave
+        load_face_rec(stc, fface, fsx, v, Rv);
+        wdv = fface + v * kFaceStride + kFaceWD + 3 * face_pattern(nbe);
+    }
     __syncthreads();
     if constexpr (K == 2) {
         // the neighbour's boundary sub-element e after the first sweep (an up one: its sweep reads its down
@@ -649,10 +674,6 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_PP_WAVES : 1) vo
         // sweep's snapshot -- face_core on v's record and the values gathered above
         if (gon) {
             if (ge.x >= 0) {
-                const int64_t v = WAVEF ? __builtin_amdgcn_readfirstlane(ge.x / TS) : ge.x / TS;   // one face a wave
-                FaceRec Rv;
-                load_face_rec(stc, fface, fsx, v, Rv);
-                const double *wd = fface + v * kFaceStride + kFaceWD + 3 * face_pattern(nbe);
                 const int yy[3] = {ge.y, ge.z, ge.w};
 #pragma unroll
                 for (int fi = 0; fi < 3; ++fi)
@@ -661,67 +682,73 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_PP_WAVES : 1) vo
                         for (int c = 0; c < 3; ++c) yv[fi][c] = X[c][-1 - yy[fi]];
                 double r[3];
                 face_core<RB ? 0 : 2>(Rv, xe, be, nbe, [&](int fi, int c) { return yv[fi][c]; },
-                                      [&](int q) { return wd[q]; }, level1, rdt, r);
+                                      [&](int q) { return wdv[q]; }, level1, rdt, r);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) HI[1][hq + c] = r[c];
+                for (int c = 0; c < 3; ++c) HI(1)[hq + c] = r[c];
             } else {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) HI[1][hq + c] = HI[0][hq + c];   // boundary words: constant
+                for (int c = 0; c < 3; ++c) HI(1)[hq + c] = HI(0)[hq + c];   // boundary words: constant
             }
         }
         __syncthreads();   // the ghost updates read the start iterate (X) before the sweeps rewrite it
     }
     auto xin = [&](int c, int q) { return X[c][q]; };
+    // one item k: face_apply<MODE> of position ij[k] from the tile, the RHS and snapshot snap
+    auto item = [&](auto mc, int k, int snap, double r[3]) {
+        constexpr int MODE = decltype(mc)::value;
+        const int j = ij[k];
+        const double *H = HI(snap);
+        auto hv = [&](int64_t, int mf, int sp, int kk) { return H[((mf - 1) * M + sp - 1) * 3 + kk]; };
+        double x[3], bb[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            x[c] = X[c][j];
+            bb[c] = B[c][j];
+        }
+        const int wb = 3 * face_pattern(inb[k]);
+        face_apply<MODE>(R, xin, x, bb, inb[k], u, hv, [&](int i) { return MODE == 3 ? 0.0 : WD[wb + i]; }, level1, rdt, r);
+    };
     auto residual = [&](int snap) {   // get_residual (A x - RHS) of the tile's iterate with snapshot snap
-        auto hv = [&](int64_t, int mf, int sp, int kk) { return HI[snap][((mf - 1) * M + sp - 1) * 3 + kk]; };
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int j = 2 * (t + NT * (k / 2)) + (k & 1);
-            double x[3], r[3];
+        for (int k = 0; k < KU + KD; ++k) {
+            if (ij[k] < 0) continue;
+            double r[3];
+            item(std::integral_constant<int, 3>{}, k, snap, r);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) x[c] = X[c][j];
-            face_apply<3>(R, xin, x, b[k], nbr[k], u, hv, [&](int) { return 0.0; }, level1, rdt, r);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) RESout[c * pitch + s0 + j] = r[c];
+            for (int c = 0; c < 3; ++c) RESout[c * pitch + s0 + ij[k]] = r[c];
         }
         __syncthreads();   // every read of the iterate before the passes rewrite it
     };
     auto sweep = [&](int snap) {
-        auto hv = [&](int64_t, int mf, int sp, int kk) { return HI[snap][((mf - 1) * M + sp - 1) * 3 + kk]; };
-        auto pass = [&](auto mc) {
-            constexpr int MODE = decltype(mc)::value;
-            double r[PER][3];
-            bool on[PER];
+        if constexpr (RB) {   // up items, then down items, in place (a colour reads only the other)
 #pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const int j = 2 * (t + NT * (k / 2)) + (k & 1);
-                const int4 nb = nbr[k];
-                on[k] = !((MODE == 0 && !nb.w) || (MODE == 1 && nb.w));
-                if (!on[k]) continue;
-                double x[3];
+            for (int k = 0; k < KU; ++k) {
+                if (ij[k] < 0) continue;
+                double r[3];
+                item(std::integral_constant<int, 0>{}, k, snap, r);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) x[c] = X[c][j];
-                const int wb = 3 * face_pattern(nb);
-                face_apply<MODE>(R, xin, x, b[k], nb, u, hv, [&](int i) { return WD[wb + i]; }, level1, rdt, r[k]);
-                if (MODE != 2)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) X[c][j] = r[k][c];
-            }
-            if (MODE == 2) {
-                __syncthreads();
-#pragma unroll
-                for (int k = 0; k < PER; ++k)
-                    if (on[k])
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) X[c][2 * (t + NT * (k / 2)) + (k & 1)] = r[k][c];
+                for (int c = 0; c < 3; ++c) X[c][ij[k]] = r[c];
             }
             __syncthreads();
-        };
-        if constexpr (RB) {
-            pass(std::integral_constant<int, 0>{});
-            pass(std::integral_constant<int, 1>{});
-        } else {
-            pass(std::integral_constant<int, 2>{});
+#pragma unroll
+            for (int k = KU; k < KU + KD; ++k) {
+                if (ij[k] < 0) continue;
+                double r[3];
+                item(std::integral_constant<int, 1>{}, k, snap, r);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) X[c][ij[k]] = r[c];
+            }
+            __syncthreads();
+        } else {   // Jacobi: every read of the old iterate before any write
+            double r[KU][3];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) item(std::integral_constant<int, 2>{}, k, snap, r[k]);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KU; ++k)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) X[c][ij[k]] = r[k][c];
+            __syncthreads();
         }
     };
     auto store = [&](double *o) {
@@ -1517,7 +1544,9 @@ static hipError_t launch_coresident(const void *f, int grid, int nt, void **args
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
                           double *out_end, bool rb, bool level1, double rdt, int res) {
     if (L.N == 0) return hipSuccess;
-    if (!face_tile_shape(L) || !L.fnb || !L.gtab || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)))
+    const int m = L.nsub == 256 ? 16 : L.nsub == 1024 ? 32 : 64;
+    if (!face_tile_shape(L) || !L.fnb || !L.gtab || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)) ||
+        (rb && (!L.cpos || L.nup != m * (m + 1) / 2)))
         return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
     const dim3 g((unsigned)(L.N / L.nsub));
@@ -1525,13 +1554,13 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
     double *R = res ? L.RES : nullptr;
 #define PAMG_FPP(TS, NT, RB_, K_)                                                                                    \
     hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, L.RHS, L.stc,  \
-                       L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.pitch, l1, rdt, res, R)
+                       L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.cpos, L.nup, L.pitch, l1, rdt, res, R)
 #define PAMG_FPPK(TS, NT)                                          \
     if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \
     else { if (K == 2) PAMG_FPP(TS, NT, false, 2); else PAMG_FPP(TS, NT, false, 1); }
-    if (L.nsub == 4096) { PAMG_FPPK(4096, 1024) }
-    else if (L.nsub == 1024) { PAMG_FPPK(1024, 512) }
-    else { PAMG_FPPK(256, 128) }
+    if (L.nsub == 1024) { PAMG_FPPK(1024, 512) }
+    else if (L.nsub == 256) { PAMG_FPPK(256, 128) }
+    else return hipErrorInvalidValue;   // (4,096: the iterate and RHS exceed the LDS)
 #undef PAMG_FPPK
 #undef PAMG_FPP
     return hipGetLastError();
