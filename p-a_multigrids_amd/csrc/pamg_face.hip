@@ -35,8 +35,11 @@ namespace {
 
 using namespace detail;
 
-__constant__ int cFNode[3][2] = {{0, 2}, {2, 1}, {1, 0}};   // face_nodes, 0-based (:142-147)
-__constant__ int cFMface[3] = {1, 3, 2};                     // the un_ele face under sub-element face f
+// face_nodes, 0-based (:142-147), and the un_ele face under sub-element face f -- compile-time, so that
+// every index derived from them in the unrolled face loops is a constant (a register array or record
+// indexed at run time goes to scratch)
+__host__ __device__ constexpr int fnode(int fi, int k) { return fi == 0 ? (k ? 2 : 0) : fi == 1 ? (k ? 1 : 2) : (k ? 0 : 1); }
+__host__ __device__ constexpr int fmface(int fi) { return fi == 0 ? 1 : fi == 1 ? 3 : 2; }
 
 // halo words of level L from its tnew, the sweep start: copy = tnew := tnew_nonlin first (:550)
 __global__ __launch_bounds__(kBlock) void k_face_halo(double *T, const double *__restrict__ TNN, int64_t pitch,
@@ -100,7 +103,7 @@ __device__ __forceinline__ void load_face_rec(const double *__restrict__ stc, co
 #pragma unroll
     for (int q = 0; q < 6; ++q) R.w[q] = fface[u * kFaceStride + q];
 #pragma unroll
-    for (int fi = 0; fi < 3; ++fi) R.sx[fi] = fsx[4 * u + cFMface[fi] - 1];
+    for (int fi = 0; fi < 3; ++fi) R.sx[fi] = fsx[4 * u + fmface(fi) - 1];
 }
 
 // the sub-element's pattern of inner faces (selects omega / D_i, kFaceWD)
@@ -108,7 +111,7 @@ __device__ __forceinline__ int face_pattern(int4 nb) { return (nb.x >= 0) | ((nb
 
 // face_point's arithmetic from a loaded record and the neighbours' values: yf(fi, c) = component c of the
 // neighbour across sub-element face fi (the inner neighbour's value, or slot -nb of the halo snapshot of
-// un_ele face cFMface[fi]); wd(i): omega / D_i of the sub-element's pattern
+// un_ele face fmface(fi)); wd(i): omega / D_i of the sub-element's pattern
 template <int MODE, class YF, class WD>
 __device__ __forceinline__ void face_core(const FaceRec &R, const double x[3], const double b[3], int4 nb, const YF &yf,
                                           const WD &wd, int level1, double rdt, double out[3]) {
@@ -118,14 +121,14 @@ __device__ __forceinline__ void face_core(const FaceRec &R, const double x[3], c
     const int nbf[3] = {nb.x, nb.y, nb.z};
 #pragma unroll
     for (int fi = 0; fi < 3; ++fi) {
-        const int a = cFNode[fi][0], bb = cFNode[fi][1];
+        const int a = fnode(fi, 0), bb = fnode(fi, 1);
         double ya, yb, wf;
         if (nbf[fi] >= 0) {   // inner neighbour: its nodes at my face nodes a, b are its b, a
             ya = yf(fi, bb);
             yb = yf(fi, a);
             wf = R.w[fi];
         } else {              // across the un_ele face: the halo (t_overlap slot sp)
-            const int mface = cFMface[fi], sx = R.sx[fi];
+            const int mface = fmface(fi), sx = R.sx[fi];
             if (!level1 && (sx & 16)) {
                 ya = 0.0;     // coarse levels carry the error equation: homogeneous boundary data
                 yb = 0.0;
@@ -149,16 +152,47 @@ __device__ __forceinline__ void face_core(const FaceRec &R, const double x[3], c
     }
 }
 
-// face_core with the neighbours read from the tile (xin(c, q): component c at un_ele position q) and the
-// halo snapshot (hv(u, mface, sp, c))
+// face_core's arithmetic with the neighbours read from the tile (xin(c, q): component c at un_ele position
+// q) and the halo snapshot (hv(u, mface, sp, c)) -- written out rather than through face_core's accessor,
+// which put the record in scratch in the tile kernels; the same operations in the same order (the
+// two-sweep passes' ghost updates use face_core: tests/test_face_operator.py holds them bitwise equal)
 template <int MODE, class XIN, class HV, class WD>
 __device__ __forceinline__ void face_apply(const FaceRec &R, const XIN &xin, const double x[3], const double b[3],
                                            int4 nb, int64_t u, const HV &hv, const WD &wd, int level1, double rdt,
                                            double out[3]) {
+    double A[3];
+    apply_A(R.S, rdt, x, A);
+    double ds[3] = {0.0, 0.0, 0.0};
     const int nbf[3] = {nb.x, nb.y, nb.z};
-    face_core<MODE>(R, x, b, nb, [&](int fi, int c) {
-        return nbf[fi] >= 0 ? xin(c, nbf[fi]) : hv(u, cFMface[fi], -nbf[fi], c);
-    }, wd, level1, rdt, out);
+#pragma unroll
+    for (int fi = 0; fi < 3; ++fi) {
+        const int a = fnode(fi, 0), bb = fnode(fi, 1);
+        double ya, yb, wf;
+        if (nbf[fi] >= 0) {   // inner neighbour: its nodes at my face nodes a, b are its b, a
+            ya = xin(bb, nbf[fi]);
+            yb = xin(a, nbf[fi]);
+            wf = R.w[fi];
+        } else {              // across the un_ele face: the halo (t_overlap slot sp)
+            const int mface = fmface(fi), sx = R.sx[fi];
+            if (!level1 && (sx & 16)) {
+                ya = 0.0;     // coarse levels carry the error equation: homogeneous boundary data
+                yb = 0.0;
+            } else {
+                ya = hv(u, mface, -nbf[fi], (sx & 3) - 1);
+                yb = hv(u, mface, -nbf[fi], ((sx >> 2) & 3) - 1);
+            }
+            wf = R.w[3 + mface - 1];
+        }
+        ds[a] = ds[a] + wf * (((2.0 * x[a] + x[bb]) - 2.0 * ya) - yb);
+        ds[bb] = ds[bb] + wf * (((x[a] + 2.0 * x[bb]) - ya) - 2.0 * yb);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double ai = A[i] + ds[i];
+        if (MODE <= 2) out[i] = x[i] + wd(i) * (b[i] - ai);
+        else if (MODE == 3) out[i] = ai - b[i];
+        else out[i] = b[i] - ai;
+    }
 }
 
 // One sub-element of the face-coupled operator (the oracle's face_terms / face_sweep order):
@@ -681,7 +715,10 @@ __global__ __launch_bounds__(NT, RB ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
 #pragma unroll
                         for (int c = 0; c < 3; ++c) yv[fi][c] = X[c][-1 - yy[fi]];
                 double r[3];
-                face_core<RB ? 0 : 2>(Rv, xe, be, nbe, [&](int fi, int c) { return yv[fi][c]; },
+                // (the component of a halo word is a run-time selector: picked by selects, so that yv stays in
+                // registers)
+                face_core<RB ? 0 : 2>(Rv, xe, be, nbe,
+                                      [&](int fi, int c) { return c == 0 ? yv[fi][0] : c == 1 ? yv[fi][1] : yv[fi][2]; },
                                       [&](int q) { return wdv[q]; }, level1, rdt, r);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) HI(1)[hq + c] = r[c];
@@ -1099,7 +1136,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
             else if (q < 13) v = stc[u * kStcStride + kStcW + q - 10];
             else if (q < 19) v = fface[u * kFaceStride + q - 13];
             else if (q < 43) v = fface[u * kFaceStride + kFaceWD + q - 19];
-            else if (q < 46) v = (double)fsx[4 * u + cFMface[q - 43] - 1];
+            else if (q < 46) v = (double)fsx[4 * u + fmface(q - 43) - 1];
             RS[i] = v;
         }
     }
