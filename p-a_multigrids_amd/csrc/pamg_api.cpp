@@ -983,11 +983,15 @@ bool face_cycle_fusable(pamg_handle *h) {
 // tnew once, after the call -- what the per-step sequence's last writer, level 1's last smoother call,
 // leaves (every coarser level writes a subset of its slots). Bitwise the per-step sequence
 // (tests/test_face_operator.py). PAMG_FACE_PP=0 keeps the one-sweep launches (A/B).
+// PAMG_FACE_PP: a mask of the level sizes that stream -- bit 0 levels of 1,024 sub-elements per un_ele,
+// bit 1 of 256; 0 none. Default 1: the 256-element launches (two waves a workgroup) measured slower as
+// two-sweep passes than as one-sweep launches (profiles/r04_d_face_pp.txt)
 bool face_pp_ok(pamg_handle *h, int l) {
     const char *ev = getenv("PAMG_FACE_PP");   // read per call: tests switch it within a process
-    if (ev && atoi(ev) == 0) return false;
+    const int mask = ev ? atoi(ev) : 1;
     const Level &L = h->lv[l];
-    return face_fusable(h, l) && face_tile_shape(L) && L.nsub <= 1024 && L.gtab && (h->p.solver != 3 || L.words_up);
+    const int bit = L.nsub == 1024 ? 1 : L.nsub == 256 ? 2 : 0;
+    return (mask & bit) && face_fusable(h, l) && face_tile_shape(L) && L.gtab && (h->p.solver != 3 || L.words_up);
 }
 
 struct PPPass { int K, res; double *in, *pre, *mid, *end; };

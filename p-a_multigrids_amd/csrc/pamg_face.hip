@@ -597,6 +597,9 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_WAVES
 #define PAMG_FACE_PP_WAVES 6
 #endif
+#ifndef PAMG_FACE_PP_BLDS
+#define PAMG_FACE_PP_BLDS 1
+#endif
 template <int TS, int NT, bool RB, int K>
 __global__ __launch_bounds__(NT, RB ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, const double *__restrict__ RHS,
@@ -609,7 +612,10 @@ __global__ __launch_bounds__(NT, RB ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
     constexpr int NUP = M * (M + 1) / 2, KU = RB ? (NUP + NT - 1) / NT : PER, KD = RB ? (TS - NUP + NT - 1) / NT : 0;
     static_assert(PER % 2 == 0 && M * M == TS && 3 * M <= NT && TS <= 1024, "whole un_ele tiles of <= 1,024, adjacent pairs per thread");
     // one LDS array: the iterate, the RHS, the halo snapshot of each sweep, omega / D
-    constexpr int OX = 0, OB = 3 * TS, OH = 6 * TS, OW = 6 * TS + K * NH;
+    // PAMG_FACE_PP_BLDS (A/B): 1 the RHS staged in LDS beside the iterate; 0 each item's RHS in registers,
+    // loaded from memory at its position (less LDS: more workgroups per CU)
+    constexpr bool BL = PAMG_FACE_PP_BLDS != 0;
+    constexpr int OX = 0, OB = 3 * TS, OH = (BL ? 6 : 3) * TS, OW = OH + K * NH;
     __shared__ double LDSM[OW + 24];
     double (*X)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OX);
     double (*B)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OB);
@@ -673,17 +679,25 @@ __global__ __launch_bounds__(NT, RB ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
         }
         inb[k] = fnb[ij[k] < 0 ? 0 : ij[k]];
     }
+    double ib[KU + KD][3];   // the items' RHS (BL = 0)
+    if constexpr (!BL)
+#pragma unroll
+        for (int k = 0; k < KU + KD; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) ib[k][c] = RHS[c * pitch + s0 + (ij[k] < 0 ? 0 : ij[k])];
     (void)nup;
 #pragma unroll
     for (int k = 0; k < PER; k += 2) {   // the iterate and the RHS into LDS, adjacent pairs
         const int j = 2 * (t + NT * (k / 2));
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const double2 v = ld2(A + c * pitch + s0 + j), r = ld2(RHS + c * pitch + s0 + j);
+            const double2 v = ld2(A + c * pitch + s0 + j), r = BL ? ld2(RHS + c * pitch + s0 + j) : make_double2(0.0, 0.0);
             X[c][j] = v.x;
             X[c][j + 1] = v.y;
-            B[c][j] = r.x;
-            B[c][j + 1] = r.y;
+            if (BL) {
+                B[c][j] = r.x;
+                B[c][j + 1] = r.y;
+            }
             if (out_pre) st2(out_pre + c * pitch + s0 + j, v);
         }
     }
@@ -740,7 +754,7 @@ __global__ __launch_bounds__(NT, RB ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             x[c] = X[c][j];
-            bb[c] = B[c][j];
+            bb[c] = BL ? B[c][j] : ib[k][c];
         }
         const int wb = 3 * face_pattern(inb[k]);
         face_apply<MODE>(R, xin, x, bb, inb[k], u, hv, [&](int i) { return MODE == 3 ? 0.0 : WD[wb + i]; }, level1, rdt, r);

@@ -5,6 +5,7 @@ SQ_BUSY_CYCLES are quad-cycle counts). usage: pmc_kernels.py FILTER DIR [DIR ...
 import collections
 import csv
 import glob
+import re
 import sys
 
 filt = sys.argv[1]
@@ -16,7 +17,8 @@ for d in sys.argv[2:]:
             name = r["Kernel_Name"]
             if filt not in name:
                 continue
-            key = name.split("(")[0][:90]
+            m = re.search(r"(k_\w+<[^>]*>|k_\w+)", name)
+            key = m.group(1) if m else name[:90]
             k = (d, int(r["Dispatch_Id"]))
             agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
             dur[key][k] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6

@@ -244,7 +244,7 @@ def test_face_two_sweep_passes_equal_one_sweep_launches(mesh, S, L, solver, ns, 
     for split in splits:
         monkeypatch.setenv("PAMG_FACE_PP", "0")
         rs, rov = run(split)
-        monkeypatch.setenv("PAMG_FACE_PP", "1")
+        monkeypatch.setenv("PAMG_FACE_PP", "3")   # both level sizes that can stream
         gs, gov = run(split)
         assert_identical(gs, rs)
         for x, y in zip(gov, rov):
