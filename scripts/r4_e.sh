@@ -22,3 +22,5 @@ for rep in 1 2; do
   done
 done > $O/corr_ab.log
 cat $O/corr_ab.log
+timeout -k 10 300 python scripts/face_strong_probe.py 5 10 > $O/face_strong.log 2>&1 || { tail -5 $O/face_strong.log; exit 1; }
+grep -v amdgpu.ids $O/face_strong.log
