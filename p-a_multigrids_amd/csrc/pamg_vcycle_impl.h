@@ -1666,8 +1666,10 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
 // Every sweep, residual, mean and interpolation is the per-step kernels' device code on the same
 // values in the same order (pamg_kernels.hip k_smooth, k_residual<.., NEG>, k_restrict_tile,
 // k_interp_add): the state after the call is bitwise the per-step sequence's (tests/test_corrected.py).
+// eight waves per SIMD (64 VGPRs, 9 spilled, four workgroups per CU): 16,536 vs 14,892 V-cycles/s at six
+// (74 VGPRs, three per CU) -- the serialized steps of a tile leave more to hide (profiles/r04_e_corr_ab.txt)
 #ifndef PAMG_CORR_WAVES
-#define PAMG_CORR_WAVES 6
+#define PAMG_CORR_WAVES 8
 #endif
 template <int S, int L>
 struct KGeo {
