@@ -242,14 +242,16 @@ int exchange_local(pamg_handle *h, int l, const double *send, hipStream_t st, in
     return PAMG_OK;
 }
 
-int exchange(pamg_handle *h, int l, int buf, hipStream_t st) {
+// dst: the t_overlap buffer the received words go into (h->tov unless a face call's other snapshot buffer)
+int exchange(pamg_handle *h, int l, int buf, hipStream_t st, double *dst = nullptr) {
     Level &L = h->lv[l];
     const HaloPlan &P = L.halo;
     const double *send = P.send_buf(buf);
+    if (!dst) dst = h->tov;
     Span sp(h, PAMG_K_HALO, 2.0 * 48.0 * (double)(P.remote.size() + P.recv_dst.size()), st);
     if (h->comm->local) {
         CHK(exchange_local(h, l, send, st, 6, P.d_recv));
-        HIPCHK(h, launch_halo_unpack(st, L, h->tov, h->tovo));
+        HIPCHK(h, launch_halo_unpack(st, L, dst, h->tovo));
         return PAMG_OK;
     }
     NCCLCHK(h, ncclGroupStart());
@@ -262,7 +264,7 @@ int exchange(pamg_handle *h, int l, int buf, hipStream_t st) {
                                     h->comm->nccl, st));
     }
     NCCLCHK(h, ncclGroupEnd());
-    HIPCHK(h, launch_halo_unpack(st, L, h->tov, h->tovo));
+    HIPCHK(h, launch_halo_unpack(st, L, dst, h->tovo));
     return PAMG_OK;
 }
 
@@ -326,11 +328,11 @@ int xc_setup(pamg_handle *h, int cycles) {
     return PAMG_OK;
 }
 
-int halo(pamg_handle *h, int l) {
+int halo(pamg_handle *h, int l, double *dst = nullptr) {
     const HaloPlan &P = h->lv[l].halo;
     if (h->comm && !P.peers.empty()) {
         h->lv[l].halo.send_cur = 0;   // the per-step kernels pack into the first buffer
-        return exchange(h, l, 0, h->stream);
+        return exchange(h, l, 0, h->stream, dst);
     }
     return PAMG_OK;
 }
@@ -593,7 +595,9 @@ bool face_tiles_ok(pamg_handle *h, int l) {
 
 // ... and the whole smoother call with the halo words handed from sweep to sweep on the device
 // (face_call): a single domain (a partition exchanges them between sweeps)
-bool face_fusable(pamg_handle *h, int l) { return face_tiles_ok(h, l) && h->nranks == 1 && !h->comm; }
+// (on a partition too: the words a launch writes for the next sweep -- the remote ones into the send buffer
+// -- are exchanged before that sweep, into the snapshot buffer it reads)
+bool face_fusable(pamg_handle *h, int l) { return face_tiles_ok(h, l); }
 
 int face_residual(pamg_handle *h, int l, bool neg);
 
@@ -624,11 +628,13 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
         if (sweeps > 0) {
             if (src_is_T) HIPCHK(h, launch_face_words(h->stream, L, h->U, h->tov, h->tovo));
             else HIPCHK(h, launch_face_halo(h->stream, L, h->tov, h->tovo, true));
+            CHK(halo(h, l));
         }
         return PAMG_OK;
     }
     if (src_is_T) HIPCHK(h, launch_face_words(h->stream, L, h->U, buf[(sweeps - 1) & 1], h->tovo));   // :555
     else HIPCHK(h, launch_face_halo(h->stream, L, buf[(sweeps - 1) & 1], h->tovo, true));   // :550, :555
+    CHK(halo(h, l, buf[(sweeps - 1) & 1]));   // a partition: the remote words into the same snapshot
     // the tagged halo granules of an in-launch call (chain or wavefront): sweep s of this call carries
     // tag wave_tag + s; the base then moves past the call's tags, so no granule is ever accepted twice
     auto tags = [&](unsigned long long **g0, unsigned long long **g1, unsigned *tag0) -> int {
@@ -683,6 +689,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
                                           s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
                                           h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store, s == 0,
                                           s == 0 && src_is_T, r ? L.RES : nullptr));
+        if (s + 1 < sweeps) CHK(halo(h, l, buf[(sweeps - 2 - s) & 1]));   // the next sweep's remote words
     }
     return PAMG_OK;
 }
@@ -991,7 +998,9 @@ bool face_pp_ok(pamg_handle *h, int l) {
     const int mask = ev ? atoi(ev) : 1;
     const Level &L = h->lv[l];
     const int bit = L.nsub == 1024 ? 1 : L.nsub == 256 ? 2 : 0;
-    return (mask & bit) && face_fusable(h, l) && face_tile_shape(L) && L.gtab && (h->p.solver != 3 || L.words_up);
+    // a single domain: the passes read the neighbours' iterate itself
+    return (mask & bit) && face_fusable(h, l) && h->nranks == 1 && !h->comm && face_tile_shape(L) && L.gtab &&
+           (h->p.solver != 3 || L.words_up);
 }
 
 struct PPPass { int K, res; double *in, *pre, *mid, *end; };

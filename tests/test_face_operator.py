@@ -135,10 +135,14 @@ def test_face_chain_8byte_snapshot_is_bitwise_the_oracle(solver, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mesh,S,L,parts,kind,solver,cycle", [
     ("untitled8192.msh", 3, 3, 4, "strip", 3, 0), ("untitled8192.msh", 3, 2, 8, "strip", 3, 1),
-    ("irregular.msh", 4, 2, 8, "strip", 1, 1), ("900_ele.msh", 2, 2, 3, "block", 3, 0)])
+    ("irregular.msh", 4, 2, 8, "strip", 1, 1), ("900_ele.msh", 2, 2, 3, "block", 3, 0),
+    # bench.py's op=1 mesh on 4 x-strips: levels of 1,024 / 256 / 64 sub-elements per un_ele as one tile
+    # launch per sweep, each launch's next-sweep words exchanged into the snapshot buffer that sweep reads
+    ("untitled8192.msh", 5, 3, 4, "strip", 3, 0), ("untitled8192.msh", 4, 3, 8, "block", 1, 0)])
 def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, solver, cycle):
     """The halo is consumed every sweep: the partitions' exchanges (the multi-rank path with the
-    device-copy transport, tests/test_multirank.py) carry the values the sweeps read."""
+    device-copy transport, tests/test_multirank.py) carry the values the sweeps read -- after every
+    launch that writes a sweep's words, into the snapshot buffer the next sweep reads."""
     import pamg
     from pamg.solver import local_group, run_ranks
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
