@@ -160,14 +160,32 @@ def cpu_baseline():
                 seconds_1cycle=t1, seconds_2cycles=t2, host_cpu=host_cpu())
 
 
-def pmc_traffic(kernel, nsplit, levels):
+def source_digest():
+    """sha256 over the kernel sources (p-a_multigrids_amd/csrc, include/pamg.h): a committed PMC
+    summary applies to the build it was measured on only (scripts/pmc_summary.py records it)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "p-a_multigrids_amd", "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")))
+    for f in files + ["../../include/pamg.h"]:
+        h.update(f.encode())
+        h.update(open(os.path.join(csrc, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel, nsplit, levels, info=None):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3
-    PMC summary (profiles/pmc_<kernel>.json), if one exists for this config."""
+    PMC summary (profiles/pmc_<kernel>.json), if one exists for this config and was
+    measured on these kernel sources (else None: a stale file is not reported)."""
     p = os.path.join(ROOT, "profiles", f"pmc_{kernel.lower()}.json")
     try:
         d = json.load(open(p))
         if int(d.get("n_split", -1)) == nsplit and int(d.get("levels", levels)) == levels:
-            return d.get("hbm_bytes_per_launch")
+            match = d.get("source_digest") == source_digest()
+            if info is not None:
+                info.update({"file": os.path.relpath(p, ROOT), "commit": d.get("commit"),
+                             "source_digest": d.get("source_digest"), "source_matches_build": match})
+            return d.get("hbm_bytes_per_launch") if match else None
     except Exception:
         pass
     return None
@@ -444,7 +462,8 @@ def main():
     ms_per_launch = kinfo["ms"] / max(1, kinfo["launches"])
     bytes_per_launch = kinfo["bytes"] / max(1, kinfo["launches"])
     achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
-    traffic = pmc_traffic(rk, a.nsplit, a.levels) if world == 1 else None
+    traffic_src = {}
+    traffic = pmc_traffic(rk, a.nsplit, a.levels, traffic_src) if world == 1 else None
     cycles_per_launch = (a.steps if live_events else post) if rk == "vcycle_res" else 1
     flops_per_launch = s.vcycle_flops() * cycles_per_launch
     tflops = flops_per_launch / (ms_per_launch * 1e-3) / 1e12 if ms_per_launch > 0 else 0.0
@@ -629,6 +648,7 @@ def main():
                                      else f"post-pass of one call of {post} cycles"),
                           "achieved": round(tflops, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(tflops / FP64_PEAK_TFLOPS, 4), "traffic": traffic,
+                          "traffic_source": traffic_src or None,
                           "fp64_flops_per_launch": flops_per_launch, "cycles_per_launch": cycles_per_launch,
                           "alg_bytes_per_launch": bytes_per_launch, "hbm_gbs": round(achieved, 1),
                           "ms_per_launch": round(ms_per_launch, 4)}

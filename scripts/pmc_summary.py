@@ -4,14 +4,29 @@
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE (KiB) reports
 half the bytes of wide coalesced streaming reads -> x2; WRITE_SIZE (KiB) is exact
 for 16-B-per-lane streaming stores. Usage:
-  pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON N_SPLIT [alg_bytes_per_launch] [kernel_prefix]
+  pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON N_SPLIT [alg_bytes_per_launch] [kernel_prefix] [levels] [commit]
 kernel_prefix selects the roofline kernel (default "k_vc_fine", the fused V-cycle's
 level-1 launch; "void k_smooth<false, true>" for the per-step level-1 smoother)."""
 import collections
 import csv
 import glob
+import hashlib
 import json
+import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def source_digest():
+    """the kernel sources the counters were measured on (bench.py source_digest: the same hash)"""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "p-a_multigrids_amd", "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")))
+    for f in files + ["../../include/pamg.h"]:
+        h.update(f.encode())
+        h.update(open(os.path.join(csrc, f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def per_kernel(d, counter):
@@ -41,6 +56,7 @@ def main():
     smooth = [r for r in rows if r["kernel"].replace("void ", "").startswith(prefix.replace("void ", ""))]
     smooth.sort(key=lambda r: -r["grid"])
     res = {"n_split": nsplit, "levels": int(sys.argv[7]) if len(sys.argv) > 7 else 3, "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1, KiB->B",
+           "commit": sys.argv[8] if len(sys.argv) > 8 else None, "source_digest": source_digest(),
            "kernels": rows}
     if smooth:
         res["hbm_bytes_per_launch"] = smooth[0]["hbm_bytes"]
