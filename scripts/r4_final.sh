@@ -31,5 +31,8 @@ if [ "$2" = "B" ]; then
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_sweep_write -o run -- python3 $R/scripts/sweep_prof.py 3 > $O/pmc_sweep_write.log 2>&1 || exit 1
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_face -o run -- python3 $R/scripts/face_probe.py 5 0 > $O/prof_face.log 2>&1
   echo "face rocprof exit $?"
+  cd $R
+  timeout -k 10 400 python scripts/strong_probe.py > $O/strong_driver.txt 2>&1 || exit 1
+  cat $O/strong_driver.txt
 fi
 echo "all ok"
