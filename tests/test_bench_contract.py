@@ -35,3 +35,33 @@ def test_bench_prints_the_contract_line():
     else:
         assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert 0 < rf["frac"] < 1.0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+
+
+def test_pmc_traffic_is_reported_only_for_the_build_it_was_measured_on(tmp_path, monkeypatch):
+    """bench.py reads roofline.traffic from the committed rocprofv3 PMC summary only when the
+    summary's kernel-source digest (scripts/pmc_summary.py) matches the current sources"""
+    sys.path.insert(0, ROOT)
+    import bench
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pmc_summary", os.path.join(ROOT, "scripts", "pmc_summary.py"))
+    ps = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ps)
+    assert ps.source_digest() == bench.source_digest()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    # the digest itself is computed over the real tree
+    monkeypatch.setattr(bench, "source_digest", lambda: ps.source_digest())
+    rec = {"n_split": 5, "levels": 3, "hbm_bytes_per_launch": 1.0e9, "commit": "abc1234",
+           "source_digest": ps.source_digest()}
+    (prof / "pmc_vcycle_res.json").write_text(json.dumps(rec))
+    info = {}
+    assert bench.pmc_traffic("vcycle_res", 5, 3, info) == 1.0e9
+    assert info["source_matches_build"] is True and info["commit"] == "abc1234"
+    assert bench.pmc_traffic("vcycle_res", 6, 3) is None   # another configuration
+    rec["source_digest"] = "0" * 16                          # measured on other kernels: stale
+    (prof / "pmc_vcycle_res.json").write_text(json.dumps(rec))
+    info = {}
+    assert bench.pmc_traffic("vcycle_res", 5, 3, info) is None
+    assert info["source_matches_build"] is False
+    assert bench.pmc_traffic("vcycle_pipe", 5, 3) is None    # no summary at all
