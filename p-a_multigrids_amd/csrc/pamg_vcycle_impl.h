@@ -95,12 +95,6 @@ struct VArgs {
     unsigned *xc_done;
     unsigned long long *xc_sig;
     unsigned xc_grid;
-    // the resident launch (k_vc_resb) with more tiles than resident workgroups: at cycle pf_cycle a
-    // tile's level-1 waves read tile + pf_tiles's state (the tile that takes over this workgroup
-    // slot, on the same XCD) through to L2 / the Infinity Cache, so that the next round's loads
-    // hit there instead of all going to HBM at the same moment; 0: off
-    int64_t pf_tiles;
-    int pf_cycle;
 };
 
 }  // namespace vc
@@ -1301,40 +1295,6 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
 #define PAMG_RESB_WAVES 6
 #endif
 
-// the cache warm-up of the next round's tile bn (VArgs::pf_tiles): its state planes as 16-byte
-// loads straight into a 1 KB LDS sink (global_load_lds_dwordx4: no registers, the data is never
-// read) by the 384 level-1 threads; they drain at the cycle's barrier
-template <int S, int L, bool RHSF>
-__device__ __forceinline__ void prefetch_tile(const VArgs &A, int64_t bn, int ti, double *sink) {
-    using G = Geo<S, L>;
-    if (bn >= A.tile0 + (int64_t)gridDim.x) return;
-    // the addresses are formed here, from values the compiler cannot see through (hoisted out of
-    // the cycle loop they held registers across it and spilled)
-    __asm__ volatile("" : "+s"(bn));
-    __asm__ volatile("" : "+v"(ti));
-    auto lds = (__attribute__((address_space(3))) void *)sink;
-    // per plane: a uniform base and 16-byte units ti, ti + 384 < nt(l) / 2 (32-bit offsets)
-    auto planes = [&](const double *f, int64_t pitch, int l) {
-        const int units = G::nt(l) / 2;
-        const uint32_t o = (uint32_t)ti << 4;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const char *b = reinterpret_cast<const char *>(f + c * pitch + bn * G::nt(l));
-            if (ti < units) __builtin_amdgcn_global_load_lds(b + o, lds, 16, 0, 0);
-            if (units > 384 && ti + 384 < units) __builtin_amdgcn_global_load_lds(b + o + 384 * 16, lds, 16, 0, 0);
-        }
-    };
-    planes(A.lv[0].T(), A.lv[0].pitch, 0);
-    planes(RHSF ? A.lv[0].SRC() : A.lv[0].RHS(), A.lv[0].pitch, 0);
-    planes(A.lv[1].T(), A.lv[1].pitch, 1);
-    planes(A.rhsn2, A.lv[1].pitch, 1);
-    static_for<2, G::C + 1>([&](auto lc) {
-        constexpr int l = decltype(lc)::value;
-        planes(A.lv[l].T(), A.lv[l].pitch, l);
-        planes(A.lv[l].RHSN(), A.lv[l].pitch, l);
-    });
-}
-
 template <int S, int L, class ST, bool RHSF, bool XC = false>
 __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) void k_vc_resb(VArgs A, const double *__restrict__ sp0,
                                                                 const double *__restrict__ sp1,
@@ -1349,7 +1309,6 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     // two parity buffers of residual means; RHSF: the tile's source s' (3 T doubles) behind them
     // -- every step's RHS reads it; in registers it pushed the launch past 128 VGPRs
     __shared__ __attribute__((aligned(16))) double MB[B::LDS(RHSF)];
-    __shared__ __attribute__((aligned(16))) double PF[128];   // prefetch_tile's sink
     double *const SQ = MB + 2 * B::MS;
     auto means = [&](int c, int l) { return MB + (c & 1) * B::MS + B::MO(l); };
     const int t = threadIdx.x;
@@ -1604,8 +1563,6 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
             if constexpr (N == 2) l2_load(std::integral_constant<int, 1>{}, gb, xs, bs, gc, vc);
             auto cycle = [&](int c, auto lastc) {
                 constexpr bool last = decltype(lastc)::value;
-                if (!XC && A.pf_tiles && c == A.pf_cycle)
-                    prefetch_tile<S, L, RHSF>(A, tb + A.pf_tiles, (wv == 5 ? 3 : wv >= 6 ? wv - 2 : wv - 1) * 64 + lane_id(), PF);
                 ST St0;
                 stencil(true, sp0, opaque(w0), St0);
                 // restriction-leg call (:331) from tnew (tnew_nonlin := tnew, :327): its tnew, in place
@@ -1928,27 +1885,6 @@ __global__ __launch_bounds__(512, PAMG_CORR_WAVES) void k_vc_corr(VArgs A, const
 }
 
 // part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
-// VArgs::pf_tiles / pf_cycle of a resident launch: the workgroups resident at once (the next round
-// starts tile + that many in the freed slot, on the same XCD); the warm-up at cycle
-// total * PAMG_RES_PF / 8 (default 4: mid-call; 0 off), only when the launch has a second round
-inline void res_prefetch(VArgs &A, const void *kf, unsigned grid) {
-    static const int at = getenv("PAMG_RES_PF") ? atoi(getenv("PAMG_RES_PF")) : 4;
-    static int dev_cu = -1;
-    if (dev_cu < 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n = 0;
-        dev_cu = n;
-    }
-    int per_cu = 0;
-    if (at <= 0 || dev_cu <= 0 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 512, 0) != hipSuccess || per_cu <= 0)
-        return;
-    const int64_t resident = (int64_t)per_cu * dev_cu, total = (int64_t)A.steps * A.cycles;
-    if ((int64_t)grid <= resident || total < 2) return;
-    A.pf_tiles = resident;
-    A.pf_cycle = (int)std::min<int64_t>(total - 1, total * std::min(at, 8) / 8);
-}
-
 template <int S, int L, class ST, bool W8>
 hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     if constexpr (std::is_same<ST, StcR>::value) {   // Richardson: the resident call only (k_vc_res)
@@ -1993,19 +1929,14 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
             return hipErrorInvalidValue;
     } else if (part >= 4 && part <= 6) {   // the resident call (5: starting a time step; 6: exchange every cycle)
         if constexpr (PAMG_RES_BALANCED && S >= 5 && L >= 3) {
-            const void *kf = part == 6 ? (const void *)k_vc_resb<S, L, ST, false, true>
-                             : part == 5 ? (const void *)k_vc_resb<S, L, ST, true>
-                                         : (const void *)k_vc_resb<S, L, ST, false>;
-            VArgs B = A;
-            res_prefetch(B, kf, grid);
             if (part == 6)
-                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false, true>), dim3(grid), dim3(512), 0, s, B,
+                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false, true>), dim3(grid), dim3(512), 0, s, A,
                                    A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
             else if (part == 5)
-                hipLaunchKernelGGL((k_vc_resb<S, L, ST, true>), dim3(grid), dim3(512), 0, s, B, A.lv[0].stc,
+                hipLaunchKernelGGL((k_vc_resb<S, L, ST, true>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
                                    A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
             else
-                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false>), dim3(grid), dim3(512), 0, s, B,
+                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false>), dim3(grid), dim3(512), 0, s, A,
                                    A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
         } else if constexpr (L >= 2 && fine_np(S) == 2) {
             if (part == 6)
