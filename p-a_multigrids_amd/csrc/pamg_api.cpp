@@ -991,11 +991,12 @@ bool face_cycle_fusable(pamg_handle *h) {
 // leaves (every coarser level writes a subset of its slots). Bitwise the per-step sequence
 // (tests/test_face_operator.py). PAMG_FACE_PP=0 keeps the one-sweep launches (A/B).
 // PAMG_FACE_PP: a mask of the level sizes that stream -- bit 0 levels of 1,024 sub-elements per un_ele,
-// bit 1 of 256; 0 none. Default 1: the 256-element launches (two waves a workgroup) measured slower as
-// two-sweep passes than as one-sweep launches (profiles/r04_d_face_pp.txt)
+// bit 1 of 256; 0 none. Default 3: both (the 256-element passes were slower while their instance
+// spilled at six waves per SIMD, profiles/r04_d_face_pp.txt; at four, 620 vs 601-603 V-cycles/s with
+// level 1 alone, profiles/r04_i_face_pp_level2.txt)
 bool face_pp_ok(pamg_handle *h, int l) {
     const char *ev = getenv("PAMG_FACE_PP");   // read per call: tests switch it within a process
-    const int mask = ev ? atoi(ev) : 1;
+    const int mask = ev ? atoi(ev) : 3;
     const Level &L = h->lv[l];
     const int bit = L.nsub == 1024 ? 1 : L.nsub == 256 ? 2 : 0;
     // a single domain: the passes read the neighbours' iterate itself

@@ -597,11 +597,16 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_WAVES
 #define PAMG_FACE_PP_WAVES 6
 #endif
+// the 256-sub-element instance (level 2 at n_split 5): at six waves per SIMD its two-sweep form spilled
+// 84 B per lane; four keep it in 104 VGPRs
+#ifndef PAMG_FACE_PP_WAVES256
+#define PAMG_FACE_PP_WAVES256 4
+#endif
 #ifndef PAMG_FACE_PP_BLDS
 #define PAMG_FACE_PP_BLDS 1
 #endif
 template <int TS, int NT, bool RB, int K>
-__global__ __launch_bounds__(NT, RB ? PAMG_FACE_PP_WAVES : 1) void k_face_pp(
+__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
     const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
