@@ -461,8 +461,9 @@ int face_chain_setup(pamg_handle *h, int l) {
     if (list.empty()) list.push_back(0);
     CHK(dev_upload(h, &L.chain_nb_off, off));
     CHK(dev_upload(h, &L.chain_nb_list, list));
-    // the polled words in one block of their own, a multiple of 16 bytes from the allocation's start
-    L.chain_flag_bytes = ((size_t)G * sizeof(unsigned) + 15) / 16 * 16;
+    // the polled words in one block of their own, a multiple of 16 bytes from the allocation's start: one
+    // per workgroup (k_face_chain) or per wave of it (k_face_chain_pw, 16 a workgroup)
+    L.chain_flag_bytes = ((size_t)G * 16 * sizeof(unsigned) + 15) / 16 * 16;
     CHK(dev_alloc(h, &L.chain_flags, L.chain_flag_bytes / sizeof(unsigned)));
     HIPCHK(h, hipMemsetAsync(L.chain_flags, 0, L.chain_flag_bytes, h->stream));
     L.chain_epoch = 0;

@@ -1463,6 +1463,196 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
     }
 }
 
+// ---- the chain with un_eles owned by waves (PAMG_CHAIN_PW, default where it applies): the red-black
+// sweep of an un_ele reads, besides the halo snapshot, only its own sub-elements -- an up one its down
+// neighbours, a down one its up neighbours -- so each wave of the workgroup takes q = k / 16 whole un_eles
+// and runs their passes without the workgroup: item 0 (the ups without halo words), the wait for the
+// words of the previous sweep, the snapshot of its own un_eles, item 1 (the ups with words, whose words
+// for the next sweep it writes at once), the drain, its own flag, the down pass. A wave's LDS writes are
+// read only by that wave (its un_eles' slots of X and HI), in order; the records are loaded behind the
+// one barrier of the launch. Flags are per wave (flags[16 w + v]); a wave waits for the 16 waves of its
+// own workgroup and of every neighbouring workgroup (a superset of the waves owning its un_eles'
+// neighbours). The buffer argument is the workgroup chain's: a wave writes snapshot buffer (s + 1) & 1
+// only after every wave that reads its words there has published sweep s - 1, i.e. loaded the snapshot
+// of sweep s - 1 from it. Same items, same face_apply on the same operands in the same colour order:
+// bitwise k_face_chain (tests/test_face_operator.py). Needs every halo sub-element to be an up one
+// (words_up) and q un_eles' colour lists in 64 lanes (level 3 at n_split = 5: 2 x 15, 2 x 21, 2 x 28).
+constexpr int kPW = kChainNT / 64;   // waves of a chain workgroup
+__global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double *TNN, const double *SRC,
+                                                               const double *__restrict__ RHS,
+                                                               const double *__restrict__ stc, const int4 *__restrict__ fnb,
+                                                               const double *__restrict__ fface, const int *__restrict__ fsx,
+                                                               double *buf0, double *buf1, HaloArgs H, unsigned *flags,
+                                                               const int *__restrict__ nb_off, const int *__restrict__ nb_list,
+                                                               unsigned *tmo, int run, int total, int store, int E,
+                                                               int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
+                                                               double rdt, double omega, const int *__restrict__ cpos,
+                                                               int nup, int nui, int early, unsigned f0, int snap_ok,
+                                                               long long *stamps) {
+    (void)omega;
+    (void)early;
+    (void)stamps;
+    constexpr int NT = kChainNT;
+    __shared__ double X[3][NT * kChainPer];
+    __shared__ double HI[kChainHalo];
+    __shared__ double RS[kChainRec * kRecW];
+    const int t = threadIdx.x, w = blockIdx.x;
+    const int v = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+    const int64_t s0 = (int64_t)w * E;
+    const int64_t nsm = (1ll << nsub_log2) - 1;
+    const int m = H.m, ke = E >> nsub_log2;
+    const int64_t u0 = s0 >> nsub_log2;
+    const int kv = (int)std::min<int64_t>(ke, (N >> nsub_log2) - u0);
+    const int q = (ke + kPW - 1) / kPW;                  // un_eles per wave
+    const int ua = std::min(kv, v * q), ub = std::min(kv, ua + q);   // this wave's un_eles [ua, ub)
+    const int nsub = 1 << nsub_log2, ndn = nsub - nup, n1 = nup - nui;
+    for (int i = t; i < kv * kRecW; i += NT) {   // the un_eles' records (as k_face_chain's LREC)
+        const int uk = i / kRecW, c = i - uk * kRecW;
+        const int64_t u = u0 + uk;
+        double val = 0.0;
+        if (c == 0) val = stc[u * kStcStride + kStcC];
+        else if (c < 10) val = stc[u * kStcStride + kStcK + c - 1];
+        else if (c < 13) val = stc[u * kStcStride + kStcW + c - 10];
+        else if (c < 19) val = fface[u * kFaceStride + c - 13];
+        else if (c < 43) val = fface[u * kFaceStride + kFaceWD + c - 19];
+        else if (c < 46) val = (double)fsx[4 * u + fmface(c - 43) - 1];
+        RS[i] = val;
+    }
+    // the lane's items: 0 an up sub-element without halo words, 1 one with words, D a down one
+    Items<1> I0, I1, ID;
+    auto mk = [&](Items<1> &I, int n, int o) {
+        const int uk = n > 0 ? ua + ln / n : ub;
+        I.j[0] = (n > 0 && ln < q * n && uk < ub) ? (uk << nsub_log2) + cpos[o + ln % n] : -1;
+        const int j = I.j[0] < 0 ? 0 : I.j[0];
+        I.nb[0] = fnb[j & nsm];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) I.b[0][c] = RHS[c * pitch + s0 + j];
+    };
+    mk(I0, nui, 0);
+    mk(I1, n1, nui);
+    mk(ID, ndn, nup);
+    // item 1's halo positions (packed 10 bits per face) and its un_ele's face records
+    int hq = 0;
+    int4 hr[3] = {};
+    if (I1.j[0] >= 0) {
+        const int4 e = H.hsub[I1.j[0] & nsm];
+        hq = e.x | (e.y << 10) | (e.z << 20);
+        const int64_t u = u0 + (I1.j[0] >> nsub_log2);
+#pragma unroll
+        for (int f = 0; f < 3; ++f) hr[f] = H.hface[3 * u + f];
+    }
+    const int pa = ua << nsub_log2, pb = ub << nsub_log2;   // the wave's tile positions
+    for (int j = pa + ln; j < pb; j += 64)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) X[c][j] = SRC[c * pitch + s0 + j];
+    __syncthreads();   // the records
+    auto ixin = [&](int c, int qq) { return X[c][qq]; };
+    auto ihv = [&](int64_t uu, int mf, int sp, int kk) { return HI[(((int)(uu - u0) * 3 + mf - 1) * m + sp - 1) * 3 + kk]; };
+    auto nohv = [](int64_t, int, int, int) { return 0.0; };
+    auto irec = [&](int j, int4 nb, auto &&f) {
+        const int uk = j >> nsub_log2;
+        const double *rs = RS + uk * kRecW;
+        FaceRec R;
+        R.S.c = rs[0];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) R.S.K[c] = rs[1 + c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) R.S.w[c] = rs[10 + c];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) R.w[c] = rs[13 + c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) R.sx[c] = (int)rs[43 + c];
+        f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
+    };
+    auto tstore = [&]() {
+        for (int j = pa + ln; j < pb; j += 64)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = X[c][j];
+    };
+    if (store == 1 && run == 1) tstore();
+    const int64_t tin_bytes64 = (N >> nsub_log2) * slots * 3 * 8;
+    const bool snap16 = snap_ok && ((3 * m) & 1) == 0 && (slots & 1) == 0 && tin_bytes64 < (1ll << 31);
+    const int tin_bytes = (int)std::min<int64_t>(tin_bytes64, (1ll << 31) - 1);
+    const int na = nb_off[w], nn = nb_off[w + 1] - na;
+    const int ha = ua * 9 * m, hb = ub * 9 * m;   // the wave's slots of the snapshot image
+    for (int sw = 0; sw < run; ++sw) {
+        const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
+        double *tout = sw + 1 < total ? (((total - 2 - sw) & 1) ? buf1 : buf0) : nullptr;
+        // opaque per sweep (as k_face_chain's): the items stay in their registers instead of being
+        // rematerialized or hoisted around the passes
+        asm volatile("" : "+v"(I0.j[0]), "+v"(I0.nb[0].x), "+v"(I0.nb[0].y), "+v"(I0.nb[0].z), "+v"(I0.nb[0].w));
+        asm volatile("" : "+v"(I1.j[0]), "+v"(I1.nb[0].x), "+v"(I1.nb[0].y), "+v"(I1.nb[0].z), "+v"(I1.nb[0].w));
+        asm volatile("" : "+v"(ID.j[0]), "+v"(ID.nb[0].x), "+v"(ID.nb[0].y), "+v"(ID.nb[0].z), "+v"(ID.nb[0].w));
+        asm volatile("" : "+v"(hq));
+#pragma unroll
+        for (int f = 0; f < 3; ++f) asm volatile("" : "+v"(hr[f].x), "+v"(hr[f].y), "+v"(hr[f].z));
+        items_pass<0>(I0, ixin, nohv, irec, level1, rdt, [&](int, const double r[3]) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) X[c][I0.j[0]] = r[c];
+        });
+        if (sw > 0) {   // every wave of this and of the neighbouring workgroups has published sweep sw - 1
+            const int tot = (nn + 1) * kPW;
+            for (int base = 0; base < tot; base += 64) {
+                const int i = base + ln;
+                const unsigned *f = nullptr;
+                if (i < tot) {
+                    const int g = i / kPW;
+                    f = flags + (size_t)(g == 0 ? w : nb_list[na + g - 1]) * kPW + (i - g * kPW);
+                }
+                bool ok = f == nullptr;
+                for (unsigned spins = 0;; ++spins) {
+                    if (!ok) ok = __hip_atomic_load((g_u32 *)const_cast<unsigned *>(f), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) >= f0 + (unsigned)sw;
+                    if (__all(ok)) break;
+                    if (spins > (1u << 22)) {
+                        if (ln == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+        }
+        // the snapshot of the wave's un_eles (sc1: through to the coherent level)
+        if (snap16) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(tin), (short)0, tin_bytes, 0x00020000);
+            for (int idx = ha + 2 * ln; idx < hb; idx += 128) {
+                const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
+                const int o = (int)(((u0 + uk) * slots * 3 + (int64_t)mf * slots + off) * 8);
+                const v4u val = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kAuxSc1);
+                HI[idx] = __longlong_as_double(((long long)val.y << 32) | val.x);
+                HI[idx + 1] = __longlong_as_double(((long long)val.w << 32) | val.z);
+            }
+        } else {
+            for (int idx = ha + ln; idx < hb; idx += 64) {
+                const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
+                HI[idx] = ld_coh(tin + (u0 + uk) * slots * 3 + (int64_t)mf * slots + off);
+            }
+        }
+        // the ups with words, their next-sweep words written through at once
+        HaloArgs Hn = H;
+        Hn.tov = tout;
+        items_pass<0>(I1, ixin, ihv, irec, level1, rdt, [&](int, const double r[3]) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) X[c][I1.j[0]] = r[c];
+            if (tout) halo_words<true>(Hn, hr, hq, r, sw == 0);
+        });
+        if (tout) {   // drained, then this wave's flag
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (ln == 0)
+                __hip_atomic_store((g_u32 *)flags + (size_t)w * kPW + v, f0 + (unsigned)(sw + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        items_pass<1>(ID, ixin, ihv, irec, level1, rdt, [&](int, const double r[3]) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) X[c][ID.j[0]] = r[c];
+        });
+        if (store == 1 && sw + 2 == run) tstore();   // the last sweep's tnew := tnew_nonlin (its start)
+    }
+    for (int j = pa + ln; j < pb; j += 64)   // tnew_nonlin (store 2: tnew, the dead last sweep's :550)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+}
+
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 inline int log2i(int v) { int r = 0; while ((1 << r) < v) ++r; return r; }
 
@@ -1687,6 +1877,14 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     const void *f = uni ? (rb ? PAMG_CHF(true, true) : PAMG_CHF(true, false))
                         : (rb ? PAMG_CHF(false, true) : PAMG_CHF(false, false));
 #undef PAMG_CHF
+    // the per-wave form (k_face_chain_pw): red-black with the split up pass, whole un_eles per wave whose
+    // colour lists fit 64 lanes, per-wave flags (face_chain_setup sizes them); PAMG_CHAIN_PW=0 keeps the
+    // workgroup form (read per launch: a test switches it within a process)
+    const char *pw_env = getenv("PAMG_CHAIN_PW");
+    const int qpw = (k + kPW - 1) / kPW;
+    if (!(pw_env && atoi(pw_env) == 0) && rb && lrec && early == 3 && !stamp_path && uni && L.nsub <= 64 &&
+        qpw * std::max(nui, std::max(L.nup - nui, L.ndn)) <= 64)
+        f = (const void *)k_face_chain_pw;
     hipError_t e = launch_coresident(f, grid, kChainNT, args, s);
     if (stamp_path) {
         std::vector<long long> h(nst);

@@ -253,3 +253,35 @@ def test_face_two_sweep_passes_equal_one_sweep_launches(mesh, S, L, solver, ns, 
         assert_identical(gs, rs)
         for x, y in zip(gov, rov):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,ns,splits", [
+    ("untitled8192.msh", 5, 3, 4, ([3], [1, 2])), ("untitled8192.msh", 5, 3, 2, ([2],)),
+    ("900_ele.msh", 5, 3, 3, ([2, 1],)), ("irregular.msh", 5, 3, 4, ([2],))])
+def test_face_chain_per_wave_equals_workgroup_chain(mesh, S, L, ns, splits, monkeypatch):
+    """The coarsest level's persistent chain with its un_eles owned by waves (k_face_chain_pw: no
+    workgroup barrier inside a sweep, per-wave flags) leaves the state of the workgroup chain
+    (k_face_chain), bit for bit -- bench.py's op = 1 configuration (level 3: 64 sub-elements per un_ele,
+    two un_eles a wave, 256 workgroups), an odd smoother length, small meshes whose last workgroup and
+    waves are partly empty, calls split over time steps."""
+    import pamg
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+
+    def run(split):
+        g = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=3, op=1)
+        for n in split:
+            g.begin_timestep()
+            g.vcycle(n)
+        st, ov = g.state(), g.overlap()
+        g.close()
+        return st, ov
+
+    for split in splits:
+        monkeypatch.setenv("PAMG_CHAIN_PW", "0")
+        rs, rov = run(split)
+        monkeypatch.setenv("PAMG_CHAIN_PW", "1")
+        gs, gov = run(split)
+        assert_identical(gs, rs)
+        for x, y in zip(gov, rov):
+            np.testing.assert_array_equal(x, y)
