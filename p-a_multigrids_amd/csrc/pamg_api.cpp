@@ -461,29 +461,6 @@ int face_chain_setup(pamg_handle *h, int l) {
     if (list.empty()) list.push_back(0);
     CHK(dev_upload(h, &L.chain_nb_off, off));
     CHK(dev_upload(h, &L.chain_nb_list, list));
-    // per wave (k_face_chain_pw: wave v of workgroup w owns un_eles w k + [v q, (v + 1) q), q = k / 16
-    // rounded up): the flag words (16 x workgroup + wave) of the other waves owning its un_eles' neighbours
-    const int q = (k + 15) / 16;
-    std::vector<int> poff(1, 0), plist;
-    for (int w = 0; w < G; ++w)
-        for (int v = 0; v < 16; ++v) {
-            std::vector<int> nb;
-            const int a = w * k + std::min(k, v * q), b = std::min(U, w * k + std::min(k, (v + 1) * q));
-            for (int u = a; u < b; ++u)
-                for (int f = 0; f < 3; ++f) {
-                    const int n = h->neig_local[3 * (size_t)u + f];
-                    if (n < 0) continue;
-                    const int fw = (n / k) * 16 + (n % k) / q;
-                    if (fw != w * 16 + v) nb.push_back(fw);
-                }
-            std::sort(nb.begin(), nb.end());
-            nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
-            plist.insert(plist.end(), nb.begin(), nb.end());
-            poff.push_back((int)plist.size());
-        }
-    if (plist.empty()) plist.push_back(0);
-    CHK(dev_upload(h, &L.chain_pw_off, poff));
-    CHK(dev_upload(h, &L.chain_pw_list, plist));
     // the polled words in one block of their own, a multiple of 16 bytes from the allocation's start: one
     // per workgroup (k_face_chain) or per wave of it (k_face_chain_pw, 16 a workgroup)
     L.chain_flag_bytes = ((size_t)G * 16 * sizeof(unsigned) + 15) / 16 * 16;
@@ -1565,7 +1542,6 @@ void free_levels(pamg_handle *h) {
         dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.d_pos); dev_free(L.blocks);
         dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx); dev_free(L.cpos); dev_free(L.gtab);
         dev_free(L.chain_nb_off); dev_free(L.chain_nb_list); dev_free(L.chain_flags);
-        dev_free(L.chain_pw_off); dev_free(L.chain_pw_list);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
         dev_free(L.halo.d_ring); dev_free(L.halo.d_recv3);

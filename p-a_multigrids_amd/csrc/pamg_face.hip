@@ -1470,11 +1470,11 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 // words of the previous sweep, the snapshot of its own un_eles, item 1 (the ups with words, whose words
 // for the next sweep it writes at once), the drain, its own flag, the down pass. A wave's LDS writes are
 // read only by that wave (its un_eles' slots of X and HI), in order; the records are loaded behind the
-// one barrier of the launch. Flags are per wave (flags[16 w + v]); a wave waits only for the waves owning
-// its un_eles' neighbours (Level::chain_pw_off / _list; its own words it drained itself). The buffer
-// argument is the workgroup chain's: a wave writes snapshot buffer (s + 1) & 1 only after every wave that
-// reads its words there -- the owners of its un_eles' neighbours, the waves it waits for -- has published
-// sweep s - 1, i.e. loaded the snapshot of sweep s - 1 from it. Same items, same face_apply on the same operands in the same colour order:
+// one barrier of the launch. Flags are per wave (flags[16 w + v]); a wave waits for the 16 waves of its
+// own workgroup and of every neighbouring workgroup (a superset of the waves owning its un_eles'
+// neighbours). The buffer argument is the workgroup chain's: a wave writes snapshot buffer (s + 1) & 1
+// only after every wave that reads its words there has published sweep s - 1, i.e. loaded the snapshot
+// of sweep s - 1 from it. Same items, same face_apply on the same operands in the same colour order:
 // bitwise k_face_chain (tests/test_face_operator.py). Needs every halo sub-element to be an up one
 // (words_up) and q un_eles' colour lists in 64 lanes (level 3 at n_split = 5: 2 x 15, 2 x 21, 2 x 28).
 constexpr int kPW = kChainNT / 64;   // waves of a chain workgroup
@@ -1573,9 +1573,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
     const int64_t tin_bytes64 = (N >> nsub_log2) * slots * 3 * 8;
     const bool snap16 = snap_ok && ((3 * m) & 1) == 0 && (slots & 1) == 0 && tin_bytes64 < (1ll << 31);
     const int tin_bytes = (int)std::min<int64_t>(tin_bytes64, (1ll << 31) - 1);
-    // nb_off / nb_list: the per-wave lists (Level::chain_pw_off / _list): flag words of the other waves
-    // owning this wave's un_eles' neighbours
-    const int na = nb_off[w * kPW + v], nn = nb_off[w * kPW + v + 1] - na;
+    const int na = nb_off[w], nn = nb_off[w + 1] - na;
     const int ha = ua * 9 * m, hb = ub * 9 * m;   // the wave's slots of the snapshot image
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
@@ -1592,10 +1590,15 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
 #pragma unroll
             for (int c = 0; c < 3; ++c) X[c][I0.j[0]] = r[c];
         });
-        if (sw > 0) {   // every wave owning a neighbour of this wave's un_eles has published sweep sw - 1
-            for (int base = 0; base < nn; base += 64) {
+        if (sw > 0) {   // every wave of this and of the neighbouring workgroups has published sweep sw - 1
+            const int tot = (nn + 1) * kPW;
+            for (int base = 0; base < tot; base += 64) {
                 const int i = base + ln;
-                const unsigned *f = i < nn ? flags + nb_list[na + i] : nullptr;
+                const unsigned *f = nullptr;
+                if (i < tot) {
+                    const int g = i / kPW;
+                    f = flags + (size_t)(g == 0 ? w : nb_list[na + g - 1]) * kPW + (i - g * kPW);
+                }
                 bool ok = f == nullptr;
                 for (unsigned spins = 0;; ++spins) {
                     if (!ok) ok = __hip_atomic_load((g_u32 *)const_cast<unsigned *>(f), __ATOMIC_RELAXED,
@@ -1863,26 +1866,25 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     // resource's 32-bit range takes (read per launch: a test switches it within a process)
     const char *snap_env = getenv("PAMG_CHAIN_SNAP16");
     int snap_ok = !(snap_env && atoi(snap_env) == 0);
+    void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
+                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &f0,
+                    &snap_ok, &stamps};
     // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
     const bool uni = L.nsub >= 64,
                lrec = k <= kChainRec && L.cpos && (int64_t)k * L.nup <= 2 * kChainNT && (int64_t)k * L.ndn <= kChainNT;
-    // the per-wave form (k_face_chain_pw): red-black with the split up pass, whole un_eles per wave whose
-    // colour lists fit 64 lanes, per-wave flags and neighbour lists (face_chain_setup); PAMG_CHAIN_PW=0
-    // keeps the workgroup form (read per launch: a test switches it within a process)
-    const char *pw_env = getenv("PAMG_CHAIN_PW");
-    const int qpw = (k + kPW - 1) / kPW;
-    const bool pw = !(pw_env && atoi(pw_env) == 0) && rb && lrec && early == 3 && !stamp_path && uni && L.nsub <= 64 &&
-                    qpw * std::max(nui, std::max(L.nup - nui, L.ndn)) <= 64 && L.chain_pw_off && L.chain_pw_list;
-    const int *nbo = pw ? L.chain_pw_off : nb_off, *nbl = pw ? L.chain_pw_list : nb_list;
-    void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nbo, &nbl, &tmo,
-                    &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &f0,
-                    &snap_ok, &stamps};
 
 #define PAMG_CHF(U_, R_) (lrec ? (const void *)k_face_chain<U_, R_, true> : (const void *)k_face_chain<U_, R_, false>)
     const void *f = uni ? (rb ? PAMG_CHF(true, true) : PAMG_CHF(true, false))
                         : (rb ? PAMG_CHF(false, true) : PAMG_CHF(false, false));
 #undef PAMG_CHF
-    if (pw) f = (const void *)k_face_chain_pw;
+    // the per-wave form (k_face_chain_pw): red-black with the split up pass, whole un_eles per wave whose
+    // colour lists fit 64 lanes, per-wave flags (face_chain_setup sizes them); PAMG_CHAIN_PW=0 keeps the
+    // workgroup form (read per launch: a test switches it within a process)
+    const char *pw_env = getenv("PAMG_CHAIN_PW");
+    const int qpw = (k + kPW - 1) / kPW;
+    if (!(pw_env && atoi(pw_env) == 0) && rb && lrec && early == 3 && !stamp_path && uni && L.nsub <= 64 &&
+        qpw * std::max(nui, std::max(L.nup - nui, L.ndn)) <= 64)
+        f = (const void *)k_face_chain_pw;
     hipError_t e = launch_coresident(f, grid, kChainNT, args, s);
     if (stamp_path) {
         std::vector<long long> h(nst);

@@ -132,9 +132,6 @@ struct Level {
     // (CSR over chain_g workgroups) and the flag words it polls (zeroed before every launch)
     int chain_g = 0;
     int *chain_nb_off = nullptr, *chain_nb_list = nullptr;
-    // the per-wave chain's (k_face_chain_pw): per (workgroup, wave) the flag words of the waves owning
-    // its un_eles' neighbours (CSR over 16 chain_g waves)
-    int *chain_pw_off = nullptr, *chain_pw_list = nullptr;
     unsigned *chain_flags = nullptr;
     size_t chain_flag_bytes = 0;
     // the flags' epoch: a chain call publishes epoch + s + 1 for its sweep s and the next call starts
