@@ -605,8 +605,14 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_BLDS
 #define PAMG_FACE_PP_BLDS 1
 #endif
+// NT = 576 (red-black, 1,024-sub-element un_eles): the 528 up items one per thread -- at 512 threads the
+// 16 left over made every up pass two face evaluations long; 72 VGPRs keep three workgroups (27 waves) per
+// CU. Likewise 192 threads for the 136 ups of a 256-sub-element un_ele (8 left over at 128)
+#ifndef PAMG_FACE_PP_WAVES576
+#define PAMG_FACE_PP_WAVES576 7
+#endif
 template <int TS, int NT, bool RB, int K>
-__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
+__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : NT == 576 ? PAMG_FACE_PP_WAVES576 : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
     const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
@@ -615,7 +621,8 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
     constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
     // red-black: the colour passes run over colour lists (Level::cpos), every lane with an item of the colour
     constexpr int NUP = M * (M + 1) / 2, KU = RB ? (NUP + NT - 1) / NT : PER, KD = RB ? (TS - NUP + NT - 1) / NT : 0;
-    static_assert(PER % 2 == 0 && M * M == TS && 3 * M <= NT && TS <= 1024, "whole un_ele tiles of <= 1,024, adjacent pairs per thread");
+    static_assert((RB || (TS % NT == 0 && PER % 2 == 0)) && M * M == TS && 3 * M <= NT && TS <= 1024,
+                  "whole un_ele tiles of <= 1,024; Jacobi: adjacent pairs per thread");
     // one LDS array: the iterate, the RHS, the halo snapshot of each sweep, omega / D
     // PAMG_FACE_PP_BLDS (A/B): 1 the RHS staged in LDS beside the iterate; 0 each item's RHS in registers,
     // loaded from memory at its position (less LDS: more workgroups per CU)
@@ -692,8 +699,8 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
             for (int c = 0; c < 3; ++c) ib[k][c] = RHS[c * pitch + s0 + (ij[k] < 0 ? 0 : ij[k])];
     (void)nup;
 #pragma unroll
-    for (int k = 0; k < PER; k += 2) {   // the iterate and the RHS into LDS, adjacent pairs
-        const int j = 2 * (t + NT * (k / 2));
+    for (int p = t; p < TS / 2; p += NT) {   // the iterate and the RHS into LDS, adjacent pairs
+        const int j = 2 * p;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const double2 v = ld2(A + c * pitch + s0 + j), r = BL ? ld2(RHS + c * pitch + s0 + j) : make_double2(0.0, 0.0);
@@ -809,8 +816,8 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
     };
     auto store = [&](double *o) {
 #pragma unroll
-        for (int k = 0; k < PER; k += 2) {
-            const int j = 2 * (t + NT * (k / 2));
+        for (int p = t; p < TS / 2; p += NT) {
+            const int j = 2 * p;
 #pragma unroll
             for (int c = 0; c < 3; ++c) st2(o + c * pitch + s0 + j, make_double2(X[c][j], X[c][j + 1]));
         }
@@ -1804,7 +1811,13 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
 #define PAMG_FPPK(TS, NT)                                          \
     if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \
     else { if (K == 2) PAMG_FPP(TS, NT, false, 2); else PAMG_FPP(TS, NT, false, 1); }
-    if (L.nsub == 1024) { PAMG_FPPK(1024, 512) }
+    // PAMG_FACE_PP_NT=512 (A/B): the red-black instances at 512 / 128 threads (k_face_pp's NT = 576 note)
+    static const bool nt512 = getenv("PAMG_FACE_PP_NT") && atoi(getenv("PAMG_FACE_PP_NT")) == 512;
+    if (L.nsub == 1024 && rb && !nt512) {
+        if (K == 2) PAMG_FPP(1024, 576, true, 2); else PAMG_FPP(1024, 576, true, 1);
+    } else if (L.nsub == 256 && rb && !nt512) {   // 136 ups: 192 threads, one each
+        if (K == 2) PAMG_FPP(256, 192, true, 2); else PAMG_FPP(256, 192, true, 1);
+    } else if (L.nsub == 1024) { PAMG_FPPK(1024, 512) }
     else if (L.nsub == 256) { PAMG_FPPK(256, 128) }
     else return hipErrorInvalidValue;   // (4,096: the iterate and RHS exceed the LDS)
 #undef PAMG_FPPK
