@@ -605,9 +605,10 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_BLDS
 #define PAMG_FACE_PP_BLDS 1
 #endif
-// NT = 576 (red-black, 1,024-sub-element un_eles): the 528 up items one per thread -- at 512 threads the
-// 16 left over made every up pass two face evaluations long; 72 VGPRs keep three workgroups (27 waves) per
-// CU. Likewise 192 threads for the 136 ups of a 256-sub-element un_ele (8 left over at 128)
+// NT: red-black passes with fewer threads than up sub-elements run a second up item on some threads. For
+// the 256-sub-element un_ele 192 threads (136 ups, one each) measured faster than 128 (0.71 vs 0.73 ms of
+// coarse launches per cycle); for the 1,024 one 576 threads (528 ups) measured slower than 512 (level-1
+// passes 0.85 vs 0.71 ms per cycle, profiles/r04_k_face_pp_nt.txt), so it keeps 512
 #ifndef PAMG_FACE_PP_WAVES576
 #define PAMG_FACE_PP_WAVES576 7
 #endif
@@ -1811,11 +1812,9 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
 #define PAMG_FPPK(TS, NT)                                          \
     if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \
     else { if (K == 2) PAMG_FPP(TS, NT, false, 2); else PAMG_FPP(TS, NT, false, 1); }
-    // PAMG_FACE_PP_NT=512 (A/B): the red-black instances at 512 / 128 threads (k_face_pp's NT = 576 note)
+    // PAMG_FACE_PP_NT=512 (A/B): the red-black 256 instance at 128 threads (k_face_pp's NT note)
     static const bool nt512 = getenv("PAMG_FACE_PP_NT") && atoi(getenv("PAMG_FACE_PP_NT")) == 512;
-    if (L.nsub == 1024 && rb && !nt512) {
-        if (K == 2) PAMG_FPP(1024, 576, true, 2); else PAMG_FPP(1024, 576, true, 1);
-    } else if (L.nsub == 256 && rb && !nt512) {   // 136 ups: 192 threads, one each
+    if (L.nsub == 256 && rb && !nt512) {   // 136 ups: 192 threads, one each
         if (K == 2) PAMG_FPP(256, 192, true, 2); else PAMG_FPP(256, 192, true, 1);
     } else if (L.nsub == 1024) { PAMG_FPPK(1024, 512) }
     else if (L.nsub == 256) { PAMG_FPPK(256, 128) }
