@@ -608,12 +608,9 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 // NT: red-black passes with fewer threads than up sub-elements run a second up item on some threads. For
 // the 256-sub-element un_ele 192 threads (136 ups, one each) measured faster than 128 (0.71 vs 0.73 ms of
 // coarse launches per cycle); for the 1,024 one 576 threads (528 ups) measured slower than 512 (level-1
-// passes 0.85 vs 0.71 ms per cycle, profiles/r04_k_face_pp_nt.txt), so it keeps 512
-#ifndef PAMG_FACE_PP_WAVES576
-#define PAMG_FACE_PP_WAVES576 7
-#endif
+// passes 0.85 vs 0.71 ms per cycle at seven waves per SIMD, profiles/r04_k_face_pp_nt.txt), so it keeps 512
 template <int TS, int NT, bool RB, int K>
-__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : NT == 576 ? PAMG_FACE_PP_WAVES576 : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
+__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
     const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
