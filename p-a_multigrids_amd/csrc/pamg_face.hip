@@ -1121,6 +1121,40 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
 // (at most kChainRec un_eles): the passes read them there instead of fetching them from memory in
 // every pass (the dependent record fetches were most of a sweep's pass time, r03 stamps)
 constexpr int kChainRec = 32, kRecW = 48;
+// the records of the workgroup's kv un_eles u0 .. into LDS, kRecW doubles each: S.c, S.K[9], S.w[3], the
+// face weights w[6], the omega / D table (24), the un_ele faces' node selectors (3)
+__device__ __forceinline__ void chain_load_recs(double *RS, const double *__restrict__ stc, const double *__restrict__ fface,
+                                                const int *__restrict__ fsx, int64_t u0, int kv, int t, int nt) {
+    for (int i = t; i < kv * kRecW; i += nt) {
+        const int uk = i / kRecW, q = i - uk * kRecW;
+        const int64_t u = u0 + uk;
+        double v = 0.0;
+        if (q == 0) v = stc[u * kStcStride + kStcC];
+        else if (q < 10) v = stc[u * kStcStride + kStcK + q - 1];
+        else if (q < 13) v = stc[u * kStcStride + kStcW + q - 10];
+        else if (q < 19) v = fface[u * kFaceStride + q - 13];
+        else if (q < 43) v = fface[u * kFaceStride + kFaceWD + q - 19];
+        else if (q < 46) v = (double)fsx[4 * u + fmface(q - 43) - 1];
+        RS[i] = v;
+    }
+}
+// item j's record from the LDS copy: f(R, un_ele, omega / D row, the un_ele's first tile position)
+template <class F>
+__device__ __forceinline__ void chain_rec(const double *RS, int j, int4 nb, int nsub_log2, int64_t u0, F &&f) {
+    const int uk = j >> nsub_log2;
+    const double *rs = RS + uk * kRecW;
+    FaceRec R;
+    R.S.c = rs[0];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) R.S.K[q] = rs[1 + q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) R.S.w[q] = rs[10 + q];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) R.w[q] = rs[13 + q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) R.sx[q] = (int)rs[43 + q];
+    f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
+}
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 constexpr int kAuxSc1 = 16;   // buffer instruction cache policy: sc1 (through to the coherent level)   // un_eles, doubles per record: S 13 | w 6 | WD 24 | sx 3
 template <bool UNI, bool RB, bool LREC>
@@ -1149,21 +1183,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
     const int m = H.m, ke = E >> nsub_log2;   // positions along an un_ele face, un_eles of the workgroup
     const int64_t u0 = s0 >> nsub_log2;
     const int nhalo = ke * 9 * m;
-    if constexpr (LREC) {
-        const int kv = (int)std::min<int64_t>(ke, (N >> nsub_log2) - u0);
-        for (int i = t; i < kv * kRecW; i += NT) {
-            const int uk = i / kRecW, q = i - uk * kRecW;
-            const int64_t u = u0 + uk;
-            double v = 0.0;
-            if (q == 0) v = stc[u * kStcStride + kStcC];
-            else if (q < 10) v = stc[u * kStcStride + kStcK + q - 1];
-            else if (q < 13) v = stc[u * kStcStride + kStcW + q - 10];
-            else if (q < 19) v = fface[u * kFaceStride + q - 13];
-            else if (q < 43) v = fface[u * kFaceStride + kFaceWD + q - 19];
-            else if (q < 46) v = (double)fsx[4 * u + fmface(q - 43) - 1];
-            RS[i] = v;
-        }
-    }
+    if constexpr (LREC) chain_load_recs(RS, stc, fface, fsx, u0, (int)std::min<int64_t>(ke, (N >> nsub_log2) - u0), t, NT);
     // with LREC the passes run over item lists (red-black: each colour over its positions, all lanes
     // busy; Jacobi: the positions in order), as k_face_wave's
     constexpr int KU = PER, KD = RB ? 1 : 0;
@@ -1318,21 +1338,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
     auto ihv = [&](int64_t uu, int mf, int sp, int kk) {
         return HI[(((int)(uu - u0) * 3 + mf - 1) * m + sp - 1) * 3 + kk];
     };
-    auto irec = [&](int j, int4 nb, auto &&f) {
-        const int uk = j >> nsub_log2;
-        const double *rs = RS + uk * kRecW;
-        FaceRec R;
-        R.S.c = rs[0];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) R.S.K[q] = rs[1 + q];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) R.S.w[q] = rs[10 + q];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) R.w[q] = rs[13 + q];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) R.sx[q] = (int)rs[43 + q];
-        f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
-    };
+    auto irec = [&](int j, int4 nb, auto &&f) { chain_rec(RS, j, nb, nsub_log2, u0, f); };
     // the snapshot's 16-byte loads: a face's 3m words and the slot pitch even (16-byte aligned pairs)
     // (and the snapshot buffer within a buffer resource's 32-bit range; snap_ok = 0 forces the 8-byte
     // form, the path of a larger buffer -- PAMG_CHAIN_SNAP16=0, tests/test_face_operator.py)
@@ -1511,18 +1517,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
     const int q = (ke + kPW - 1) / kPW;                  // un_eles per wave
     const int ua = std::min(kv, v * q), ub = std::min(kv, ua + q);   // this wave's un_eles [ua, ub)
     const int nsub = 1 << nsub_log2, ndn = nsub - nup, n1 = nup - nui;
-    for (int i = t; i < kv * kRecW; i += NT) {   // the un_eles' records (as k_face_chain's LREC)
-        const int uk = i / kRecW, c = i - uk * kRecW;
-        const int64_t u = u0 + uk;
-        double val = 0.0;
-        if (c == 0) val = stc[u * kStcStride + kStcC];
-        else if (c < 10) val = stc[u * kStcStride + kStcK + c - 1];
-        else if (c < 13) val = stc[u * kStcStride + kStcW + c - 10];
-        else if (c < 19) val = fface[u * kFaceStride + c - 13];
-        else if (c < 43) val = fface[u * kFaceStride + kFaceWD + c - 19];
-        else if (c < 46) val = (double)fsx[4 * u + fmface(c - 43) - 1];
-        RS[i] = val;
-    }
+    chain_load_recs(RS, stc, fface, fsx, u0, kv, t, NT);   // the un_eles' records
     // the lane's items: 0 an up sub-element without halo words, 1 one with words, D a down one
     Items<1> I0, I1, ID;
     auto mk = [&](Items<1> &I, int n, int o) {
@@ -1554,21 +1549,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
     auto ixin = [&](int c, int qq) { return X[c][qq]; };
     auto ihv = [&](int64_t uu, int mf, int sp, int kk) { return HI[(((int)(uu - u0) * 3 + mf - 1) * m + sp - 1) * 3 + kk]; };
     auto nohv = [](int64_t, int, int, int) { return 0.0; };
-    auto irec = [&](int j, int4 nb, auto &&f) {
-        const int uk = j >> nsub_log2;
-        const double *rs = RS + uk * kRecW;
-        FaceRec R;
-        R.S.c = rs[0];
-#pragma unroll
-        for (int c = 0; c < 9; ++c) R.S.K[c] = rs[1 + c];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) R.S.w[c] = rs[10 + c];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) R.w[c] = rs[13 + c];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) R.sx[c] = (int)rs[43 + c];
-        f(R, u0 + uk, rs + 19 + 3 * face_pattern(nb), uk << nsub_log2);
-    };
+    auto irec = [&](int j, int4 nb, auto &&f) { chain_rec(RS, j, nb, nsub_log2, u0, f); };
     auto tstore = [&]() {
         for (int j = pa + ln; j < pb; j += 64)
 #pragma unroll
