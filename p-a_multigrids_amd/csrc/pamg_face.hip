@@ -1501,6 +1501,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                                                                int nup, int nui, int early, unsigned f0, int snap_ok,
                                                                long long *stamps) {
     (void)omega;
+    (void)early;
     (void)stamps;
     constexpr int NT = kChainNT;
     __shared__ double X[3][NT * kChainPer];
@@ -1621,20 +1622,16 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
             for (int c = 0; c < 3; ++c) X[c][I1.j[0]] = r[c];
             if (tout) halo_words<true>(Hn, hr, hq, r, sw == 0);
         });
-        // drained, then this wave's flag: before the down pass, or (early = 4, A/B) after it, the drain
-        // under the pass
-        auto publish = [&]() {
+        if (tout) {   // drained, then this wave's flag
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (ln == 0)
                 __hip_atomic_store((g_u32 *)flags + (size_t)w * kPW + v, f0 + (unsigned)(sw + 1), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-        };
-        if (tout && early != 4) publish();
+        }
         items_pass<1>(ID, ixin, ihv, irec, level1, rdt, [&](int, const double r[3]) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) X[c][ID.j[0]] = r[c];
         });
-        if (tout && early == 4) publish();
         if (store == 1 && sw + 2 == run) tstore();   // the last sweep's tnew := tnew_nonlin (its start)
     }
     for (int j = pa + ln; j < pb; j += 64)   // tnew_nonlin (store 2: tnew, the dead last sweep's :550)
@@ -1850,8 +1847,7 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     int nup = L.nup;
     const double *SRC = from_T ? L.T : L.TNN;
     // PAMG_CHAIN_EARLY (A/B): 0 publish after the down pass, 1 the words after the up pass, 2 words and
-    // flag, 3 (default) as 2 with the up pass split around the wait (k_face_chain); 4 the per-wave chain
-    // with its flag after the down pass (the workgroup chain takes it as 2)
+    // flag, 3 (default) as 2 with the up pass split around the wait (k_face_chain)
     static const int early_env = [] { const char *e = getenv("PAMG_CHAIN_EARLY"); return e ? atoi(e) : 3; }();
     int nui = L.nui, early = L.words_up ? early_env : 0;
     // the split up pass needs each half's items in one item per thread
@@ -1876,7 +1872,7 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     // workgroup form (read per launch: a test switches it within a process)
     const char *pw_env = getenv("PAMG_CHAIN_PW");
     const int qpw = (k + kPW - 1) / kPW;
-    if (!(pw_env && atoi(pw_env) == 0) && rb && lrec && (early == 3 || early == 4) && !stamp_path && uni && L.nsub <= 64 &&
+    if (!(pw_env && atoi(pw_env) == 0) && rb && lrec && early == 3 && !stamp_path && uni && L.nsub <= 64 &&
         qpw * std::max(nui, std::max(L.nup - nui, L.ndn)) <= 64)
         f = (const void *)k_face_chain_pw;
     hipError_t e = launch_coresident(f, grid, kChainNT, args, s);
