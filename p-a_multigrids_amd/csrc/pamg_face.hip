@@ -1561,6 +1561,18 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
     const int tin_bytes = (int)std::min<int64_t>(tin_bytes64, (1ll << 31) - 1);
     const int na = nb_off[w], nn = nb_off[w + 1] - na;
     const int ha = ua * 9 * m, hb = ub * 9 * m;   // the wave's slots of the snapshot image
+    // the snapshot loads' byte offsets (the same every sweep: only the buffer alternates) when a lane
+    // has at most two (two un_eles of m = 8: 144 words, 72 pairs), so the sweep does no index division
+    const bool snap_pre = snap16 && hb - ha <= 256;
+    int so[2] = {-1, -1};
+    if (snap_pre)
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            const int idx = ha + 2 * ln + 128 * it;
+            if (idx >= hb) continue;
+            const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
+            so[it] = (int)(((u0 + uk) * slots * 3 + (int64_t)mf * slots + off) * 8);
+        }
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
         double *tout = sw + 1 < total ? (((total - 2 - sw) & 1) ? buf1 : buf0) : nullptr;
@@ -1599,7 +1611,18 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
             }
         }
         // the snapshot of the wave's un_eles (sc1: through to the coherent level)
-        if (snap16) {
+        if (snap_pre) {   // at most two 16-byte loads a lane, their offsets computed once for the call
+            asm volatile("" : "+v"(so[0]), "+v"(so[1]));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(tin), (short)0, tin_bytes, 0x00020000);
+#pragma unroll
+            for (int it = 0; it < 2; ++it) {
+                if (so[it] < 0) continue;
+                const int idx = ha + 2 * ln + 128 * it;
+                const v4u val = __builtin_amdgcn_raw_buffer_load_b128(rs, so[it], 0, kAuxSc1);
+                HI[idx] = __longlong_as_double(((long long)val.y << 32) | val.x);
+                HI[idx + 1] = __longlong_as_double(((long long)val.w << 32) | val.z);
+            }
+        } else if (snap16) {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(tin), (short)0, tin_bytes, 0x00020000);
             for (int idx = ha + 2 * ln; idx < hb; idx += 128) {
                 const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
