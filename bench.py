@@ -56,7 +56,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # lanes x 2 flops x 2.4 GHz)
 FP64_PEAK_TFLOPS = 78.6
 EVENT_STRIDE = 10
-ALL_CLASSES = 0x7F7F   # every timing class (PAMG_K_*) but sweep_bench
+ALL_CLASSES = 0xFF7F   # every timing class (PAMG_K_*) but sweep_bench
+SWEEP_LAUNCHES = 60    # launches of each level-1 HBM sweep roofline measurement
 
 
 def parse():
@@ -371,6 +372,7 @@ def main():
     a = parse()
     time_loop = None
     roofline_hbm = None
+    extra_pre = {}
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -404,6 +406,26 @@ def main():
                                    halo_mode=a.halo_mode, comm=comm, fused=a.fused, arith=a.arith,
                                    halo_exchange=a.halo_exchange)
     s.begin_timestep()
+    if rank == 0 and world == 1 and not a.no_extra:
+        # the north star's HBM roofline: one level-1 sweep of the assembled element-block-sparse
+        # operator, 168 B per sub-element (x, b, out, the 3x3 block, omega/D), and the matrix-free sweep beside
+        # it; HIP events around SWEEP_LAUNCHES launches each (tests/test_roofline_kernels.py pins their output).
+        # Measured first, on the same handle (the sweeps write a scratch buffer only), so the V-cycle's warm-up and
+        # timed call follow ~30 ms of GPU work (profiles/r05_a_shape_probe.txt: +2 % over an idle GPU's first call)
+        for asm in (False, True):
+            ms, by = s.sweep_bench(SWEEP_LAUNCHES, asm)
+            extra_pre["sweep_assembled" if asm else "sweep_stencil"] = dict(
+                ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
+                frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3), launches=SWEEP_LAUNCHES)
+            if asm:
+                roofline_hbm = {"bound": "hbm", "kernel": "k_sweep_assembled (one level-1 Jacobi sweep over the "
+                                "assembled block-CSR operator, matrices.F90:997-1198; contracted arithmetic)",
+                                "achieved": round(by / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "traffic": pmc_traffic("sweep_assembled", a.nsplit, 1),
+                                "alg_bytes_per_launch": by, "bytes_per_sub_element": 168,
+                                "sub_elements": mesh.U * 4 ** a.nsplit, "ms_per_launch": round(ms, 4),
+                                "events": f"HIP event pair around each of {SWEEP_LAUNCHES} launches"}
     s.vcycle(a.warmup)
     s.synchronize()
     # per-kernel HIP events (the roofline) inside the timed region on one GPU; with N ranks
@@ -494,6 +516,12 @@ def main():
         kk = [None] * world
         dist.all_gather_object(kk, ms_per_launch / cycles_per_launch)
         extra["rank_kernel_ms_per_cycle"] = [round(v, 5) for v in kk]
+        # the per-call exchange started early (post-pass call): per rank (exchange start, exchange end,
+        # resident launch end) in us from the launch's start -- end < launch end: hidden behind the launch
+        xt = s.early_exchange_times() if not live_events else None
+        xa = [None] * world
+        dist.all_gather_object(xa, [round(v, 1) for v in xt] if xt else None)
+        extra["early_exchange_us"] = xa
     if rank == 0 and world == 1 and not a.no_extra:
         # the round-1 form on the same workload: one HBM-bound launch per cycle (call schedule 1),
         # its pipelined launch against the HBM roofline
@@ -521,23 +549,7 @@ def main():
                 pipe_gbs=round(bp / (msp * 1e-3) / 1e9, 1), pipe_frac=round(bp / (msp * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 pipe_traffic=pmc_traffic("vcycle_pipe", a.nsplit, a.levels))
         s1.close()
-        for asm in (False, True):
-            ms, by = s.sweep_bench(20, asm)
-            extra["sweep_assembled" if asm else "sweep_stencil"] = dict(
-                ms=round(ms, 4), bytes_per_launch=by, gbs=round(by / (ms * 1e-3) / 1e9, 1),
-                frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
-            if asm:
-                # the north star's HBM roofline: one level-1 sweep of the assembled
-                # element-block-sparse operator, 168 B per sub-element (x, b, out, the 3x3 block,
-                # omega/D), HIP events around 20 launches (tests/test_roofline_kernels.py pins its output)
-                roofline_hbm = {"bound": "hbm", "kernel": "k_sweep_assembled (one level-1 Jacobi sweep over the "
-                                "assembled block-CSR operator, matrices.F90:997-1198; contracted arithmetic)",
-                                "achieved": round(by / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                "traffic": pmc_traffic("sweep_assembled", a.nsplit, 1),
-                                "alg_bytes_per_launch": by, "bytes_per_sub_element": 168,
-                                "sub_elements": mesh.U * 4 ** a.nsplit, "ms_per_launch": round(ms, 4),
-                                "events": "HIP event pair around each of 20 launches"}
+        extra.update(extra_pre)
         time_loop = measure_time_loop(s)
         # the matrices.F90 SpMV (csr_mul_array, 3 entries per row) over the level-1 operator's
         # size in the reference's block numbering: 3 N1 rows, 52 B per row (3 x (4 B column +

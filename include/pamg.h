@@ -64,7 +64,9 @@ extern "C" {
 #define PAMG_K_VCYCLE_RES 12     /* resident V-cycle call: every cycle of a pamg_vcycle call in one launch */
 #define PAMG_K_VCYCLE_RES_RHSF 13 /* the resident launch that starts a pamg_run step */
 #define PAMG_K_VCYCLE_CORR 14    /* the corrected V-cycle's resident call (cycle = 1): a pamg_vcycle call in one launch */
-#define PAMG_K_COUNT 15
+#define PAMG_K_HALO_EARLY 15     /* the resident call's per-call exchange, started on a device signal once the tiles
+                                    with remote faces have finished (comm stream; overlapped with the launch) */
+#define PAMG_K_COUNT 16
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;
@@ -283,6 +285,11 @@ int pamg_comm_local_group(pamg_handle *const *hs, int n);
 /* RCCL version (ncclGetVersion) and the path of the librccl this library is bound to;
  * returns 0 (no communicator), 1 (RCCL) or 2 (local group), < 0 on error */
 int pamg_comm_info(pamg_handle *h, int *version, char *lib_path, int len);
+/* the last pamg_vcycle call whose per-call exchange started early (timing class PAMG_K_HALO_EARLY enabled):
+ * t[0] the exchange's start (the comm stream past the device signal), t[1] its end, t[2] the end of the
+ * resident launch -- microseconds from the launch's start (t[1] < t[2]: the exchange was hidden). PAMG_ERR_STATE
+ * if no such call was recorded since the timing was enabled */
+int pamg_early_exchange_times(pamg_handle *h, double t[3]);
 
 /* ---- host-only halo plan (tooling / CPU tests of the partitioned exchange) ---- */
 typedef struct pamg_plan pamg_plan;

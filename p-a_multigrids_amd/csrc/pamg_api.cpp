@@ -112,19 +112,44 @@ hipEvent_t take_event(pamg_handle *h) {
     return e;
 }
 
+// in_packet (the resident launches, one kernel per call) with PAMG_EVENTS_IN_PACKET=1: the pair goes to the
+// launch itself (launch_events, hipExtLaunchKernel), which records it in its dispatch packet around the
+// kernel, instead of two marker packets (a marker pair costs ~26 us per 20-cycle call in the driver's shape,
+// profiles/r05_a_shape_probe.txt; A/B runs)
+bool events_in_packet() {
+    static const bool on = getenv("PAMG_EVENTS_IN_PACKET") && atoi(getenv("PAMG_EVENTS_IN_PACKET")) == 1;
+    return on;
+}
 struct Span {
-    pamg_handle *h; int kid; double bytes; hipStream_t s; hipEvent_t a = nullptr;
-    Span(pamg_handle *h_, int kid_, double bytes_, hipStream_t s_ = nullptr)
+    pamg_handle *h; int kid; double bytes; hipStream_t s; hipEvent_t a = nullptr, b = nullptr; bool pk = false;
+    Span(pamg_handle *h_, int kid_, double bytes_, hipStream_t s_ = nullptr, bool in_packet = false)
         : h(h_), kid(kid_), bytes(bytes_), s(s_ ? s_ : h_->stream) {
         if ((h->timing.mask & (1u << kid)) && h->timing.seq[kid]++ % h->timing.stride == 0) {
             a = take_event(h);
-            (void)hipEventRecord(a, s);
+            if (in_packet && events_in_packet()) {
+                pk = true;
+                b = take_event(h);
+                launch_events() = LaunchEvents{a, b, false};
+            } else {
+                (void)hipEventRecord(a, s);
+            }
         }
     }
     ~Span() {
         if (!a) return;
-        hipEvent_t b = take_event(h);
-        (void)hipEventRecord(b, s);
+        if (pk) {
+            LaunchEvents &E = launch_events();
+            const bool used = E.used;
+            E = LaunchEvents{};
+            if (!used) {   // the launch did not take them (an error path): nothing was recorded
+                h->timing.pool.push_back(a);
+                h->timing.pool.push_back(b);
+                return;
+            }
+        } else {
+            b = take_event(h);
+            (void)hipEventRecord(b, s);
+        }
         h->timing.pending.push_back(Timing::Rec{kid, a, b, bytes});
     }
 };
@@ -328,6 +353,42 @@ int xc_setup(pamg_handle *h, int cycles) {
     return PAMG_OK;
 }
 
+// the early per-call exchange of the resident call: the tile order with the tiles that hold a remote
+// face first (they then run in the launch's first round of workgroups, and the exchange of their words
+// overlaps the rounds after it), the counter and the signal. PAMG_EARLY_XC=0 turns it off (A/B runs)
+int xe_setup(pamg_handle *h) {
+    if (h->xe_nremote < 0) {
+        std::vector<char> rem;
+        vcycle_remote_tiles(h->lv[1], h->U, h->p.n_split, rem);
+        std::vector<int> order;
+        order.reserve(rem.size());
+        for (size_t b = 0; b < rem.size(); ++b)
+            if (rem[b]) order.push_back((int)b);
+        const int nr = (int)order.size();
+        for (size_t b = 0; b < rem.size(); ++b)
+            if (!rem[b]) order.push_back((int)b);
+        if (nr > 0) CHK(dev_upload(h, &h->xe_map, order));
+        h->xe_nremote = nr;
+    }
+    if (h->xe_nremote > 0 && !h->xe_done) {
+        CHK(dev_alloc(h, &h->xe_done, 1));
+        HIPCHK(h, hipMemsetAsync(h->xe_done, 0, sizeof(unsigned), h->stream));
+        h->xe_total = 0;
+    }
+    if (h->xe_nremote > 0 && !h->xc_sig) {
+        HIPCHK(h, hipExtMallocWithFlags((void **)&h->xc_sig, sizeof(unsigned long long), hipMallocSignalMemory));
+        unsigned long long v = 0;
+        HIPCHK(h, hipMemcpy(&v, h->xc_sig, sizeof v, hipMemcpyDeviceToHost));
+        h->xc_sig_base = v;
+    }
+    return PAMG_OK;
+}
+
+bool early_xc_enabled() {
+    static const bool on = !(getenv("PAMG_EARLY_XC") && atoi(getenv("PAMG_EARLY_XC")) == 0);
+    return on;
+}
+
 int halo(pamg_handle *h, int l, double *dst = nullptr) {
     const HaloPlan &P = h->lv[l].halo;
     if (h->comm && !P.peers.empty()) {
@@ -381,11 +442,12 @@ int comm_error(pamg_handle *h) {
 // completes; PAMG_COMM_TIMEOUT_S, when set, also bounds the wait. The device-copy transport
 // (pamg_comm_local_group) is polled the same way with its exchange bound (PAMG_COMM_TIMEOUT_S,
 // default 120 s): its resident call's comm stream waits on a device signal (hipStreamWaitValue64)
-// that a faulted or stopped launch would never raise. The poll sleeps 20 us between queries and
-// checks the communicator every 16th; PAMG_SYNC_SPIN_MS=<ms> spins on hipStreamQuery first (the
-// N = 8 rank's 20-cycle call: blocking hipStreamSynchronize 150.3 us, a 20 ms spin 154.2, the
-// sleeping poll 155.3 -- within noise of each other, profiles/r03_m_sync_probe.txt; a spin keeps a
-// core busy per rank for no measured gain, so it is off by default)
+// that a faulted or stopped launch would never raise. The poll spins on hipStreamQuery for the first
+// PAMG_SYNC_SPIN_MS (default 5 ms; the communicator checked every 256th query), then sleeps 20 us
+// between queries and checks the communicator every 16th. A sleep of 20 us lasts ~60 us or more (the
+// kernel's timer slack): with the sleeping poll from the start, a rank's 20-cycle call at config 4's
+// N = 8 shape (1,024 un_eles, an RCCL self-peer exchange) took 233.7 us against 169.2 us without a
+// communicator, its exchange hidden behind the launch (profiles/r05_c_xe_probe.txt)
 int sync_stream(pamg_handle *h, hipStream_t s) {
     if (!h->comm || (!h->comm->nccl && !h->comm->local)) {
         HIPCHK(h, hipStreamSynchronize(s));
@@ -394,7 +456,7 @@ int sync_stream(pamg_handle *h, hipStream_t s) {
     const char *env = getenv("PAMG_COMM_TIMEOUT_S");
     // unset: no limit on an RCCL rank (only the error polling), the exchange bound on a local group
     const int limit = env ? atoi(env) : h->comm->local ? local_timeout_s() : 0;
-    static const int spin_ms = getenv("PAMG_SYNC_SPIN_MS") ? std::max(0, atoi(getenv("PAMG_SYNC_SPIN_MS"))) : 0;
+    static const int spin_ms = getenv("PAMG_SYNC_SPIN_MS") ? std::max(0, atoi(getenv("PAMG_SYNC_SPIN_MS"))) : 5;
     const auto t0 = std::chrono::steady_clock::now();
     const auto spin_end = t0 + std::chrono::milliseconds(spin_ms);
     for (unsigned i = 0;; ++i) {
@@ -1242,7 +1304,7 @@ int vcycle_corrected_resident(pamg_handle *h, int n) {
     }
     h->rhsn_valid = false;   // residuals and coarse RHS rewritten (RHSN does not follow them)
     {
-        Span sp(h, PAMG_K_VCYCLE_CORR, vcycle_corr_bytes(h));
+        Span sp(h, PAMG_K_VCYCLE_CORR, vcycle_corr_bytes(h), nullptr, true);
         HIPCHK(h, launch_vcycle_corrected(h->stream, h->lv, L, h->U, h->p.n_split, h->p.n_smooth, h->p.n_coarse,
                                           1 / h->p.dt, h->tov, h->tovo, P1.send_buf(buf), h->lv[2].RHSN, PAMG_KEEP_ALL, n));
     }
@@ -1381,7 +1443,8 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
             CHK(xc_setup(h, n));
             HIPCHK(h, hipMemsetAsync(h->xc_done, 0, (size_t)(n - 1) * sizeof(unsigned), h->stream));
             {
-                Span sp(h, PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, false) + 24.0 * (n - 1) * P1.remote.size());
+                Span sp(h, PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, false) + 24.0 * (n - 1) * P1.remote.size(),
+                        nullptr, true);
                 HIPCHK(h, launch_vcycle_resident_xc(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt,
                                                     h->tov, h->tovo, P1.send_buf(buf), L2.RHSN, keep, n, P1.d_ring,
                                                     3 * (int64_t)P1.remote.size(), h->xc_done, h->xc_sig));
@@ -1394,10 +1457,54 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
                 }
             h->xc_sig_base += (unsigned long long)(n - 1);
         } else {
-            Span sp(h, rhsf ? PAMG_K_VCYCLE_RES_RHSF : PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, rhsf));
-            HIPCHK(h, launch_vcycle_resident(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
-                                             h->tovo, P1.send_buf(buf), L2.RHSN, keep, rhsf,
-                                             two ? P1.send_buf(1 - buf) : nullptr, n, steps));
+            // the per-call exchange, started early: the call's halo words are final once a tile has run its
+            // last cycle, so the tiles with remote faces run first (tile order), count their ends, and the
+            // last of them raises xc_sig; the comm stream waits on it and exchanges while the other tiles'
+            // rounds run (the exchange reads only their send words and writes only the remote slots of
+            // t_overlap / t_overlap_old, which no tile of the launch writes). A call that starts a time step
+            // (RHSF) writes the send buffers' told halves itself and exchanges after the launch.
+            const bool xe = !rhsf && !dead_after && steps == 1 && h->comm && !P1.peers.empty() && early_xc_enabled();
+            EarlyXc X{};
+            if (xe) {
+                // the counter is never reset (a memset before the launch delays it by a few us): this call's
+                // remote tiles complete it at the running total
+                CHK(xe_setup(h));
+                h->xe_total += (unsigned)h->xe_nremote;
+                X = EarlyXc{h->xe_map, h->xe_done, h->xe_total, h->xc_sig};
+            }
+            const bool diag = xe && (h->timing.mask & (1u << PAMG_K_HALO_EARLY));
+            if (diag) {
+                for (auto &e : h->xe_ev)
+                    if (!e) HIPCHK(h, hipEventCreate(&e));
+                HIPCHK(h, hipEventRecord(h->xe_ev[0], h->stream));
+            }
+            {
+                Span sp(h, rhsf ? PAMG_K_VCYCLE_RES_RHSF : PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, rhsf), nullptr,
+                        true);
+                HIPCHK(h, launch_vcycle_resident(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
+                                                 h->tovo, P1.send_buf(buf), L2.RHSN, keep, rhsf,
+                                                 two ? P1.send_buf(1 - buf) : nullptr, n, steps, xe ? &X : nullptr));
+            }
+            if (xe) {
+                if (diag) HIPCHK(h, hipEventRecord(h->xe_ev[3], h->stream));
+                HIPCHK(h, hipStreamWaitValue64(h->stream_comm, h->xc_sig, h->xc_sig_base + 1, hipStreamWaitValueGte));
+                h->xc_sig_base += 1;
+                if (diag) HIPCHK(h, hipEventRecord(h->xe_ev[1], h->stream_comm));
+                {
+                    Span sp(h, PAMG_K_HALO_EARLY, 2.0 * 48.0 * (double)(P1.remote.size() + P1.recv_dst.size()),
+                            h->stream_comm);
+                    CHK(exchange(h, 1, buf, h->stream_comm));
+                }
+                if (diag) {
+                    HIPCHK(h, hipEventRecord(h->xe_ev[2], h->stream_comm));
+                    h->xe_ev_valid = true;
+                }
+                HIPCHK(h, hipEventRecord(h->ev_sent[buf], h->stream_comm));
+                h->sent_pending[buf] = true;
+                P1.send_cur = buf;
+                h->tnn_level = 1;
+                return join_comm(h);
+            }
         }
         if (rhsf) {
             h->overlap_static_l1 = kt != 0;
@@ -1556,6 +1663,9 @@ void free_levels(pamg_handle *h) {
     h->wave_flags = nullptr;
     h->wave_gran = nullptr;
     h->wave_band = -1;
+    dev_free(h->xe_map);
+    h->xe_map = nullptr;
+    h->xe_nremote = -1;
     h->mesh_ready = false;
 }
 
@@ -2205,8 +2315,22 @@ int pamg_timing_enable(pamg_handle *h, unsigned mask) {
     return PAMG_OK;
 }
 
+int pamg_early_exchange_times(pamg_handle *h, double t[3]) {
+    if (!h || !t) return PAMG_ERR_ARG;
+    if (!h->xe_ev_valid) return PAMG_ERR_STATE;
+    CHK(sync_stream(h, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream_comm));
+    for (int k = 0; k < 3; ++k) {
+        float ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&ms, h->xe_ev[0], h->xe_ev[k + 1]));
+        t[k] = 1e3 * (double)ms;
+    }
+    return PAMG_OK;
+}
+
 int pamg_timing_reset(pamg_handle *h) {
     if (!h) return PAMG_ERR_ARG;
+    h->xe_ev_valid = false;
     CHK(drain_timing(h));
     for (int k = 0; k < PAMG_K_COUNT; ++k) {
         h->timing.ms[k] = 0; h->timing.count[k] = 0; h->timing.bytes[k] = 0; h->timing.seq[k] = 0;
@@ -2314,6 +2438,9 @@ int pamg_destroy(pamg_handle *h) {
     dev_free(h->scratch);
     dev_free(h->chain_tmo);
     dev_free(h->xc_done);
+    dev_free(h->xe_done);
+    for (auto e : h->xe_ev)
+        if (e) (void)hipEventDestroy(e);
     if (h->xc_sig) (void)hipFree(h->xc_sig);
     for (auto e : h->timing.pool) (void)hipEventDestroy(e);
     for (auto &r : h->timing.pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }

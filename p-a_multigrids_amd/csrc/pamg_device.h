@@ -209,7 +209,9 @@ __device__ __forceinline__ void st_halo(double *p, double x) {
 // both arrays, the told half of a send entry). The per-step kernels write both;
 // the fused V-cycle writes TNEW only and leaves STATIC to k_overlap_static.
 // COH: the t_overlap words are written through (st_coh) for readers in other workgroups
-template <bool TNEW = true, bool STATIC = true, bool COH = false>
+// SCOH: the tnew half of a send entry is written through (the resident call's early exchange reads
+// the send buffer while the launch still runs, pamg_api.cpp vcycle_fused)
+template <bool TNEW = true, bool STATIC = true, bool COH = false, bool SCOH = false>
 __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, int i, const double t[3],
                                           const double to[3]) {
     const int mode = rec.x & 3;
@@ -234,7 +236,7 @@ __device__ __forceinline__ void halo_face(const HaloArgs &H, int4 rec, int f, in
         double *o = H.send + 6 * (int64_t)(rec.z + i - 1);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            if (TNEW) o[c] = t[c];
+            if (TNEW) st_halo<SCOH>(o + c, t[c]);
             if (STATIC) o[3 + c] = to[c];
         }
     }

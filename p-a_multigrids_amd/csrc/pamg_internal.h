@@ -228,6 +228,16 @@ struct pamg_handle {
     int xc_cap = 0;
     unsigned long long *xc_sig = nullptr;
     unsigned long long xc_sig_base = 0;
+    // the early per-call exchange of the resident call (halo_exchange = 0 on a partition): the tile
+    // order with the remote tiles first (device, built on first use), their count, its counter
+    int *xe_map = nullptr;
+    int xe_nremote = -1;             // -1: not built
+    unsigned *xe_done = nullptr;
+    unsigned xe_total = 0;           // remote-tile ends counted in *xe_done so far (mod 2**32)
+    // diagnostics (timing class PAMG_K_HALO_EARLY enabled): events at the last early-exchange call's launch
+    // start, exchange start (the signal seen), exchange end and launch end
+    hipEvent_t xe_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool xe_ev_valid = false;
     int cus = 0;                     // compute units of the device
 };
 
@@ -255,6 +265,14 @@ int build_face(pamg_handle *h, int l, const double *Xg, const int *neig, const i
 
 // ---- kernels (pamg_kernels.hip) ----
 namespace pamg {
+// the timing events of the next resident launch on this host thread (pamg_api.cpp Span, in-packet form): a
+// launch that finds them set launches with hipExtLaunchKernel, whose dispatch packet records them around the
+// kernel itself -- no marker packets between back-to-back work (pamg_vcycle.hip)
+struct LaunchEvents {
+    hipEvent_t a = nullptr, b = nullptr;
+    bool used = false;
+};
+LaunchEvents &launch_events();
 hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int sweeps, int solver,
                          double rdt, double omega, double *tov, double *tovo);
 hipError_t launch_residual(hipStream_t s, const Level &L, double rdt, bool neg = false);
@@ -310,9 +328,22 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
 // stores as keep says; rhsf: the launch starts the time step (as launch_vcycle_fine's)
 // steps > 1 (rhsf): a whole pamg_run -- `steps` time steps of `cycles` cycles, each step starting
 // with told := tnew and its RHS -- in one launch (vcycle_resident_run_supported)
+// the early per-call exchange (pamg_api.cpp vcycle_fused): the workgroups take the tiles in tile_map's
+// order (remote tiles first); each tile with a face on another rank counts its end in *done once its send
+// words are written through, and the one whose count reaches `target` (the running total of remote-tile
+// ends, mod 2**32: the counter is never reset) adds 1 to *sig
+struct EarlyXc {
+    const int *tile_map;
+    unsigned *done;
+    unsigned target;
+    unsigned long long *sig;
+};
 hipError_t launch_vcycle_resident(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                   int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                                  int keep, bool rhsf, double *send_b, int cycles, int steps = 1);
+                                  int keep, bool rhsf, double *send_b, int cycles, int steps = 1,
+                                  const EarlyXc *xe = nullptr);
+// per level-1 tile of the resident launch: does it hold a face whose neighbour is on another rank
+void vcycle_remote_tiles(const Level &L1, int U, int n_split, std::vector<char> &remote);
 // the resident call with an exchange after every cycle (halo_exchange = 1): cycle c < cycles - 1
 // packs its remote halo words (3 per entry) into ring + c ring_stride and, once every workgroup has,
 // adds 1 to *xc_sig (xc_done: cycles - 1 zeroed counters); the last cycle is the plain resident call's

@@ -47,6 +47,11 @@ PAMG_VC_DECL(1) PAMG_VC_DECL(2) PAMG_VC_DECL(3) PAMG_VC_DECL(4) PAMG_VC_DECL(5) 
 PAMG_VC_DECL(8)
 #undef PAMG_VC_DECL
 
+LaunchEvents &launch_events() {
+    thread_local LaunchEvents e;
+    return e;
+}
+
 namespace {
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,
@@ -56,7 +61,10 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     const bool coarse = part == 1;
     if (part >= 2 && L < 2) return hipErrorInvalidValue;
     if (part >= 4 && cycles < 1) return hipErrorInvalidValue;
-    if ((part == 6) != (xc != nullptr) || (part == 6 && (cycles < 2 || !xc->ring || !xc->xc_done || !xc->xc_sig)))
+    // part 6: the per-cycle exchange's ring; part 4 may carry the early per-call exchange (tile order,
+    // remote-tile counter, signal)
+    if ((part == 6 && (!xc || cycles < 2 || !xc->ring || !xc->xc_done || !xc->xc_sig)) ||
+        (xc && part != 6 && (part != 4 || !xc->tile_map || !xc->xe_done || !xc->xc_sig)))
         return hipErrorInvalidValue;
     if (steps != 1 && !(part == 5 && steps > 1 && vcycle_resident_run_supported(n_split, L))) return hipErrorInvalidValue;
     if (!vcycle_fusable(lv, L, n_split, 1, 0, n_smooth)) return hipErrorInvalidValue;
@@ -95,12 +103,18 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.tile0 = fa >> TL;
     const unsigned grid = fb > fa ? (unsigned)((fb - fa + tm) >> TL) : 0u;
     if (grid == 0) return hipSuccess;
-    if (xc) {
+    if (xc && part == 6) {
         A.ring = xc->ring;
         A.ring_stride = xc->ring_stride;
         A.xc_done = xc->xc_done;
         A.xc_sig = xc->xc_sig;
         A.xc_grid = grid;
+    } else if (xc) {   // the early exchange: the map covers the grid's tiles (tile0 = 0)
+        if (A.tile0 != 0) return hipErrorInvalidValue;
+        A.tile_map = xc->tile_map;
+        A.xe_done = xc->xe_done;
+        A.xe_n = xc->xe_n;
+        A.xc_sig = xc->xc_sig;
     }
     // diagnostics: PAMG_VCYCLE_STAMPS=<file> appends every launch's phase timeline
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_VCYCLE_STAMPS") : nullptr;
@@ -170,9 +184,32 @@ hipError_t launch_vcycle_fine(hipStream_t s, const Level *lv, int L, int U, int 
 
 hipError_t launch_vcycle_resident(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,
                                   int n_coarse, double rdt, double *tov, double *tovo, double *send1, double *rhsn2,
-                                  int keep, bool rhsf, double *send_b, int cycles, int steps) {
+                                  int keep, bool rhsf, double *send_b, int cycles, int steps, const EarlyXc *xe) {
+    VArgs X{};
+    if (xe) {
+        if (rhsf || steps != 1) return hipErrorInvalidValue;
+        X.tile_map = xe->tile_map;
+        X.xe_done = xe->done;
+        X.xe_n = xe->target;
+        X.xc_sig = xe->sig;
+    }
     return launch_part(s, lv, L, U, n_split, n_smooth, n_coarse, rdt, tov, tovo, send1, rhsn2, rhsf ? 5 : 4, keep, 0, -1,
-                       send_b, cycles, steps);
+                       send_b, cycles, steps, xe ? &X : nullptr);
+}
+
+// the level-1 tiles of the resident launch and whether each holds a face whose neighbour is on another
+// rank (tile_remote's test on the host, from the level's face records)
+void vcycle_remote_tiles(const Level &L1, int U, int n_split, std::vector<char> &remote) {
+    const int TL = fine_tl(n_split);
+    const int64_t n1 = (int64_t)U << (2 * n_split), nt = (n1 + (1ll << TL) - 1) >> TL;
+    remote.assign((size_t)nt, 0);
+    for (int64_t b = 0; b < nt; ++b) {
+        int64_t u0 = (b << TL) >> (2 * n_split), u1 = (((b + 1) << TL) - 1) >> (2 * n_split);
+        if (u1 >= U) u1 = U - 1;
+        for (int64_t u = u0; u <= u1 && !remote[b]; ++u)
+            for (int f = 0; f < 3; ++f)
+                if ((L1.halo.hface[3 * u + f].x & 3) == 2) remote[b] = 1;
+    }
 }
 
 hipError_t launch_vcycle_resident_xc(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth,

@@ -41,6 +41,7 @@
 // by pamg_vcycle.hip)
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdio>
 #include <algorithm>
@@ -95,6 +96,15 @@ struct VArgs {
     unsigned *xc_done;
     unsigned long long *xc_sig;
     unsigned xc_grid;
+    // the resident call with its per-call exchange started early (pamg_api.cpp vcycle_fused): tile_map
+    // (non-null) gives workgroup b the tile tile_map[b] -- the tiles holding a face whose neighbour is on
+    // another rank first, so that they finish in the first round; each such tile counts its end in
+    // *xe_done after its last cycle's send words are drained (written through), and the one whose count
+    // reaches xe_n (the running total, the counter is never reset) adds 1 to *xc_sig: the comm stream's
+    // signal to exchange while the other tiles run
+    const int *tile_map;
+    unsigned *xe_done;
+    unsigned xe_n;
 };
 
 }  // namespace vc
@@ -339,9 +349,10 @@ __device__ __forceinline__ void hs_write(bool uni, const HaloArgs &H, uint32_t u
     if (uni) u = __builtin_amdgcn_readfirstlane(u);
     const int4 r1 = H.hface[3 * u], r2 = H.hface[3 * u + 1], r3 = H.hface[3 * u + 2];
     const int a = h & 1023, b = (h >> 10) & 1023, c = h >> 20;
-    if (a) halo_face<true, false>(H, r1, 1, a, t, t);
-    if (b) halo_face<true, false>(H, r2, 2, b, t, t);
-    if (c) halo_face<true, false>(H, r3, 3, c, t, t);
+    // the send words written through: the early exchange may read them while the launch runs
+    if (a) halo_face<true, false, false, true>(H, r1, 1, a, t, t);
+    if (b) halo_face<true, false, false, true>(H, r2, 2, b, t, t);
+    if (c) halo_face<true, false, false, true>(H, r3, 3, c, t, t);
 }
 
 // the tnew words of one sub-element's remote halo entries (mode 2) into a ring buffer of 3 words
@@ -371,6 +382,19 @@ __device__ __forceinline__ void hs_ring(bool uni, const HaloArgs &H, double *rin
 __device__ __forceinline__ void xc_signal(const VArgs &A, int c) {
     const unsigned old = __hip_atomic_fetch_add(A.xc_done + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old + 1 == A.xc_grid) __hip_atomic_fetch_add(A.xc_sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// a remote tile's end of the call (after the barrier that follows its waves' drained write-through
+// send words): the count that completes the remote tiles raises the comm stream's signal (the form of
+// xc_signal, once per call)
+__device__ __forceinline__ void xe_signal(const VArgs &A) {
+    const unsigned old = __hip_atomic_fetch_add(A.xe_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == A.xe_n) __hip_atomic_fetch_add(A.xc_sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// the tile of this workgroup: the early exchange's order (remote tiles first), else the grid's
+__device__ __forceinline__ int64_t resident_tile(const VArgs &A) {
+    return A.tile_map ? (int64_t)A.tile_map[blockIdx.x] : (int64_t)blockIdx.x + A.tile0;
 }
 
 // XC: does tile tb (T level-1 sub-elements from tb T) hold a face whose neighbour is on another rank?
@@ -1047,8 +1071,9 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
     const int t = threadIdx.x;
     const double rdt = A.rdt;
     const int ns = A.n_smooth, m = A.cycles;
-    const int64_t tb = (int64_t)blockIdx.x + A.tile0;   // tile
-    const bool xr = XC && tile_remote<S, T>(A, tb);
+    const int64_t tb = resident_tile(A);   // tile
+    const bool xe = !XC && A.xe_done != nullptr;   // the per-call exchange starts when the remote tiles end
+    const bool xr = (XC || xe) && tile_remote<S, T>(A, tb);
     const VLevel &V0 = A.lv[0];
     const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo, keepc = A.keep & kKeepCoarse;
     bool v0;
@@ -1231,9 +1256,13 @@ __global__ __launch_bounds__(fine_mt(S), PAMG_RES_WAVES) void k_vc_res(VArgs A, 
         });
         if constexpr (XC && !last)
             if (xr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring words drained
+        if constexpr (last)
+            if (xe && xr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the send words drained
         __syncthreads();
         if constexpr (XC && !last)
             if (t == 0) xc_signal(A, c);
+        if constexpr (last)
+            if (xe && xr && t == 0) xe_signal(A);
         // ---- after the call's last cycle: every coarse owner's RHSN, the restriction of the
         //      finer level's residual of that cycle (the next call's first RHS)
         if (last)
@@ -1317,8 +1346,9 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const double rdt = A.rdt;
     const int ns = A.n_smooth, m = A.cycles;
-    const int64_t tb = (int64_t)blockIdx.x + A.tile0;
-    const bool xr = XC && tile_remote<S, T>(A, tb);
+    const int64_t tb = resident_tile(A);
+    const bool xe = !XC && A.xe_done != nullptr;   // the per-call exchange starts when the remote tiles end
+    const bool xr = (XC || xe) && tile_remote<S, T>(A, tb);
     const bool keep1 = A.keep & kKeepL1, keeph = A.keep & kKeepHalo, keepc = A.keep & kKeepCoarse;
     const int total = A.steps * m;
     // the restrictor (:336): the RHS of coarse sub-element i of level l from the means of its
@@ -1474,6 +1504,8 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
             __syncthreads();
             if constexpr (XC && !last)
                 if (lane_id() == 0) xc_signal(A, c);
+            if constexpr (last)   // behind the barrier the level-1 waves passed with their send words drained
+                if (xe && xr && lane_id() == 0) xe_signal(A);
             if (last) {
                 l2_rhsn(std::integral_constant<int, 2>{}, c, i2, g2, v2);
                 static_for<2, C>([&](auto lc) {
@@ -1615,6 +1647,8 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
                 if constexpr (N == 2) l2_legs(std::integral_constant<int, 1>{}, lastc, c, gb, xs, bs, gc, vc);
                 if constexpr (XC && !last)
                     if (xr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring words drained
+                if constexpr (last)
+                    if (xe && xr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the send words drained
                 __syncthreads();
                 if constexpr (N == 2 && last) l2_rhsn(std::integral_constant<int, 1>{}, c, gb, gc, vc);
             };
@@ -1884,20 +1918,33 @@ __global__ __launch_bounds__(512, PAMG_CORR_WAVES) void k_vc_corr(VArgs A, const
     else role(std::integral_constant<int, 0>{});
 }
 
+// a resident launch (one kernel per pamg_vcycle call): with the caller's timing events set (launch_events),
+// through hipExtLaunchKernel -- the dispatch packet records them around the kernel
+template <class K>
+void launch_resident_kernel(K k, unsigned grid, unsigned block, hipStream_t s, const VArgs &A) {
+    LaunchEvents &E = launch_events();
+    if (E.a && E.b) {
+        hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, E.a, E.b, 0u, A, A.lv[0].stc, A.lv[1].stc,
+                              A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+        E.used = true;
+        E.a = E.b = nullptr;
+    } else {
+        hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, A, A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc,
+                           A.lv[4].stc);
+    }
+}
+
 // part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
 template <int S, int L, class ST, bool W8>
 hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     if constexpr (std::is_same<ST, StcR>::value) {   // Richardson: the resident call only (k_vc_res)
         if constexpr (L >= 2 && fine_np(S) == 2) {
             if (part == 6)
-                hipLaunchKernelGGL((k_vc_res<S, L, ST, false, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A,
-                                   A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_res<S, L, ST, false, true>, grid, Geo<S, L>::MT, s, A);
             else if (part == 5)
-                hipLaunchKernelGGL((k_vc_res<S, L, ST, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
-                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_res<S, L, ST, true>, grid, Geo<S, L>::MT, s, A);
             else if (part == 4)
-                hipLaunchKernelGGL((k_vc_res<S, L, ST, false>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
-                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_res<S, L, ST, false>, grid, Geo<S, L>::MT, s, A);
             else
                 return hipErrorInvalidValue;
             return hipGetLastError();
@@ -1923,31 +1970,24 @@ hipError_t launch_sltw(hipStream_t s, const VArgs &A, unsigned grid, int part) {
             return hipErrorInvalidValue;
     } else if (part == 7) {   // the resident corrected call (k_vc_corr)
         if constexpr (L >= 2 && fine_np(S) == 2 && fine_tl(S) == 10)
-            hipLaunchKernelGGL((k_vc_corr<S, L, ST>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc, A.lv[1].stc,
-                               A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+            launch_resident_kernel(k_vc_corr<S, L, ST>, grid, 512, s, A);
         else
             return hipErrorInvalidValue;
     } else if (part >= 4 && part <= 6) {   // the resident call (5: starting a time step; 6: exchange every cycle)
         if constexpr (PAMG_RES_BALANCED && S >= 5 && L >= 3) {
             if (part == 6)
-                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false, true>), dim3(grid), dim3(512), 0, s, A,
-                                   A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_resb<S, L, ST, false, true>, grid, 512, s, A);
             else if (part == 5)
-                hipLaunchKernelGGL((k_vc_resb<S, L, ST, true>), dim3(grid), dim3(512), 0, s, A, A.lv[0].stc,
-                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_resb<S, L, ST, true>, grid, 512, s, A);
             else
-                hipLaunchKernelGGL((k_vc_resb<S, L, ST, false>), dim3(grid), dim3(512), 0, s, A,
-                                   A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_resb<S, L, ST, false>, grid, 512, s, A);
         } else if constexpr (L >= 2 && fine_np(S) == 2) {
             if (part == 6)
-                hipLaunchKernelGGL((k_vc_res<S, L, ST, false, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A,
-                                   A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_res<S, L, ST, false, true>, grid, Geo<S, L>::MT, s, A);
             else if (part == 5)
-                hipLaunchKernelGGL((k_vc_res<S, L, ST, true>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
-                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_res<S, L, ST, true>, grid, Geo<S, L>::MT, s, A);
             else
-                hipLaunchKernelGGL((k_vc_res<S, L, ST, false>), dim3(grid), dim3(Geo<S, L>::MT), 0, s, A, A.lv[0].stc,
-                                   A.lv[1].stc, A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
+                launch_resident_kernel(k_vc_res<S, L, ST, false>, grid, Geo<S, L>::MT, s, A);
         } else {
             return hipErrorInvalidValue;
         }

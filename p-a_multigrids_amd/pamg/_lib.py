@@ -21,7 +21,8 @@ TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN, SOURCE = 0, 1, 2, 3, 4, 5
 (K_SMOOTH_L1, K_SMOOTH, K_RESIDUAL, K_RESTRICT, K_PROLONG, K_RHS, K_HALO, K_SWEEP_BENCH, K_VCYCLE,
  K_VCYCLE_COARSE) = range(10)
 K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle",
-           "vcycle_coarse", "vcycle_pipe", "vcycle_rhsf", "vcycle_res", "vcycle_res_rhsf", "vcycle_corr"]
+           "vcycle_coarse", "vcycle_pipe", "vcycle_rhsf", "vcycle_res", "vcycle_res_rhsf", "vcycle_corr",
+           "halo_early"]
 
 
 class PamgParams(C.Structure):
@@ -104,6 +105,7 @@ def lib():
         "pamg_comm_local_group": (I, [C.POINTER(P), I]),
         "pamg_comm_init_self": (I, [P, C.c_char_p, I, ip]),
         "pamg_comm_info": (I, [P, C.POINTER(I), C.c_char_p, I]),
+        "pamg_early_exchange_times": (I, [P, dp]),
         "pamg_plan_build": (I, [I, dp, ip, ip, ip, I, I, I, I, ip, C.POINTER(P)]),
         "pamg_plan_sizes": (I, [P, ip]),
         "pamg_plan_get": (I, [P] + [C.c_void_p] * 10),

@@ -218,6 +218,17 @@ class SemiImplicitIterative:
         return {0: "none", 1: "rccl", 2: "local"}[rc], v.value, buf.value.decode(errors="replace")
     def synchronize(self): self._call("pamg_synchronize")
 
+    def early_exchange_times(self):
+        """the last call whose per-call exchange started early (timing class halo_early enabled):
+        (exchange start, exchange end, launch end) in us from the launch's start, or None"""
+        t = np.zeros(3)
+        rc = self.L.pamg_early_exchange_times(self.h, t)
+        if rc == -4:   # PAMG_ERR_STATE: none recorded
+            return None
+        if rc < 0:
+            _check("pamg_early_exchange_times", rc, self.h)
+        return tuple(float(v) for v in t)
+
     # ---- measurement ------------------------------------------------------
     def timing_enable(self, mask): self._call("pamg_timing_enable", mask)
     def timing_reset(self): self._call("pamg_timing_reset")

@@ -175,3 +175,41 @@ def test_comm_info_names_the_rccl_library():
     s = pamg.SemiImplicitIterative(m, 2, 2)
     kind, version, path = s.comm_info()
     assert kind == "none" and version >= 20000 and "rccl" in os.path.basename(path)
+
+
+XE_CASES = [
+    # mesh, n_split, levels, parts, owner, drive
+    ("untitled8192.msh", 5, 3, 8, "strip", "vcycle20"),   # config 4's shape: k_vc_resb
+    ("untitled8192.msh", 5, 3, 8, "block", "calls"),
+    ("untitled8192.msh", 3, 3, 4, "block", "calls"),      # k_vc_res (16 un_eles per tile)
+    ("irregular.msh", 6, 3, 8, "strip", "vcycle20"),      # config 5: tiles are quarters of an un_ele
+]
+
+
+@pytest.mark.parametrize("mesh,S,L,nparts,kind,how", XE_CASES)
+def test_local_group_early_per_call_exchange(mesh, S, L, nparts, kind, how):
+    """halo_exchange = 0 on a partition: the resident call's per-call exchange starts early -- the tiles
+    holding a remote face run first (the launch's tile order), count their ends once their send words are
+    written through, and the last raises the device signal on which the comm stream starts the exchange
+    while the other tiles run (pamg_api.cpp vcycle_fused). One early exchange per
+    vcycle call; the state is the single domain's bit for bit."""
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    full = pamg.SemiImplicitIterative(m, S, L, fused=0, arith=1)
+    drive(full, how)
+    owner = owners(m, kind, nparts)
+    parts = [pamg.SemiImplicitIterative(m, S, L, comm=(nparts, r, None, owner), fused=3, arith=1, halo_exchange=0)
+             for r in range(nparts)]
+    local_group(parts)
+    for p in parts:
+        p.timing_enable(0xFFFF)
+        p.timing_reset()
+    run_ranks(parts, lambda p: drive(p, how))
+    check_parts(full, parts, owner)
+    calls = 1 if how == "vcycle20" else 3
+    for p in parts:
+        tm = p.timing()
+        assert tm["vcycle_res"]["issued"] == calls, tm["vcycle_res"]
+        assert tm["halo_early"]["issued"] == calls, tm["halo_early"]
+        t = p.early_exchange_times()
+        assert t is not None and 0 <= t[0] <= t[1] and t[2] > 0, t
+        p.close()

@@ -64,3 +64,29 @@ def test_rccl_self_peer_face_operator():
         x.begin_timestep()
         x.vcycle(2)
     _same(full, s)
+
+
+def test_rccl_self_peer_early_exchange_is_hidden():
+    """The resident call's per-call exchange starts on the device signal raised when the tiles with remote
+    faces (scheduled first) have finished, and runs through RCCL while the other tiles compute: one early
+    exchange per call, the state bitwise the single domain's, and the exchange (ncclSend / ncclRecv and the
+    unpack) ends before the resident launch does. The shape of one rank of config 4 on 8 GPUs: 1,024 un_eles
+    at n_split 5 (a 32 x 16 x 2 strip, 1.33 rounds of resident workgroups), one cut of 16 faces' rows; on the
+    full mesh's 10.7 full rounds the exchange's kernels only find free CUs in the launch's tail."""
+    mesh = pamg.Mesh.strip(32, 16)
+    full, s = _pair(mesh, 5, 3, 2, n_smooth=4, solver=3, arith=1)
+    for x in (full, s):
+        x.begin_timestep()
+        x.vcycle(5)
+    s.timing_enable(0xFFFF)
+    s.timing_reset()
+    for x in (full, s):
+        x.vcycle(20)
+    _same(full, s)
+    tm = s.timing()
+    assert tm["vcycle_res"]["issued"] == 1 and tm["halo_early"]["issued"] == 1, tm
+    t0, t1, t2 = s.early_exchange_times()
+    print(f"early exchange: start {t0:.1f} us, end {t1:.1f} us, launch end {t2:.1f} us")
+    assert 0 <= t0 <= t1 < t2, (t0, t1, t2)
+    s.close()
+    full.close()
