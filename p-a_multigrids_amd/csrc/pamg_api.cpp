@@ -384,6 +384,13 @@ int xe_setup(pamg_handle *h) {
     return PAMG_OK;
 }
 
+// PAMG_PITCH_PAD=<doubles> (A/B runs, rounded to 64): a gap between the state planes of a level, so that
+// the planes of one sub-element are not a power-of-two distance apart (64 MiB at n_split = 5)
+int64_t plane_pad() {
+    static const int64_t pad = getenv("PAMG_PITCH_PAD") ? (std::max(0L, atol(getenv("PAMG_PITCH_PAD"))) + 63) / 64 * 64 : 0;
+    return pad;
+}
+
 bool early_xc_enabled() {
     static const bool on = !(getenv("PAMG_EARLY_XC") && atoi(getenv("PAMG_EARLY_XC")) == 0);
     return on;
@@ -1905,7 +1912,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         L.richardson = h->p.solver == 2;
         L.nsub = 1 << (2 * L.isplit);
         L.N = (int64_t)L.nsub * Ul;
-        L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64);
+        L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64) + plane_pad();
         double *base = nullptr;
         // level 1: the source term s' (SRC); level 2: RHSN_alt for the concurrent fused cycle
         const size_t planes = (l <= 2) ? 21 : 18;
@@ -2379,7 +2386,7 @@ int pamg_sweep_bench(pamg_handle *h, int sweeps, int assembled, double *ms_avg, 
     const double rdt = 1 / h->p.dt;
     CHK(ensure_scratch(h, 3 * (size_t)L.pitch * sizeof(double)));
     if (assembled && !L.blocks) {
-        CHK(dev_alloc(h, &L.blocks, 12 * (size_t)L.pitch));
+        CHK(dev_alloc(h, &L.blocks, asm_blocks_doubles(L)));
         HIPCHK(h, launch_build_blocks(h->stream, L, rdt));
     }
     const double bytes = assembled ? 168.0 * (double)L.N : 72.0 * (double)L.N + 168.0 * h->U;
@@ -2409,7 +2416,7 @@ int pamg_sweep_bench_output(pamg_handle *h, int assembled, double *host) {
     // the sweep's output planes, then its (3, nsub, U) image
     CHK(ensure_scratch(h, 6 * (size_t)L.pitch * sizeof(double)));
     if (assembled && !L.blocks) {
-        CHK(dev_alloc(h, &L.blocks, 12 * (size_t)L.pitch));
+        CHK(dev_alloc(h, &L.blocks, asm_blocks_doubles(L)));
         HIPCHK(h, launch_build_blocks(h->stream, L, rdt));
     }
     if (assembled) HIPCHK(h, launch_sweep_assembled(h->stream, L, h->scratch, rdt));

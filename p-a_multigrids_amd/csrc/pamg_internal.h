@@ -370,6 +370,7 @@ hipError_t launch_block_ops(hipStream_t s, const Level &L, int U, double rdt, do
 hipError_t launch_block_solve(hipStream_t s, const Level &L, const double *Ainv);
 hipError_t launch_to_aos(hipStream_t s, const Level &L, const double *soa, double *aos);
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt);
+size_t asm_blocks_doubles(const Level &L);   // the size of Level::blocks (launch_build_blocks' layout)
 // face-coupled operator (pamg_face.hip): the halo words of level L from its tnew (copy: tnew :=
 // tnew_nonlin first, the sweep start :550); one sweep (mode 0 up sub-elements, 1 down ones --
 // red-black Gauss-Seidel in place on tnew_nonlin -- 2 Jacobi from tnew); the residual A tnew - RHS

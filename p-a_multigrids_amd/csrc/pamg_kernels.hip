@@ -462,28 +462,37 @@ __global__ __launch_bounds__(kBlock) void k_to_aos(const double *__restrict__ so
 // (3 planes). Traffic per sub-element: x 24 + b 24 + out 24 + A 72 + w 24 = 168 B
 // (SURVEY.md 8d). The sweep is the contracted arithmetic of arith = 1 (one fma chain
 // per row, pamg_device.h StcF): bitwise the oracle's orc_sweep_once(arith = 1).
+// Layout of the assembled blocks (PAMG_ASM_LAYOUT, A/B runs; asm_layout below):
+//   0  twelve SoA planes (blk[q pitch + s]): 18 load streams + 3 store streams a launch, the planes N
+//      doubles (64 MiB at n_split = 5) apart -- 0.63-0.69 of 8 TB/s across boxes (round 4);
+//   1  tiled: per tile of kAsmTile = 128 sub-elements the twelve planes of the tile, one after the other
+//      (blk[(s / 128) 12 128 + q 128 + s % 128]) -- a wave's 64 lanes x 2 sub-elements read each of its
+//      twelve 1 KiB pieces with one 16-byte load per lane, and the wave's block words are ONE contiguous
+//      12 KiB run: 7 streams a launch (x, b and the blocks in, the sweep out) instead of 21.
+// Measured (scripts/asm_probe.py, profiles/r05_e_asm_layouts.txt; 4 layouts x 2 plane gaps, two interleaved
+// rounds, one process each): every variant 0.240-0.259 ms per launch = 5.4-5.9 TB/s, the spread between
+// processes of one variant (their allocations' placement) as large as between variants -- the stream count
+// is not what bounds it; 0.70-0.73 of 8 TB/s is ~93 % of the guide's measured 6.3 TB/s streaming copy.
+// Default 12 (tiled, two tiles per wave: the best mean, 0.246 ms).
+constexpr int kAsmTile = 128;
+__device__ __forceinline__ int64_t asm_index(int layout, int64_t pitch, int q, int64_t s) {
+    return layout == 0 ? q * pitch + s : (s / kAsmTile) * (12 * kAsmTile) + q * kAsmTile + (s % kAsmTile);
+}
+
 __global__ __launch_bounds__(kBlock) void k_build_blocks(const double *__restrict__ stc, double *__restrict__ blk,
-                                                         int64_t pitch, int64_t N, int nsub_log2) {
+                                                         int64_t pitch, int64_t N, int nsub_log2, int layout) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= N) return;
     const double *r = stc + (s >> nsub_log2) * kStcStride;
 #pragma unroll
-    for (int q = 0; q < 9; ++q) blk[q * pitch + s] = r[kStcA + q];
+    for (int q = 0; q < 9; ++q) blk[asm_index(layout, pitch, q, s)] = r[kStcA + q];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) blk[(9 + q) * pitch + s] = r[kStcW + q];
+    for (int q = 0; q < 3; ++q) blk[asm_index(layout, pitch, 9 + q, s)] = r[kStcW + q];
 }
 
-__global__ __launch_bounds__(kBlock) void k_sweep_assembled(const double *__restrict__ x, const double *__restrict__ b,
-                                                            const double *__restrict__ blk, double *__restrict__ out,
-                                                            int64_t pitch, int64_t npairs) {
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (p >= npairs) return;
-    const int64_t s = 2 * p;
-    double2 xv[3], bv[3], a[12];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) { xv[c] = ld2(x + c * pitch + s); bv[c] = ld2(b + c * pitch + s); }
-#pragma unroll
-    for (int q = 0; q < 12; ++q) a[q] = ld2(blk + q * pitch + s);
+// one adjacent pair s, s + 1 (s even) of the sweep from its loaded words
+__device__ __forceinline__ void asm_pair(const double2 xv[3], const double2 bv[3], const double2 a[12],
+                                         double *__restrict__ out, int64_t pitch, int64_t s) {
     StcF S0, S1;
 #pragma unroll
     for (int q = 0; q < 9; ++q) { S0.A[q] = a[q].x; S1.A[q] = a[q].y; }
@@ -495,6 +504,43 @@ __global__ __launch_bounds__(kBlock) void k_sweep_assembled(const double *__rest
     sweep(S1, 0.0, b1, x1);
 #pragma unroll
     for (int c = 0; c < 3; ++c) st2(out + c * pitch + s, make_double2(x0[c], x1[c]));
+}
+
+// LAYOUT 0: a thread per pair. LAYOUT 1: a wave per run of K tiles (K x 128 sub-elements), a lane takes pair
+// `lane` of each tile, every load of the K tiles issued before the first sweep
+template <int LAYOUT, int K>
+__global__ __launch_bounds__(kBlock) void k_sweep_assembled(const double *__restrict__ x, const double *__restrict__ b,
+                                                            const double *__restrict__ blk, double *__restrict__ out,
+                                                            int64_t pitch, int64_t npairs) {
+    if constexpr (LAYOUT == 0) {
+        const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        if (p >= npairs) return;
+        const int64_t s = 2 * p;
+        double2 xv[3], bv[3], a[12];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { xv[c] = ld2(x + c * pitch + s); bv[c] = ld2(b + c * pitch + s); }
+#pragma unroll
+        for (int q = 0; q < 12; ++q) a[q] = ld2(blk + q * pitch + s);
+        asm_pair(xv, bv, a, out, pitch, s);
+    } else {
+        const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+        const int lane = threadIdx.x & 63;
+        double2 xv[K][3], bv[K][3], a[K][12];
+        int64_t sk[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            sk[k] = (w * K + k) * kAsmTile + 2 * lane;
+            if (sk[k] >= 2 * npairs) continue;
+            const double *t = blk + (w * K + k) * (12 * kAsmTile) + 2 * lane;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) a[k][q] = ld2(t + q * kAsmTile);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { xv[k][c] = ld2(x + c * pitch + sk[k]); bv[k][c] = ld2(b + c * pitch + sk[k]); }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (sk[k] < 2 * npairs) asm_pair(xv[k], bv[k], a[k], out, pitch, sk[k]);
+    }
 }
 
 // Matrix-free form of the same sweep (the reference's own structure: one
@@ -829,18 +875,47 @@ hipError_t launch_to_aos(hipStream_t s, const Level &L, const double *soa, doubl
     return hipGetLastError();
 }
 
+// PAMG_ASM_LAYOUT=<layout><K> (A/B runs; read once): the layout of the assembled blocks and, tiled, the
+// tiles per wave
+int asm_layout() {
+    static const int v = getenv("PAMG_ASM_LAYOUT") ? atoi(getenv("PAMG_ASM_LAYOUT")) : 12;
+    return v;
+}
+
+size_t asm_blocks_doubles(const Level &L) {
+    return 12 * (size_t)((L.pitch + kAsmTile - 1) / kAsmTile * kAsmTile);
+}
+
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt) {
     (void)rdt;   // the blocks are the records' kStcA words, assembled with rdt on the host
     hipLaunchKernelGGL(k_build_blocks, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.stc, L.blocks, L.pitch, L.N,
-                       log2i(L.nsub));
+                       log2i(L.nsub), asm_layout() / 10);
     return hipGetLastError();
 }
 
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt) {
     (void)rdt;
+    if (L.N % 2) return hipErrorInvalidValue;
     const int64_t npairs = L.N / 2;
-    hipLaunchKernelGGL(k_sweep_assembled, dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
-                       L.pitch, npairs);
+    const int v = asm_layout();
+    if (v / 10 == 0) {
+        hipLaunchKernelGGL((k_sweep_assembled<0, 1>), dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks,
+                           out, L.pitch, npairs);
+        return hipGetLastError();
+    }
+    // tiled: a wave per K tiles of 128 sub-elements
+    const int K = v % 10;
+    const int64_t ntiles = (L.N + kAsmTile - 1) / kAsmTile, waves = (ntiles + K - 1) / K;
+    const unsigned grid = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
+    switch (K) {
+        case 1: hipLaunchKernelGGL((k_sweep_assembled<1, 1>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
+                                   L.pitch, npairs); break;
+        case 2: hipLaunchKernelGGL((k_sweep_assembled<1, 2>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
+                                   L.pitch, npairs); break;
+        case 4: hipLaunchKernelGGL((k_sweep_assembled<1, 4>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
+                                   L.pitch, npairs); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
