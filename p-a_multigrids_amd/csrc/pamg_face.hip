@@ -632,7 +632,12 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
     double *WD = LDSM + OW;
     auto HI = [&](int snap) { return LDSM + OH + snap * NH; };
     const int t = threadIdx.x;
-    const int64_t u = blockIdx.x, s0 = u * TS;
+    // (Measured, not kept: starting the first round's k-th workgroup of a CU k x 4 / 8 / 12 us late, so that the
+    // co-resident workgroups' load, sweep and store phases fall apart -- the level-1 passes 0.74 -> 0.75 / 0.76 /
+    // 0.80 ms per cycle, profiles/r05_f_face_pp_stagger.txt; a persistent grid looping over tiles spilled 272 B
+    // per lane.) The tile body is a lambda called once: 76 -> 70 VGPRs.
+    auto tile = [&](const int64_t u) {
+    const int64_t s0 = u * TS;
     FaceRec R;
     load_face_rec(stc, fface, fsx, u, R);
     if (t < 24) WD[t] = fface[u * kFaceStride + kFaceWD + t];
@@ -828,6 +833,8 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
         sweep(1);
     }
     if (out_end) store(out_end);
+    };
+    tile((int64_t)blockIdx.x);
 }
 
 // ---- the wavefront call: every sweep of one smoother call on a level too large to stay on-chip
