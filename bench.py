@@ -279,11 +279,12 @@ def measure_workload(pamg, m, S, L, ns, arith, device, cycles=100):
     return out
 
 
-def measure_face(pamg, m, S, L, device, cycles=20):
+def measure_face(pamg, m, S, L, device, cycles=20, cycle=0):
     """the face-coupled operator (op = 1) on mesh m: V-cycles/s of the reference's
-    cycle (n_smooth 4, red-black GS) and, from an evented pass, each kernel class's time and
-    algorithmic bytes per cycle; the level-1 sweeps (HBM-bound) against the HBM roofline"""
-    s = pamg.SemiImplicitIterative(m, S, L, n_smooth=4, solver=3, device=device, op=1, cycle=0)
+    cycle (cycle = 0) or the corrected one (cycle = 1; n_smooth 4, red-black GS) and, from an evented
+    pass, each kernel class's time and algorithmic bytes per cycle; the level-1 sweeps (HBM-bound)
+    against the HBM roofline"""
+    s = pamg.SemiImplicitIterative(m, S, L, n_smooth=4, solver=3, device=device, op=1, cycle=cycle)
     s.begin_timestep()
     s.vcycle(3)
     s.synchronize()
@@ -304,10 +305,11 @@ def measure_face(pamg, m, S, L, device, cycles=20):
     k1 = tm["smooth_L1"]
     if k1["launches"] and k1["ms"] > 0:
         # level 1's launches: one sweep each, or two (k_face_pp, the default); a cycle executes 2 (n_smooth - 1)
-        # level-1 sweeps (a smoother call's last sweep only in the call's last cycle)
+        # level-1 sweeps (a smoother call's last sweep only in the call's last cycle), the
+        # corrected cycle 2 n_smooth
         gbs = k1["bytes"] / (k1["ms"] * 1e-3) / 1e9
         lpc = k1["launches"] / cycles
-        spl = 2 * (4 - 1) / lpc
+        spl = (2 * 4 if cycle else 2 * (4 - 1)) / lpc
         out["roofline_level1_launch"] = dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                                              frac=round(gbs / HBM_PEAK_GBS, 4), sweeps_per_launch=round(spl, 2),
                                              ms_per_launch=round(k1["ms"] / k1["launches"], 4),
@@ -612,6 +614,8 @@ def main():
             extra[tag] = measure_workload(pamg, m_, S_, a.levels, a.nsmooth, a.arith, device)
         # the face-coupled operator on the benchmarked mesh, n_split 5, 3 levels
         extra["op1"] = measure_face(pamg, mesh, a.nsplit, 3, device)
+        # and the corrected cycle on it (cycle = 1: levels 1-2 in two-sweep passes, the coarsest level's chain)
+        extra["op1_cycle1"] = measure_face(pamg, mesh, a.nsplit, 3, device, cycle=1)
         extra["cycle1"] = measure_corrected(pamg, mesh, a.nsplit, a.levels, a.nsmooth, a.arith, device)
     if world > 1 and not a.no_extra:
         # the other exchange mode on the same partition (timed region the same shape): halo words

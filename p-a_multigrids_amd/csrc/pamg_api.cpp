@@ -1074,16 +1074,18 @@ bool face_pp_ok(pamg_handle *h, int l) {
            (h->p.solver != 3 || L.words_up);
 }
 
-struct PPPass { int K, res; double *in, *pre, *mid, *end; };
+struct PPPass { int K, res; double *in, *pre, *mid, *end, *end2; };
 
 // the passes of a stream of `total` sweeps from src with get_residual after sweep r for each r in res_at
 // (0 < r < total), ending with the final stores fin (1: tnew = the iterate before the last sweep,
-// tnew_nonlin = after it; 2: tnew = the last result, the dead sweep's :550)
+// tnew_nonlin = after it; 2: tnew = the last result, the dead sweep's :550; 3: tnew and tnew_nonlin both
+// the last result, the corrected cycle's smoother call)
 int face_pp_plan(pamg_handle *h, int l, int total, double *src, const std::vector<int> &res_at, int fin,
                  std::vector<PPPass> &plan) {
     Level &L = h->lv[l];
     plan.clear();
-    for (int s = 0; s < total; s += 2) plan.push_back(PPPass{std::min(2, total - s), 0, nullptr, nullptr, nullptr, nullptr});
+    for (int s = 0; s < total; s += 2)
+        plan.push_back(PPPass{std::min(2, total - s), 0, nullptr, nullptr, nullptr, nullptr, nullptr});
     for (int r : res_at) {
         if (r <= 0 || r >= total) { h->err = "internal: face stream residual point"; return PAMG_ERR_STATE; }
         PPPass &q = plan[r / 2];
@@ -1097,6 +1099,7 @@ int face_pp_plan(pamg_handle *h, int l, int total, double *src, const std::vecto
         z.end = L.TNN;
     } else {
         z.end = L.T;
+        if (fin == 3) z.end2 = L.TNN;
     }
     double *const buf[3] = {L.RHSN, L.TNN, L.T};
     // inputs, last to first: the last pass reads RHSN (neither of its outputs); every other pass writes the
@@ -1110,7 +1113,8 @@ int face_pp_plan(pamg_handle *h, int l, int total, double *src, const std::vecto
     for (int p = 0; p < P; ++p) {
         plan[p].in = in[p];
         if (p + 1 < P) plan[p].end = in[p + 1];
-        if (plan[p].in == plan[p].end || plan[p].in == plan[p].mid || plan[p].in == plan[p].pre) {
+        if (plan[p].in == plan[p].end || plan[p].in == plan[p].mid || plan[p].in == plan[p].pre ||
+            plan[p].in == plan[p].end2) {
             h->err = "internal: a face pass writes its own input";
             return PAMG_ERR_STATE;
         }
@@ -1123,11 +1127,12 @@ int face_pp_emit(pamg_handle *h, int l, const PPPass &q) {
     const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
     // iterate and RHS in, the outputs and the residual out (the halo gathers of the neighbours' boundary
     // sub-elements are overhead, not counted)
-    const double by = (48.0 + 24.0 * ((q.pre != nullptr) + (q.mid != nullptr) + (q.end != nullptr) + (q.res != 0))) *
-                      (double)L.N + 168.0 * h->U;
+    const double by = (48.0 + 24.0 * ((q.pre != nullptr) + (q.mid != nullptr) + (q.end != nullptr) + (q.end2 != nullptr) +
+                                      (q.res != 0))) * (double)L.N + 168.0 * h->U;
     if (q.res) h->rhsn_valid = false;
     Span sp(h, kid, by);
-    HIPCHK(h, launch_face_pp(h->stream, L, q.K, q.in, q.pre, q.mid, q.end, h->p.solver == 3, l == 1, 1 / h->p.dt, q.res));
+    HIPCHK(h, launch_face_pp(h->stream, L, q.K, q.in, q.pre, q.mid, q.end, h->p.solver == 3, l == 1, 1 / h->p.dt, q.res,
+                             q.end2));
     return PAMG_OK;
 }
 
@@ -1271,6 +1276,70 @@ int vcycle_corrected(pamg_handle *h) {
     if (L > 1) CHK(residual_corrected(h, 1));   // the fine residual after the cycle
     h->tnn_level = 1;
     return PAMG_OK;
+}
+
+// The corrected cycle on the face-coupled operator (op = 1, cycle = 1) with the smoother calls of the levels
+// below the coarsest as two-sweep passes (k_face_pp; single domain, face_pp_ok) instead of one launch per
+// sweep and a copy: each call runs its n_smooth sweeps from tnew in passes whose last one stores the result
+// as tnew (and, in the call's last cycle, as tnew_nonlin too -- inside the call tnew_nonlin is overwritten
+// before any read); the coarsest level's calls stay one chain launch (face_call). The passes do not publish
+// halo words between sweeps (they read the neighbours' iterate itself), and no operation of the cycle reads
+// t_overlap but the residuals, each of which refreshes the words from its level's tnew first (face_residual)
+// -- as does the per-step sequence's last operation, the fine residual after the cycle, which only the
+// call's last cycle runs here (the next cycle's first residual rewrites it unread, and its words). Every
+// sub-element's arithmetic is face_apply's: the state after the call is bitwise vcycle_corrected's
+// (tests/test_face_operator.py). PAMG_FACE_CORR_PP=0 keeps the per-step sequence (A/B).
+bool face_corrected_pp_ok(pamg_handle *h) {
+    const char *ev = getenv("PAMG_FACE_CORR_PP");   // read per call: tests switch it within a process
+    const bool off = ev && atoi(ev) == 0;
+    if (off || !(h->p.op == 1 && h->p.cycle == 1 && h->p.fused && h->p.coarse_solver == 0 && h->p.n_smooth >= 3 &&
+                 h->p.multi_levels >= 2))
+        return false;
+    for (int l = 1; l < h->p.multi_levels; ++l)
+        if (face_pp_ok(h, l)) return true;
+    return false;
+}
+
+// one smoother call of the corrected cycle on level l < L: tnew := the result of n_smooth sweeps from tnew
+int face_corr_call(pamg_handle *h, int l, bool last) {
+    const int ns = h->p.n_smooth;
+    if (!face_pp_ok(h, l)) {
+        CHK(smooth_to_tnew(h, l, ns));
+        return PAMG_OK;
+    }
+    h->tnn_level = l;
+    h->overlap_static_l1 = false;
+    std::vector<PPPass> plan;
+    CHK(face_pp_plan(h, l, ns, h->lv[l].T, {}, last ? 3 : 2, plan));
+    for (const PPPass &q : plan) CHK(face_pp_emit(h, l, q));
+    return PAMG_OK;
+}
+
+int vcycle_corrected_face_pp(pamg_handle *h, int n) {
+    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    h->overlap_static_l1 = false;
+    for (int c = 0; c < n; ++c) {
+        const bool last = c + 1 == n;
+        for (int l = 1; l < L; ++l) {
+            if (l > 1) HIPCHK(h, hipMemsetAsync(h->lv[l].T, 0, 3 * (size_t)h->lv[l].pitch * sizeof(double), h->stream));
+            CHK(face_corr_call(h, l, last));
+            CHK(residual_corrected(h, l));
+            CHK(restrict_(h, l));
+        }
+        Level &C = h->lv[L];
+        HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));   // from zero
+        CHK(smooth_to_tnew(h, L, ns * h->p.n_coarse));
+        for (int l = L - 1; l >= 1; --l) {
+            {
+                Span sp(h, PAMG_K_PROLONG, 216.0 * (double)h->lv[l + 1].N);
+                HIPCHK(h, launch_interp_add(h->stream, h->lv[l], h->lv[l + 1]));
+            }
+            CHK(face_corr_call(h, l, last));
+        }
+        if (last) CHK(residual_corrected(h, 1));   // the fine residual after the cycle
+    }
+    h->tnn_level = 1;
+    return face_chain_check(h);
 }
 
 // the corrected cycle as one resident launch per pamg_vcycle call (pamg_vcycle_impl.h k_vc_corr): the
@@ -2220,6 +2289,7 @@ int vcycle(pamg_handle *h, int n, bool dead_after) {
     CHK(check_level(h, 1));
     if (h->p.cycle == 1) {
         if (corrected_resident_ok(h)) return vcycle_corrected_resident(h, n);
+        if (face_corrected_pp_ok(h)) return vcycle_corrected_face_pp(h, n);
         for (int c = 0; c < n; ++c) CHK(vcycle_corrected(h));
         return PAMG_OK;
     }

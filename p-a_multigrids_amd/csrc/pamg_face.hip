@@ -591,7 +591,7 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 // the same operands as v's own workgroup: bitwise the per-sweep launches (tests/test_face_operator.py).
 // A pass: K = 1 or 2 sweeps; res 1: get_residual of the start iterate, 2: of the iterate after the first
 // sweep (the residual point of a smoother stream, with the snapshot the second sweep reads); outputs:
-// out_pre the start iterate, out_mid the iterate after sweep 1 (K = 2), out_end the iterate after the
+// out_pre the start iterate, out_mid the iterate after sweep 1 (K = 2), out_end (and out_end2) the iterate after the
 // last sweep (none of them aliases A).
 // gtab (U x 3 x m, Level::gtab): the gather entry of every halo slot (see the prologue).
 #ifndef PAMG_FACE_PP_WAVES
@@ -611,7 +611,8 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 // passes 0.85 vs 0.71 ms per cycle at seven waves per SIMD, profiles/r04_k_face_pp_nt.txt), so it keeps 512
 template <int TS, int NT, bool RB, int K>
 __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
-    const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, const double *__restrict__ RHS,
+    const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, double *out_end2,
+    const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
     const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
     const double2 *__restrict__ bcv, const int *__restrict__ cpos, int nup, int64_t pitch, int level1, double rdt,
@@ -833,6 +834,7 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
         sweep(1);
     }
     if (out_end) store(out_end);
+    if (out_end2) store(out_end2);   // the corrected cycle's smoother call: tnew and tnew_nonlin both its result
     };
     tile((int64_t)blockIdx.x);
 }
@@ -1804,10 +1806,11 @@ static hipError_t launch_coresident(const void *f, int grid, int nt, void **args
 
 // k_face_pp: K sweeps of a whole-un_ele-tile level in one launch (face_tile_shape; single domain)
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
-                          double *out_end, bool rb, bool level1, double rdt, int res) {
+                          double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2) {
     if (L.N == 0) return hipSuccess;
     const int m = L.nsub == 256 ? 16 : L.nsub == 1024 ? 32 : 64;
     if (!face_tile_shape(L) || !L.fnb || !L.gtab || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)) ||
+        (out_end2 && (out_end2 == in || !out_end)) ||
         (rb && (!L.cpos || L.nup != m * (m + 1) / 2)))
         return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
@@ -1815,7 +1818,8 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
     const int l1 = level1 ? 1 : 0;
     double *R = res ? L.RES : nullptr;
 #define PAMG_FPP(TS, NT, RB_, K_)                                                                                    \
-    hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, L.RHS, L.stc,  \
+    hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, out_end2, L.RHS, \
+                       L.stc,                                                                                         \
                        L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.cpos, L.nup, L.pitch, l1, rdt, res, R)
 #define PAMG_FPPK(TS, NT)                                          \
     if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \

@@ -398,7 +398,7 @@ bool face_tile_shape(const Level &L);
 // iterate / the iterate after the first sweep; out_pre / out_mid / out_end (any may be null, none `in`):
 // the start iterate, the iterate after sweep 1, after the last sweep
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
-                          double *out_end, bool rb, bool level1, double rdt, int res);
+                          double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2 = nullptr);
 // the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of
 // the call's `total` sweeps in one launch, the iterate in LDS, the halo handed over between
 // workgroups inside the launch; store 1: tnew (the last sweep's start) and tnew_nonlin, 2: tnew :=

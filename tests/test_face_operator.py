@@ -285,3 +285,39 @@ def test_face_chain_per_wave_equals_workgroup_chain(mesh, S, L, ns, splits, monk
         assert_identical(gs, rs)
         for x, y in zip(gov, rov):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,S,L,solver,ns,splits", [
+    ("untitled8192.msh", 5, 3, 3, 4, ([3], [1, 2])), ("untitled8192.msh", 4, 3, 1, 3, ([2],)),
+    ("irregular.msh", 6, 3, 3, 3, ([2, 1],)), ("900_ele.msh", 5, 2, 3, 4, ([2],))])
+def test_face_corrected_cycle_passes_equal_per_step(mesh, S, L, solver, ns, splits, monkeypatch):
+    """The corrected cycle on the face operator with its smoother calls below the coarsest level as two-sweep
+    passes (k_face_pp, the call's result stored as tnew -- and as tnew_nonlin in the call's last cycle -- and
+    the fine residual after the cycle only in the call's last cycle) leaves the per-step sequence's state bit
+    for bit (bench.py's extra.op1_cycle1 configuration first), and its level-1 calls are the passes."""
+    import pamg
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+
+    def run(split):
+        g = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, op=1, cycle=1)
+        g.timing_enable(1)   # PAMG_K_SMOOTH_L1
+        g.timing_reset()
+        for n in split:
+            g.begin_timestep()
+            g.vcycle(n)
+        st, ov = g.state(), g.overlap()
+        issued = g.timing()["smooth_L1"]["issued"]
+        g.close()
+        return st, ov, issued
+
+    for split in splits:
+        monkeypatch.setenv("PAMG_FACE_CORR_PP", "0")
+        rs, rov, _ = run(split)
+        monkeypatch.setenv("PAMG_FACE_CORR_PP", "1")
+        gs, gov, issued = run(split)
+        assert_identical(gs, rs)
+        for x, y in zip(gov, rov):
+            np.testing.assert_array_equal(x, y)
+        if 4 ** S == 1024 or 4 ** S == 256:   # level 1 streams: two calls per cycle, ceil(ns / 2) passes each
+            assert issued == sum(split) * 2 * ((ns + 1) // 2), issued
