@@ -66,7 +66,10 @@ extern "C" {
 #define PAMG_K_VCYCLE_CORR 14    /* the corrected V-cycle's resident call (cycle = 1): a pamg_vcycle call in one launch */
 #define PAMG_K_HALO_EARLY 15     /* the resident call's per-call exchange, started on a device signal once the tiles
                                     with remote faces have finished (comm stream; overlapped with the launch) */
-#define PAMG_K_COUNT 16
+#define PAMG_K_FACE_FALLBACK 16  /* face-operator smoother calls whose persistent chain launch found its workgroups not
+                                    all resident and left the state untouched: run with one launch per sweep instead
+                                    (counted in pamg_timing_issued whatever the timing mask) */
+#define PAMG_K_COUNT 17
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;

@@ -637,6 +637,14 @@ int face_wave_grid_for(pamg_handle *h, int l, int run) {
     return g;
 }
 
+// PAMG_CHAIN_GUARD=0 (A/B): the chain's workgroups start without the co-residency guard and the host does
+// not wait for each chain launch (a launch that is not co-resident then gives up on its bounded spins and the
+// call fails, face_chain_check)
+bool chain_guard_on() {
+    const char *e = getenv("PAMG_CHAIN_GUARD");   // read per call: tests switch it within a process
+    return !(e && atoi(e) == 0);
+}
+
 // the give-up word of the chain's and the wavefront's bounded spins: a call that hit it failed, and
 // the state it left was computed from halo words that had not all arrived -- the handle's fields are
 // invalid after the error (set them again, or start a new time step from a known tnew). Checked only
@@ -730,13 +738,25 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
         }
         const unsigned f0 = L.chain_epoch;
         L.chain_epoch += (unsigned)run + 1;
-        // the state crosses HBM once per call: tnew_nonlin and RHS in, tnew (+ tnew_nonlin) out
-        Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
-        h->chain_pending = true;
-        HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags, L.chain_nb_off,
-                                    L.chain_nb_list, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
-                                    l == 1, rdt, h->p.omega, h->slots, src_is_T, f0));
-        return PAMG_OK;
+        const bool guard = chain_guard_on();
+        {
+            // the state crosses HBM once per call: tnew_nonlin and RHS in, tnew (+ tnew_nonlin) out
+            Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
+            h->chain_pending = true;
+            HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags,
+                                        L.chain_nb_off, L.chain_nb_list, h->chain_tmo, run, sweeps, dead_last ? 2 : 1,
+                                        h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, src_is_T, f0, guard ? 1 : 0));
+        }
+        // fail safe: a launch whose workgroups were not all resident (a CU-masked stream, another stream's or
+        // process's kernels on the CUs) aborted before touching anything -- the call runs below, one launch
+        // per sweep, from the same input and halo snapshot (the host waits for the chain to know)
+        if (!guard) return PAMG_OK;
+        if (!h->guard_host) HIPCHK(h, hipHostMalloc((void **)&h->guard_host, sizeof(unsigned)));
+        HIPCHK(h, hipMemcpyAsync(h->guard_host, h->chain_tmo + 3, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+        CHK(sync_stream(h, h->stream));
+        if (*h->guard_host == 0) return PAMG_OK;
+        HIPCHK(h, hipMemsetAsync(h->chain_tmo + 3, 0, sizeof(unsigned), h->stream));
+        h->timing.seq[PAMG_K_FACE_FALLBACK] += 1;
     }
     if (const int g = face_wave_grid_for(h, l, run)) {   // the call in one wavefront launch
         CHK(tags(&g0, &g1, &tag0));
@@ -1784,8 +1804,22 @@ int pamg_create(const pamg_params *p, pamg_handle **out) {
     auto *h = new pamg_handle;
     h->p = *p;
     h->device = p->device;
-    if (hipSetDevice(h->device) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+    // PAMG_STREAM_CU_MASK=<n> | half (tests): the handle's stream runs on the first n CUs only (hipExtStreamCreateWithCUMask)
+    // -- a persistent chain grid sized for every CU is then not co-resident (the chain's fail-safe path)
+    const char *cm = getenv("PAMG_STREAM_CU_MASK");
+    int ncu_mask = cm ? atoi(cm) : 0;
+    if (cm && std::strcmp(cm, "half") == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) n = 0;
+        ncu_mask = n / 2;
+    }
+    auto make_stream = [&](hipStream_t *st) -> bool {
+        if (ncu_mask <= 0) return hipStreamCreateWithFlags(st, hipStreamNonBlocking) == hipSuccess;
+        std::vector<uint32_t> mask((size_t)(ncu_mask + 31) / 32, 0u);
+        for (int c = 0; c < ncu_mask; ++c) mask[c / 32] |= 1u << (c % 32);
+        return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+    };
+    if (hipSetDevice(h->device) != hipSuccess || !make_stream(&h->stream) ||
         hipStreamCreateWithFlags(&h->stream_comm, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_sent[0], hipEventDisableTiming) != hipSuccess ||
@@ -2514,6 +2548,7 @@ int pamg_destroy(pamg_handle *h) {
     free_levels(h);
     dev_free(h->scratch);
     dev_free(h->chain_tmo);
+    if (h->guard_host) (void)hipHostFree(h->guard_host);
     dev_free(h->xc_done);
     dev_free(h->xe_done);
     for (auto e : h->xe_ev)

@@ -1126,6 +1126,59 @@ __global__ __launch_bounds__(NT, TS <= 1024 ? PAMG_WAVE_WAVES : 1) void k_face_w
     }
 }
 
+// The co-residency guard of a chain launch. A chain's workgroups wait on each other's
+// flags, so they must all be resident at once; the launch checks the occupancy bound (launch_coresident),
+// but a CU-masked stream, another stream's kernels or another process can still hold CUs. Before touching any
+// state every workgroup counts its arrival in g[0]; all proceed once all `grid` have arrived, and if one has
+// waited kGuardTicks (200 us) in vain it sets the abort bit in the same word -- by compare-and-swap, only while
+// the count is short, so either every workgroup proceeds or none does -- and counts the abort in *aborted.
+// Late arrivals see the bit and leave. An aborted launch leaves the state untouched: the host reads *aborted
+// and runs the call with one launch per sweep instead (pamg_api.cpp face_call). g[1] counts the workgroups
+// leaving; the last one re-zeroes g[0] and g[1] for the next launch (stream order: nothing else runs on them).
+constexpr unsigned kGuardAbort = 0x80000000u;
+constexpr long long kGuardTicks = 20000;   // wall clock, 100 MHz
+__device__ __forceinline__ bool chain_enter(unsigned *g, unsigned *aborted) {
+    __shared__ int go;
+    if (threadIdx.x == 0) {
+        const unsigned grid = gridDim.x;
+        unsigned v = __hip_atomic_fetch_add((g_u32 *)g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        const long long t0 = wall_clock64();
+        int r = -1;
+        while (r < 0) {
+            if (v & kGuardAbort) {
+                r = 0;
+            } else if ((v & 0xffffu) >= grid) {
+                r = 1;
+            } else if (wall_clock64() - t0 > kGuardTicks) {
+                unsigned want = v;
+                if (__hip_atomic_compare_exchange_strong((g_u32 *)g, &want, v | kGuardAbort, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    __hip_atomic_fetch_add((g_u32 *)aborted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    r = 0;
+                } else {
+                    v = want;   // the word moved: decide on its new value
+                }
+            } else {
+                __builtin_amdgcn_s_sleep(2);
+                v = __hip_atomic_load((g_u32 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        go = r;
+    }
+    __syncthreads();
+    return go != 0;
+}
+__device__ __forceinline__ void chain_leave(unsigned *g) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned e = __hip_atomic_fetch_add((g_u32 *)g + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (e + 1 == gridDim.x) {
+            __hip_atomic_store((g_u32 *)g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((g_u32 *)g + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // LREC: the workgroup's un_eles' operator records (FaceRec + omega / D) sit in LDS for the whole call
 // (at most kChainRec un_eles): the passes read them there instead of fetching them from memory in
 // every pass (the dependent record fetches were most of a sweep's pass time, r03 stamps)
@@ -1176,7 +1229,11 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                                                           int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                           double rdt, double omega, const int *__restrict__ cpos,
                                                           int nup, int nui, int early, unsigned f0, int snap_ok,
-                                                          long long *stamps) {
+                                                          long long *stamps, int guard) {
+    if (guard && !chain_enter(tmo + 1, tmo + 3)) {   // not co-resident: leave the state to the host's fallback
+        chain_leave(tmo + 1);
+        return;
+    }
     constexpr int NT = kChainNT, PER = kChainPer;
     // early (LREC red-black only; the host checked that every halo sub-element is an up one):
     // 1 a sweep's halo words go out right after its up pass, 2 and its flag, 3 as 2 with the up
@@ -1481,6 +1538,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 #pragma unroll
             for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
     }
+    if (guard) chain_leave(tmo + 1);
 }
 
 // ---- the chain with un_eles owned by waves (PAMG_CHAIN_PW, default where it applies): the red-black
@@ -1508,10 +1566,14 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                                                                int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                                double rdt, double omega, const int *__restrict__ cpos,
                                                                int nup, int nui, int early, unsigned f0, int snap_ok,
-                                                               long long *stamps) {
+                                                               long long *stamps, int guard) {
     (void)omega;
     (void)early;
     (void)stamps;
+    if (guard && !chain_enter(tmo + 1, tmo + 3)) {   // not co-resident: leave the state to the host's fallback
+        chain_leave(tmo + 1);
+        return;
+    }
     constexpr int NT = kChainNT;
     __shared__ double X[3][NT * kChainPer];
     __shared__ double HI[kChainHalo];
@@ -1669,6 +1731,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
     for (int j = pa + ln; j < pb; j += 64)   // tnew_nonlin (store 2: tnew, the dead last sweep's :550)
 #pragma unroll
         for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+    if (guard) chain_leave(tmo + 1);
 }
 
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -1852,7 +1915,7 @@ bool face_chain_fits(int nsub, int U, int cus) {
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
                              int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T,
-                             unsigned f0) {
+                             unsigned f0, int guard) {
     if (L.N == 0 || run <= 0) return hipSuccess;
     if (!face_chain_fits(L.nsub, U, cus) || !L.fnb) return hipErrorInvalidValue;
     const int g = std::max(1, std::min(cus, U));
@@ -1892,7 +1955,7 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     int snap_ok = !(snap_env && atoi(snap_env) == 0);
     void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
                     &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &f0,
-                    &snap_ok, &stamps};
+                    &snap_ok, &stamps, &guard};
     // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
     const bool uni = L.nsub >= 64,
                lrec = k <= kChainRec && L.cpos && (int64_t)k * L.nup <= 2 * kChainNT && (int64_t)k * L.ndn <= kChainNT;

@@ -213,6 +213,8 @@ struct pamg_handle {
     // op = 1: the local un_eles' neighbours (0-based local ids, -1: none or another rank), 3 per un_ele
     std::vector<int> neig_local;
     unsigned *chain_tmo = nullptr;   // give-up word of the face chain's / wavefront's bounded spins
+                                     // ([1..2] the chain's co-residency guard, [3] its aborts)
+    unsigned *guard_host = nullptr;  // pinned: the chain's abort count, read after each guarded launch
     bool chain_pending = false;      // a chain or wavefront launch ran since face_chain_check last read it
     // the face operator's wavefront calls (k_face_wave; lazy, single domain): the ticket order (a
     // reverse Cuthill-McKee numbering of neig_local), its band, the neighbours on the device and the
@@ -399,6 +401,8 @@ bool face_tile_shape(const Level &L);
 // the start iterate, the iterate after sweep 1, after the last sweep
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
                           double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2 = nullptr);
+// guard: the workgroups check that they are all resident before touching the state; if not, none does and
+// the launch counts an abort in tmo[3] (tmo[1..2] the guard's own words) -- the host runs the call another way
 // the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of
 // the call's `total` sweeps in one launch, the iterate in LDS, the halo handed over between
 // workgroups inside the launch; store 1: tnew (the last sweep's start) and tnew_nonlin, 2: tnew :=
@@ -419,7 +423,7 @@ int face_chain_per_wg(int nsub, int U, int cus);
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
                              int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T = false,
-                             unsigned f0 = 0);
+                             unsigned f0 = 0, int guard = 0);
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg

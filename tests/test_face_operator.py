@@ -321,3 +321,25 @@ def test_face_corrected_cycle_passes_equal_per_step(mesh, S, L, solver, ns, spli
             np.testing.assert_array_equal(x, y)
         if 4 ** S == 1024 or 4 ** S == 256:   # level 1 streams: two calls per cycle, ceil(ns / 2) passes each
             assert issued == sum(split) * 2 * ((ns + 1) // 2), issued
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cycle", [0, 1])
+def test_face_chain_not_coresident_falls_back_bitwise(cycle, monkeypatch):
+    """Fail-safe co-resident launches: with the handle's stream on half the GPU's CUs
+    (PAMG_STREAM_CU_MASK, hipExtStreamCreateWithCUMask) the coarsest level's persistent chain -- a grid sized
+    for every CU, launched after an occupancy check that cannot see the mask -- cannot be co-resident. Its
+    workgroups find that out before touching anything (the arrival guard) and leave; the host then runs the
+    call with one launch per sweep from the same input. bench.py's extra.op1 configuration: the state equals
+    the oracle's bit for bit, and timing() reports the fallback calls."""
+    monkeypatch.setenv("PAMG_STREAM_CU_MASK", "half")
+    g, o = gpu_pair("untitled8192.msh", 5, 3, 3, cycle, 4)
+    g.timing_reset()
+    drive(g, False, cycle, steps=1, cycles=2)
+    drive(o, True, cycle, steps=1, cycles=2)
+    sg, so = g.state(), o.state()
+    sg["t_overlap"], sg["t_overlap_old"] = g.overlap()
+    so["t_overlap"], so["t_overlap_old"] = o.overlap()
+    assert_identical(sg, so)
+    assert g.timing()["face_fallback"]["issued"] >= 2, g.timing()["face_fallback"]
+    g.close()
