@@ -429,6 +429,11 @@ int join_comm(pamg_handle *h) {
     return PAMG_OK;
 }
 
+// the entry of a call that may read or write what an exchange still in flight touches (the send and receive
+// buffers, t_overlap, t_overlap_old): its work waits for the exchange (the resident call's early exchange is
+// not joined when the call returns, vcycle_fused)
+int settle(pamg_handle *h) { return h->comm ? join_comm(h) : PAMG_OK; }
+
 // RCCL's asynchronous error state (polled at the ends of the hot-path calls): a
 // failed peer or link is reported as PAMG_ERR_COMM instead of a hang in the next exchange
 int comm_error(pamg_handle *h) {
@@ -1599,7 +1604,11 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
                 h->sent_pending[buf] = true;
                 P1.send_cur = buf;
                 h->tnn_level = 1;
-                return join_comm(h);
+                // the join of `stream` behind the exchange is left to the next operation that needs it (settle,
+                // at the entry of every other call; the next resident call waits only for the exchange that
+                // read the send buffer it packs): a barrier packet behind the launch cost ~5-8 us of a 20-cycle
+                // call at an N = 8 rank's shape (profiles/r05_i_xe_join.txt); pamg_synchronize waits for both
+                return PAMG_OK;
             }
         }
         if (rhsf) {
@@ -1940,6 +1949,7 @@ int pamg_comm_info(pamg_handle *h, int *version, char *lib_path, int len) {
 int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, const int *neig, const int *fneig,
                      const int *dir) {
     if (!h || U < 1 || !X || !region || !neig || !fneig || !dir) return PAMG_ERR_ARG;
+    CHK(settle(h));
     HIPCHK(h, hipSetDevice(h->device));
     free_levels(h);
     h->U_global = U;
@@ -2197,6 +2207,7 @@ int pamg_tnn_level(pamg_handle *h) { return h ? h->tnn_level : PAMG_ERR_ARG; }
 
 int pamg_set_state(pamg_handle *h, int level, int what, const double *host) {
     if (!h || !host) return PAMG_ERR_ARG;
+    CHK(settle(h));
     if (what == PAMG_TNEW_NONLIN) { CHK(check_level(h, level)); h->tnn_level = level; }
     CHK(check_level(h, level));
     Level &L = h->lv[level];
@@ -2213,6 +2224,7 @@ int pamg_set_state(pamg_handle *h, int level, int what, const double *host) {
 
 int pamg_get_state(pamg_handle *h, int level, int what, double *host) {
     if (!h || !host) return PAMG_ERR_ARG;
+    CHK(settle(h));
     if (what == PAMG_TNEW_NONLIN) level = h->tnn_level;
     CHK(check_level(h, level));
     Level &L = h->lv[level];
@@ -2227,6 +2239,7 @@ int pamg_get_state(pamg_handle *h, int level, int what, double *host) {
 
 int pamg_get_overlap(pamg_handle *h, double *tov, double *tovo) {
     if (!h || !h->mesh_ready) return PAMG_ERR_STATE;
+    CHK(settle(h));
     const size_t n = (size_t)h->slots * 3 * h->U * sizeof(double);
     if (tov) HIPCHK(h, hipMemcpyAsync(tov, h->tov, n, hipMemcpyDeviceToHost, h->stream));
     if (tovo) HIPCHK(h, hipMemcpyAsync(tovo, h->tovo, n, hipMemcpyDeviceToHost, h->stream));
@@ -2267,11 +2280,13 @@ int begin_timestep(pamg_handle *h, bool tnn_dead, bool told_lazy = false, bool d
 
 int pamg_begin_timestep(pamg_handle *h) {
     if (!h) return PAMG_ERR_ARG;
+    CHK(settle(h));
     return begin_timestep(h, false);
 }
 
 int pamg_copy_to_nonlin(pamg_handle *h, int level) {
     if (!h) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, level));
     Level &L = h->lv[level];
     HIPCHK(h, launch_copy(h->stream, L.T, L.TNN, 3 * L.pitch));
@@ -2281,6 +2296,7 @@ int pamg_copy_to_nonlin(pamg_handle *h, int level) {
 
 int pamg_smoother(pamg_handle *h, int level, int n_calls) {
     if (!h || n_calls < 0) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, level));
     if (h->tnn_level != level) {
         h->err = "smoother: tnew_nonlin holds another level (call pamg_copy_to_nonlin first)";
@@ -2292,6 +2308,7 @@ int pamg_smoother(pamg_handle *h, int level, int n_calls) {
 
 int pamg_sweep(pamg_handle *h, int level, int n_sweeps) {
     if (!h || n_sweeps < 0) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, level));
     if (h->tnn_level != level) {
         h->err = "sweep: tnew_nonlin holds another level (call pamg_copy_to_nonlin first)";
@@ -2303,24 +2320,30 @@ int pamg_sweep(pamg_handle *h, int level, int n_sweeps) {
 
 int pamg_restrictor(pamg_handle *h, int level) {
     if (!h) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, level));
     return restrict_(h, level);
 }
 
 int pamg_get_residual(pamg_handle *h, int level) {
     if (!h) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, level));
     return residual(h, level);
 }
 
 int pamg_prolongator(pamg_handle *h, int level) {
     if (!h) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, level));
     return prolong(h, level, false);
 }
 
 int vcycle(pamg_handle *h, int n, bool dead_after) {
     CHK(check_level(h, 1));
+    // the fused op = 0 forms wait only for the exchange that read the send buffer they pack; the others may
+    // touch anything an early exchange still in flight touches
+    if (!(h->p.cycle == 0 && fused_ok(h))) CHK(settle(h));
     if (h->p.cycle == 1) {
         if (corrected_resident_ok(h)) return vcycle_corrected_resident(h, n);
         if (face_corrected_pp_ok(h)) return vcycle_corrected_face_pp(h, n);
@@ -2341,6 +2364,7 @@ int pamg_vcycle(pamg_handle *h, int n) {
 
 int pamg_direct_solve(pamg_handle *h, int level) {
     if (!h) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, level));
     return direct_solve(h, level);
 }
@@ -2372,6 +2396,7 @@ int pamg_block_inverse(pamg_handle *h, int n, long nb, const double *A, double *
 
 int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
     if (!h || ntime < 0 || n_multigrid < 0) return PAMG_ERR_ARG;
+    CHK(settle(h));
     {
         // the resident schedule runs the whole loop as one launch: a step touches only its own
         // tiles (told := tnew, the RHS from it and s', n_multigrid cycles), so every tile goes
@@ -2417,6 +2442,7 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
 int pamg_synchronize(pamg_handle *h) {
     if (!h) return PAMG_ERR_ARG;
     CHK(sync_stream(h, h->stream));
+    if (h->sent_pending[0] || h->sent_pending[1]) CHK(sync_stream(h, h->stream_comm));
     return PAMG_OK;
 }
 
@@ -2485,6 +2511,7 @@ int pamg_timing_issued(pamg_handle *h, int kid, long *issued) {
 
 int pamg_sweep_bench(pamg_handle *h, int sweeps, int assembled, double *ms_avg, double *bytes_per_launch) {
     if (!h || sweeps < 1) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, 1));
     Level &L = h->lv[1];
     const double rdt = 1 / h->p.dt;
@@ -2514,6 +2541,7 @@ int pamg_sweep_bench(pamg_handle *h, int sweeps, int assembled, double *ms_avg, 
 
 int pamg_sweep_bench_output(pamg_handle *h, int assembled, double *host) {
     if (!h || !host) return PAMG_ERR_ARG;
+    CHK(settle(h));
     CHK(check_level(h, 1));
     Level &L = h->lv[1];
     const double rdt = 1 / h->p.dt;
