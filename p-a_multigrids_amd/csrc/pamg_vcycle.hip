@@ -94,6 +94,7 @@ hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split
     A.send_b = send_b;
     A.cycles = cycles;
     A.steps = steps;
+
     // tile: 2**TL level-1 sub-elements, TL = fine_tl (level-1 launch) or CGeo's (coarse launch)
     const int TL = coarse ? (2 * n_split > 8 ? std::min(2 * n_split, kFineTLMax) : 8) : fine_tl(n_split);
     // un_eles [ua, ub) (ub < 0: all); ua on a tile boundary, ub too unless it is U

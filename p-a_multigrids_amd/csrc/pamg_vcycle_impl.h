@@ -1346,6 +1346,10 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const double rdt = A.rdt;
     const int ns = A.n_smooth, m = A.cycles;
+    // (Measured, not kept: starting the first round's k-th workgroup of a CU k x 1-2 us per cycle of the call late,
+    // so that the co-resident tiles' loads and stores fall apart in time -- 0-4 % slower at 20 and 200 cycles,
+    // profiles/r05_l_res_stagger.txt. A call's state crosses HBM once, ~250 us at one cycle, and is hidden under the
+    // cycles from about five on: profiles/r05_k_call_fit.txt.)
     const int64_t tb = resident_tile(A);
     const bool xe = !XC && A.xe_done != nullptr;   // the per-call exchange starts when the remote tiles end
     const bool xr = (XC || xe) && tile_remote<S, T>(A, tb);
