@@ -605,10 +605,22 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_BLDS
 #define PAMG_FACE_PP_BLDS 1
 #endif
+#ifndef PAMG_FACE_PP_SNAP1
+#define PAMG_FACE_PP_SNAP1 1
+#endif
 // NT: red-black passes with fewer threads than up sub-elements run a second up item on some threads. For
 // the 256-sub-element un_ele 192 threads (136 ups, one each) measured faster than 128 (0.71 vs 0.73 ms of
 // coarse launches per cycle); for the 1,024 one 576 threads (528 ups) measured slower than 512 (level-1
 // passes 0.85 vs 0.71 ms per cycle at seven waves per SIMD, profiles/r04_k_face_pp_nt.txt), so it keeps 512
+// phase stamps of the two-sweep passes (diagnostics build: make PAMG_STAMPS=1 and PAMG_PP_STAMPS=<file>;
+// scripts/pp_stamps.py): per workgroup the wall clock (100 MHz) at its start, after its loads, after the ghost
+// update, after each sweep and after its stores
+constexpr int kPPStamps = 6;
+__device__ long long *g_pp_stamps = nullptr;
+__device__ __forceinline__ void pp_stamp(int i) {
+    if (PAMG_STAMPS && g_pp_stamps && threadIdx.x == 0) g_pp_stamps[(int64_t)blockIdx.x * kPPStamps + i] = wall_clock64();
+}
+
 template <int TS, int NT, bool RB, int K>
 __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, double *out_end2,
@@ -626,18 +638,25 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
     // PAMG_FACE_PP_BLDS (A/B): 1 the RHS staged in LDS beside the iterate; 0 each item's RHS in registers,
     // loaded from memory at its position (less LDS: more workgroups per CU)
     constexpr bool BL = PAMG_FACE_PP_BLDS != 0;
-    constexpr int OX = 0, OB = 3 * TS, OH = (BL ? 6 : 3) * TS, OW = OH + K * NH;
+    // ONE snapshot image (PAMG_FACE_PP_SNAP1, default): the second sweep's snapshot -- the ghost updates -- stays in the
+    // registers of the threads that compute it and replaces the first sweep's once that sweep's last reader has
+    // passed: the up pass (a down sub-element never reads the snapshot, words_up) or Jacobi's read phase. 53,952 ->
+    // 51,648 B of LDS: three workgroups per CU instead of two (phase stamps, profiles/r05_n_pp_stamps.txt: 512 of
+    // the 768 slots were ever resident)
+    constexpr bool SNAP1 = PAMG_FACE_PP_SNAP1 != 0 && K == 2;
+    constexpr int OX = 0, OB = 3 * TS, OH = (BL ? 6 : 3) * TS, OW = OH + (SNAP1 ? 1 : K) * NH;
     __shared__ double LDSM[OW + 24];
     double (*X)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OX);
     double (*B)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OB);
     double *WD = LDSM + OW;
-    auto HI = [&](int snap) { return LDSM + OH + snap * NH; };
+    auto HI = [&](int snap) { return LDSM + OH + (SNAP1 ? 0 : snap) * NH; };
     const int t = threadIdx.x;
     // (Measured, not kept: starting the first round's k-th workgroup of a CU k x 4 / 8 / 12 us late, so that the
     // co-resident workgroups' load, sweep and store phases fall apart -- the level-1 passes 0.74 -> 0.75 / 0.76 /
     // 0.80 ms per cycle, profiles/r05_f_face_pp_stagger.txt; a persistent grid looping over tiles spilled 272 B
     // per lane.) The tile body is a lambda called once: 76 -> 70 VGPRs.
     auto tile = [&](const int64_t u) {
+    pp_stamp(0);
     const int64_t s0 = u * TS;
     FaceRec R;
     load_face_rec(stc, fface, fsx, u, R);
@@ -732,6 +751,8 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
         wdv = fface + v * kFaceStride + kFaceWD + 3 * face_pattern(nbe);
     }
     __syncthreads();
+    pp_stamp(1);
+    double hn[3] = {0.0, 0.0, 0.0};   // SNAP1: this thread's slot of the second sweep's snapshot
     if constexpr (K == 2) {
         // the neighbour's boundary sub-element e after the first sweep (an up one: its sweep reads its down
         // neighbours, unchanged since the previous sweep, and the snapshot across its faces): the second
@@ -751,14 +772,24 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
                                       [&](int fi, int c) { return c == 0 ? yv[fi][0] : c == 1 ? yv[fi][1] : yv[fi][2]; },
                                       [&](int q) { return wdv[q]; }, level1, rdt, r);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) HI(1)[hq + c] = r[c];
-            } else {
+                for (int c = 0; c < 3; ++c) {
+                    if (SNAP1) hn[c] = r[c];
+                    else HI(1)[hq + c] = r[c];
+                }
+            } else if (!SNAP1) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c) HI(1)[hq + c] = HI(0)[hq + c];   // boundary words: constant
             }
         }
         __syncthreads();   // the ghost updates read the start iterate (X) before the sweeps rewrite it
+        pp_stamp(2);
     }
+    // SNAP1: the second sweep's snapshot into the image, after the first sweep's last read of it (boundary words: constant)
+    auto snap_next = [&]() {
+        if (SNAP1 && gon && ge.x >= 0)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) HI(0)[hq + c] = hn[c];
+    };
     auto xin = [&](int c, int q) { return X[c][q]; };
     // one item k: face_apply<MODE> of position ij[k] from the tile, the RHS and snapshot snap
     auto item = [&](auto mc, int k, int snap, double r[3]) {
@@ -797,6 +828,7 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
                 for (int c = 0; c < 3; ++c) X[c][ij[k]] = r[c];
             }
             __syncthreads();
+            if (snap == 0) snap_next();   // the down pass reads no snapshot
 #pragma unroll
             for (int k = KU; k < KU + KD; ++k) {
                 if (ij[k] < 0) continue;
@@ -811,6 +843,7 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
 #pragma unroll
             for (int k = 0; k < KU; ++k) item(std::integral_constant<int, 2>{}, k, snap, r[k]);
             __syncthreads();
+            if (snap == 0) snap_next();
 #pragma unroll
             for (int k = 0; k < KU; ++k)
 #pragma unroll
@@ -828,13 +861,17 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
     };
     if (res == 1) residual(0);
     sweep(0);
+    pp_stamp(3);
     if constexpr (K == 2) {
         if (out_mid) store(out_mid);
         if (res == 2) residual(1);
         sweep(1);
     }
+    pp_stamp(4);
     if (out_end) store(out_end);
     if (out_end2) store(out_end2);   // the corrected cycle's smoother call: tnew and tnew_nonlin both its result
+    if (PAMG_STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_stamp(5);
     };
     tile((int64_t)blockIdx.x);
 }
@@ -1880,6 +1917,17 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
     const dim3 g((unsigned)(L.N / L.nsub));
     const int l1 = level1 ? 1 : 0;
     double *R = res ? L.RES : nullptr;
+    // PAMG_PP_STAMPS=<file> (a PAMG_STAMPS=1 build): append each launch's per-workgroup phase stamps
+    static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_PP_STAMPS") : nullptr;
+    long long *stamps = nullptr;
+    const size_t nst = (size_t)g.x * kPPStamps;
+    if (stamp_path) {
+        hipError_t e = hipMalloc(&stamps, nst * sizeof(long long));
+        if (e == hipSuccess) e = hipMemsetAsync(stamps, 0, nst * sizeof(long long), s);
+        if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_pp_stamps), &stamps, sizeof stamps, 0,
+                                                        hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return e;
+    }
 #define PAMG_FPP(TS, NT, RB_, K_)                                                                                    \
     hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, out_end2, L.RHS, \
                        L.stc,                                                                                         \
@@ -1896,7 +1944,22 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
     else return hipErrorInvalidValue;   // (4,096: the iterate and RHS exceed the LDS)
 #undef PAMG_FPPK
 #undef PAMG_FPP
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (stamp_path) {
+        std::vector<long long> hst(nst);
+        long long *null = nullptr;
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpy(hst.data(), stamps, nst * sizeof(long long), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_pp_stamps), &null, sizeof null);
+        (void)hipFree(stamps);
+        if (FILE *f = fopen(stamp_path, "ab")) {
+            const long long hdr[4] = {(long long)g.x, kPPStamps, L.nsub, K};
+            fwrite(hdr, sizeof hdr, 1, f);
+            fwrite(hst.data(), sizeof(long long), nst, f);
+            fclose(f);
+        }
+    }
+    return e;
 }
 
 int face_chain_per_wg(int nsub, int U, int cus) {

@@ -1350,6 +1350,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
     // so that the co-resident tiles' loads and stores fall apart in time -- 0-4 % slower at 20 and 200 cycles,
     // profiles/r05_l_res_stagger.txt. A call's state crosses HBM once, ~250 us at one cycle, and is hidden under the
     // cycles from about five on: profiles/r05_k_call_fit.txt.)
+    stamp<512>(A, 0);
     const int64_t tb = resident_tile(A);
     const bool xe = !XC && A.xe_done != nullptr;   // the per-call exchange starts when the remote tiles end
     const bool xr = (XC || xe) && tile_remote<S, T>(A, tb);
@@ -1466,6 +1467,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
         };
         for (int c = 0; c + 1 < total; ++c) cycle(c, std::false_type{});
         cycle(total - 1, std::true_type{});
+        stamp<512>(A, 7);   // the role's end (diagnostics build)
     } else if (wv == 0) {
         // ---- level 2: sub-elements 128 + 2 lane, +1; levels 3 .. L-1 (1-based), one sub-element
         //      of each per lane (none with L = 3)
@@ -1523,6 +1525,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
         };
         for (int c = 0; c + 1 < total; ++c) cycle(c, std::false_type{});
         cycle(total - 1, std::true_type{});
+        stamp<512>(A, 7);   // the role's end (diagnostics build)
     } else {
         // ---- level 1 (the reference's): waves 1,2,3,5 an adjacent pair + a single sub-element
         //      per thread (N = 3), waves 6,7 a pair (N = 2) and one sub-element of level 2
@@ -1670,6 +1673,7 @@ __global__ __launch_bounds__(512, L >= 5 ? PAMG_RES_WAVES : PAMG_RESB_WAVES) voi
             }
             for (; c + 1 < total; ++c) cycle(c, std::false_type{});
             cycle(total - 1, std::true_type{});
+            stamp<512>(A, 7);   // the role's end (diagnostics build)
         };
         if (grpB) level1(std::integral_constant<int, 2>{});
         else level1(std::integral_constant<int, 3>{});
