@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--mesh", default=MESH)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the n_split=3 and sweep-kernel side measurements")
+    ap.add_argument("--extras-after", action="store_true",
+                    help="run the side measurements after the timed region instead of before the warm-up")
     ap.add_argument("--halo-mode", type=int, default=0)
     ap.add_argument("--comm", choices=["rccl", "detached"], default="rccl",
                     help="detached: partitions without the RCCL exchange -- a check of the multi-process "
@@ -463,6 +465,109 @@ def main():
                                 "alg_bytes_per_launch": by, "bytes_per_sub_element": 168,
                                 "sub_elements": mesh.U * 4 ** a.nsplit, "ms_per_launch": round(ms, 4),
                                 "events": f"HIP event pair around each of {SWEEP_LAUNCHES} launches"}
+    def other_measurements():
+        """the side measurements reported under "extra" (and time_loop); the time loop last, on the bench's
+        own handle, so that with the default order the warm-up and the timed call follow it without an idle gap"""
+        nonlocal time_loop
+        ex = {}
+        # the round-1 form on the same workload: one HBM-bound launch per cycle (call schedule 1),
+        # its pipelined launch against the HBM roofline
+        s1 = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
+                                        fused=a.fused, arith=a.arith)
+        s1.set_call_schedule(1)
+        s1.begin_timestep()
+        s1.vcycle(a.warmup)
+        s1.synchronize()
+        t0 = time.perf_counter()
+        s1.vcycle(a.steps)
+        s1.synchronize()
+        v1 = a.steps / (time.perf_counter() - t0)
+        s1.timing_enable(ALL_CLASSES)
+        s1.timing_stride(EVENT_STRIDE)
+        s1.timing_reset()
+        s1.vcycle(a.steps)
+        s1.synchronize()
+        kp = s1.timing()["vcycle_pipe"]
+        if kp["launches"]:
+            msp = kp["ms"] / kp["launches"]
+            bp = kp["bytes"] / kp["launches"]
+            ex["one_launch_per_cycle"] = dict(
+                vcycles_per_s=round(v1, 1), pipe_ms=round(msp, 4), pipe_alg_bytes=bp,
+                pipe_gbs=round(bp / (msp * 1e-3) / 1e9, 1), pipe_frac=round(bp / (msp * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                pipe_traffic=pmc_traffic("vcycle_pipe", a.nsplit, a.levels))
+        s1.close()
+        # the matrices.F90 SpMV (csr_mul_array, 3 entries per row) over the level-1 operator's
+        # size in the reference's block numbering: 3 N1 rows, 52 B per row (3 x (4 B column +
+        # 8 B value), 8 B result, 8 B of the gathered vector)
+        nrows = 3 * mesh.U * 4 ** a.nsplit
+        base = 3 * (np.arange(nrows, dtype=np.int32) // 3)
+        jloc = (base[:, None] + np.arange(1, 4, dtype=np.int32)[None, :]).reshape(-1)
+        del base
+        sp = pamg.Sparse(s, np.arange(1, 3 * nrows, 3, dtype=np.int32), jloc,
+                         np.random.default_rng(20251015).uniform(-1, 1, 3 * nrows))
+        del jloc
+        ms = sp.bench(nrows, 20)
+        by = 52.0 * nrows
+        ex["csr_mul_array"] = dict(rows=nrows, ms=round(ms, 4), bytes_per_launch=by,
+                                   gbs=round(by / (ms * 1e-3) / 1e9, 1),
+                                   frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
+        sp.close()
+        # the same workload in the other schedules / arithmetic: the per-step kernel sequence
+        # (bitwise equal to the fused cycle), the concurrent fused launches, and the reference's
+        # operation order (bitwise equal to the reference)
+        for tag, kw in (("fused0", dict(fused=0, arith=a.arith)), ("fused1", dict(fused=1, arith=a.arith)),
+                        ("fused2", dict(fused=2, arith=a.arith)), ("fused3", dict(fused=3, arith=a.arith)),
+                        ("arith0", dict(fused=a.fused, arith=0)), ("arith1", dict(fused=a.fused, arith=1))):
+            if kw["fused"] == a.fused and kw["arith"] == a.arith:
+                continue
+            su = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
+                                            **kw)
+            su.begin_timestep()
+            su.vcycle(a.warmup)
+            su.synchronize()
+            t0 = time.perf_counter()
+            su.vcycle(a.steps)
+            su.synchronize()
+            ex[f"{tag}_vcycles_per_s"] = round(a.steps / (time.perf_counter() - t0), 2)
+            su.close()
+        s3 = pamg.SemiImplicitIterative(mesh, 3, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
+                                        arith=a.arith)
+        s3.begin_timestep()
+        s3.vcycle(a.warmup)
+        s3.synchronize()
+        t0 = time.perf_counter()
+        s3.vcycle(max(a.steps, 200))
+        s3.synchronize()
+        ex["nsplit3_vcycles_per_s"] = round(max(a.steps, 200) / (time.perf_counter() - t0), 1)
+        # config 3 driven as the reference drives it: pamg_run(50, 2), one resident launch
+        s3.run(5, 2)
+        s3.synchronize()
+        t0 = time.perf_counter()
+        s3.run(TIME_LOOP_STEPS, 2)
+        s3.synchronize()
+        ex["nsplit3_time_loop_vcycles_per_s"] = round(2 * TIME_LOOP_STEPS / (time.perf_counter() - t0), 1)
+        s3.close()
+        # the other workloads of the north star on one GPU: config 5's mesh at n_split = 6 (tiles are
+        # quarters of an un_ele there), config 3 at n_split = 6, and a synthetic structured strip
+        # 4x untitled8192 (256 x 64 x 2, pamg_msh_strip) at the benchmarked n_split = 5
+        for tag, m_, S_ in (("irregular_nsplit6", pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "irregular.msh")), 6),
+                            ("untitled8192_nsplit6", mesh, 6),
+                            ("strip256x64_nsplit5", pamg.Mesh.strip(256, 64), 5)):
+            ex[tag] = measure_workload(pamg, m_, S_, a.levels, a.nsmooth, a.arith, device)
+        # SURVEY.md 8(f) rank 1: the face-coupled operator on the benchmarked mesh, n_split 5, 3 levels
+        ex["op1"] = measure_face(pamg, mesh, a.nsplit, 3, device)
+        # and the corrected cycle on it (cycle = 1: levels 1-2 in two-sweep passes, the coarsest level's chain)
+        ex["op1_cycle1"] = measure_face(pamg, mesh, a.nsplit, 3, device, cycle=1)
+        ex["cycle1"] = measure_corrected(pamg, mesh, a.nsplit, a.levels, a.nsmooth, a.arith, device)
+        time_loop = measure_time_loop(s)
+        return ex
+
+    extra_other = {}
+    if rank == 0 and world == 1 and not a.no_extra and not a.extras_after:
+        # before the warm-up (default): the timed call then starts on a GPU that has been running this
+        # workload for a while, its clocks settled, as in a deployment's steady state, instead of on a GPU
+        # coming out of the idle host work around handle creation (profiles/r05_p_extras_order.txt)
+        extra_other = other_measurements()
     s.vcycle(a.warmup)
     s.synchronize()
     # per-kernel HIP events (the roofline) inside the timed region on one GPU; with N ranks
@@ -559,99 +664,11 @@ def main():
         xa = [None] * world
         dist.all_gather_object(xa, [round(v, 1) for v in xt] if xt else None)
         extra["early_exchange_us"] = xa
+    if rank == 0 and world == 1 and not a.no_extra and a.extras_after:
+        extra_other = other_measurements()
     if rank == 0 and world == 1 and not a.no_extra:
-        # the round-1 form on the same workload: one HBM-bound launch per cycle (call schedule 1),
-        # its pipelined launch against the HBM roofline
-        s1 = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
-                                        fused=a.fused, arith=a.arith)
-        s1.set_call_schedule(1)
-        s1.begin_timestep()
-        s1.vcycle(a.warmup)
-        s1.synchronize()
-        t0 = time.perf_counter()
-        s1.vcycle(a.steps)
-        s1.synchronize()
-        v1 = a.steps / (time.perf_counter() - t0)
-        s1.timing_enable(ALL_CLASSES)
-        s1.timing_stride(EVENT_STRIDE)
-        s1.timing_reset()
-        s1.vcycle(a.steps)
-        s1.synchronize()
-        kp = s1.timing()["vcycle_pipe"]
-        if kp["launches"]:
-            msp = kp["ms"] / kp["launches"]
-            bp = kp["bytes"] / kp["launches"]
-            extra["one_launch_per_cycle"] = dict(
-                vcycles_per_s=round(v1, 1), pipe_ms=round(msp, 4), pipe_alg_bytes=bp,
-                pipe_gbs=round(bp / (msp * 1e-3) / 1e9, 1), pipe_frac=round(bp / (msp * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                pipe_traffic=pmc_traffic("vcycle_pipe", a.nsplit, a.levels))
-        s1.close()
         extra.update(extra_pre)
-        time_loop = measure_time_loop(s)
-        # the matrices.F90 SpMV (csr_mul_array, 3 entries per row) over the level-1 operator's
-        # size in the reference's block numbering: 3 N1 rows, 52 B per row (3 x (4 B column +
-        # 8 B value), 8 B result, 8 B of the gathered vector)
-        nrows = 3 * mesh.U * 4 ** a.nsplit
-        base = 3 * (np.arange(nrows, dtype=np.int32) // 3)
-        jloc = (base[:, None] + np.arange(1, 4, dtype=np.int32)[None, :]).reshape(-1)
-        del base
-        sp = pamg.Sparse(s, np.arange(1, 3 * nrows, 3, dtype=np.int32), jloc,
-                         np.random.default_rng(20251015).uniform(-1, 1, 3 * nrows))
-        del jloc
-        ms = sp.bench(nrows, 20)
-        by = 52.0 * nrows
-        extra["csr_mul_array"] = dict(rows=nrows, ms=round(ms, 4), bytes_per_launch=by,
-                                      gbs=round(by / (ms * 1e-3) / 1e9, 1),
-                                      frac=round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3))
-        sp.close()
-        s.close()
-        # the same workload in the other schedules / arithmetic: the per-step kernel sequence
-        # (bitwise equal to the fused cycle), the concurrent fused launches, and the reference's
-        # operation order (bitwise equal to the reference)
-        for tag, kw in (("fused0", dict(fused=0, arith=a.arith)), ("fused1", dict(fused=1, arith=a.arith)),
-                        ("fused2", dict(fused=2, arith=a.arith)), ("fused3", dict(fused=3, arith=a.arith)),
-                        ("arith0", dict(fused=a.fused, arith=0)), ("arith1", dict(fused=a.fused, arith=1))):
-            if kw["fused"] == a.fused and kw["arith"] == a.arith:
-                continue
-            su = pamg.SemiImplicitIterative(mesh, a.nsplit, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
-                                            **kw)
-            su.begin_timestep()
-            su.vcycle(a.warmup)
-            su.synchronize()
-            t0 = time.perf_counter()
-            su.vcycle(a.steps)
-            su.synchronize()
-            extra[f"{tag}_vcycles_per_s"] = round(a.steps / (time.perf_counter() - t0), 2)
-            su.close()
-        s3 = pamg.SemiImplicitIterative(mesh, 3, a.levels, n_smooth=a.nsmooth, solver=3, device=device,
-                                        arith=a.arith)
-        s3.begin_timestep()
-        s3.vcycle(a.warmup)
-        s3.synchronize()
-        t0 = time.perf_counter()
-        s3.vcycle(max(a.steps, 200))
-        s3.synchronize()
-        extra["nsplit3_vcycles_per_s"] = round(max(a.steps, 200) / (time.perf_counter() - t0), 1)
-        # config 3 driven as the reference drives it: pamg_run(50, 2), one resident launch
-        s3.run(5, 2)
-        s3.synchronize()
-        t0 = time.perf_counter()
-        s3.run(TIME_LOOP_STEPS, 2)
-        s3.synchronize()
-        extra["nsplit3_time_loop_vcycles_per_s"] = round(2 * TIME_LOOP_STEPS / (time.perf_counter() - t0), 1)
-        s3.close()
-        # the other workloads of the north star on one GPU: config 5's mesh at n_split = 6 (tiles are
-        # quarters of an un_ele there), config 3 at n_split = 6, and a synthetic structured strip
-        # 4x untitled8192 (256 x 64 x 2, pamg_msh_strip) at the benchmarked n_split = 5
-        for tag, m_, S_ in (("irregular_nsplit6", pamg.Mesh.read(os.path.join(ROOT, "tests", "meshes", "irregular.msh")), 6),
-                            ("untitled8192_nsplit6", mesh, 6),
-                            ("strip256x64_nsplit5", pamg.Mesh.strip(256, 64), 5)):
-            extra[tag] = measure_workload(pamg, m_, S_, a.levels, a.nsmooth, a.arith, device)
-        # the face-coupled operator on the benchmarked mesh, n_split 5, 3 levels
-        extra["op1"] = measure_face(pamg, mesh, a.nsplit, 3, device)
-        # and the corrected cycle on it (cycle = 1: levels 1-2 in two-sweep passes, the coarsest level's chain)
-        extra["op1_cycle1"] = measure_face(pamg, mesh, a.nsplit, 3, device, cycle=1)
-        extra["cycle1"] = measure_corrected(pamg, mesh, a.nsplit, a.levels, a.nsmooth, a.arith, device)
+        extra.update(extra_other)
     if world > 1 and not a.no_extra:
         # the other exchange mode on the same partition (timed region the same shape): halo words
         # exchanged after every cycle, overlapped with the next one
