@@ -2,7 +2,9 @@
 # Round-5 final evidence, in two calls (a call is limited to 20 minutes):
 #   r5_final.sh TAG A   GPU tests, smoke, the bench (default and the driver's shape, with the CPU
 #                       baseline), the strong-scaling probe, the coarsest-chain microbenchmark
-#   r5_final.sh TAG B   rocprofv3 kernel stats of the bench and of the face probe, PMC FETCH / WRITE
+#   r5_final.sh TAG B   rocprofv3 kernel stats of the bench (the driver's shape with its side measurements
+#                       first, as bench.py runs it; the timed call's dispatch beside the bench line's events)
+#                       and of the face probe, PMC FETCH / WRITE
 #                       passes of the resident call and of the level-1 roofline sweeps
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/${1:-final}; mkdir -p $O
@@ -23,7 +25,10 @@ fi
 if [ "$2" = "B" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- python3 $R/bench.py --no-cpu-baseline --no-extra > $O/prof_bench.log 2>&1 || exit 1
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench_driver -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra > $O/prof_bench_driver.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench_driver -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench_driver.log 2>&1 || exit 1
+  python3 $R/scripts/trace_timed.py $O/prof_bench_driver "void pamg::(anonymous namespace)::k_vc_resb<5, 3" $O/prof_bench_driver.log > $O/prof_bench_driver_timed.txt || exit 1
+  python3 $R/scripts/trace_timed.py $O/prof_bench "void pamg::(anonymous namespace)::k_vc_resb<5, 3" $O/prof_bench.log > $O/prof_bench_timed.txt || exit 1
+  tail -2 $O/prof_bench_driver_timed.txt $O/prof_bench_timed.txt
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_res_fetch -o run -- python3 $R/bench.py --steps 20 --warmup 1 --no-cpu-baseline --no-extra > $O/pmc_res_fetch.log 2>&1 || exit 1
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_res_write -o run -- python3 $R/bench.py --steps 20 --warmup 1 --no-cpu-baseline --no-extra > $O/pmc_res_write.log 2>&1 || exit 1
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_sweep_fetch -o run -- python3 $R/scripts/sweep_prof.py 3 > $O/pmc_sweep_fetch.log 2>&1 || exit 1
