@@ -1340,16 +1340,40 @@ int face_corr_call(pamg_handle *h, int l, bool last) {
     return PAMG_OK;
 }
 
+// the corrected cycle's get_residual and restrictor of a level l < L (:336-338) as one sweep-less k_face_pp pass
+// (res 3): the residual RHS - A tnew from the neighbours' iterate itself, restricted straight into RHS_{l+1}
+// (k_restrict_tile's arithmetic). The residual is stored only where the state keeps it: level 1's is rewritten
+// by the fine residual after the cycle (the call's last cycle); a coarser level's is kept from the call's last
+// cycle. The halo words the per-step residual refreshes first are rewritten, unread, by that same fine residual
+// (every coarser level's words are a subset of level 1's slots).
+int face_res_restrict(pamg_handle *h, int l, bool last) {
+    Level &L = h->lv[l];
+    h->rhsn_valid = false;
+    h->overlap_static_l1 = false;
+    const bool store = l > 1 && last;
+    Span sp(h, PAMG_K_RESIDUAL, (48.0 + (store ? 24.0 : 0.0)) * (double)L.N + 24.0 * (double)h->lv[l + 1].N + 168.0 * h->U);
+    HIPCHK(h, launch_face_pp(h->stream, L, 1, L.T, nullptr, nullptr, nullptr, h->p.solver == 3, l == 1, 1 / h->p.dt, 3,
+                             nullptr, &h->lv[l + 1], store));
+    return PAMG_OK;
+}
+
 int vcycle_corrected_face_pp(pamg_handle *h, int n) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     h->overlap_static_l1 = false;
+    // PAMG_FACE_RR=0 (A/B): the residual and the restrictor as their own launches
+    const char *rr_env = getenv("PAMG_FACE_RR");
+    const bool rr = !(rr_env && atoi(rr_env) == 0);
     for (int c = 0; c < n; ++c) {
         const bool last = c + 1 == n;
         for (int l = 1; l < L; ++l) {
             if (l > 1) HIPCHK(h, hipMemsetAsync(h->lv[l].T, 0, 3 * (size_t)h->lv[l].pitch * sizeof(double), h->stream));
             CHK(face_corr_call(h, l, last));
-            CHK(residual_corrected(h, l));
-            CHK(restrict_(h, l));
+            if (rr && face_pp_ok(h, l)) {
+                CHK(face_res_restrict(h, l, last));
+            } else {
+                CHK(residual_corrected(h, l));
+                CHK(restrict_(h, l));
+            }
         }
         Level &C = h->lv[L];
         HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));   // from zero

@@ -628,7 +628,7 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
     const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
     const double2 *__restrict__ bcv, const int *__restrict__ cpos, int nup, int64_t pitch, int level1, double rdt,
-    int res, double *RESout) {
+    int res, double *RESout, double *RHSc, int64_t pitch_c) {
     constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
     // red-black: the colour passes run over colour lists (Level::cpos), every lane with an item of the colour
     constexpr int NUP = M * (M + 1) / 2, KU = RB ? (NUP + NT - 1) / NT : PER, KD = RB ? (TS - NUP + NT - 1) / NT : 0;
@@ -817,6 +817,26 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
         }
         __syncthreads();   // every read of the iterate before the passes rewrite it
     };
+    // res 3 (the corrected cycle's residual and restrictor, :336-338, in one pass): get_residual RHS - A x of the
+    // start iterate, and the restrictor of it into the coarse RHS RHSc (k_restrict_tile's: the coarse
+    // sub-element cc of this tile takes component i from child pick_i = 4 cc + {2, 3, 0}[i], the mean of that
+    // child's three residual components, in k_restrict_tile's order) -- so child 4 cc + 1 is not evaluated unless
+    // the residual itself is stored (RESout: a level whose residual is read after the call)
+    auto residual_restrict = [&]() {
+        const int64_t c0 = s0 >> 2;
+#pragma unroll
+        for (int k = 0; k < KU + KD; ++k) {
+            const int j = ij[k];
+            if (j < 0 || (!RESout && (j & 3) == 1)) continue;
+            double r[3];
+            item(std::integral_constant<int, 4>{}, k, 0, r);
+            if (RESout)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) RESout[c * pitch + s0 + j] = r[c];
+            const int q = j & 3;
+            if (q != 1) RHSc[(q == 2 ? 0 : q == 3 ? 1 : 2) * pitch_c + c0 + (j >> 2)] = div3(r[0] + r[1] + r[2]);
+        }
+    };
     auto sweep = [&](int snap) {
         if constexpr (RB) {   // up items, then down items, in place (a colour reads only the other)
 #pragma unroll
@@ -859,6 +879,10 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
             for (int c = 0; c < 3; ++c) st2(o + c * pitch + s0 + j, make_double2(X[c][j], X[c][j + 1]));
         }
     };
+    if (res == 3) {   // get_residual (RHS - A x) restricted: no sweep, no stores of the iterate
+        residual_restrict();
+        return;
+    }
     if (res == 1) residual(0);
     sweep(0);
     pp_stamp(3);
@@ -1906,17 +1930,25 @@ static hipError_t launch_coresident(const void *f, int grid, int nt, void **args
 
 // k_face_pp: K sweeps of a whole-un_ele-tile level in one launch (face_tile_shape; single domain)
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
-                          double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2) {
+                          double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2, const Level *coarse,
+                          bool res_store) {
     if (L.N == 0) return hipSuccess;
     const int m = L.nsub == 256 ? 16 : L.nsub == 1024 ? 32 : 64;
     if (!face_tile_shape(L) || !L.fnb || !L.gtab || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)) ||
         (out_end2 && (out_end2 == in || !out_end)) ||
         (rb && (!L.cpos || L.nup != m * (m + 1) / 2)))
         return hipErrorInvalidValue;
+    // res 3: the residual restricted into the coarse RHS, one sweep-less pass (K 1, no iterate outputs); the coarse
+    // level is this one's quarter (4 children per coarse sub-element, the same un_eles)
+    if (res == 3 && (K != 1 || out_pre || out_end || out_end2 || !coarse || !coarse->RHS || coarse->N * 4 != L.N))
+        return hipErrorInvalidValue;
+    if (res != 3 && (coarse || res_store)) return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
     const dim3 g((unsigned)(L.N / L.nsub));
     const int l1 = level1 ? 1 : 0;
-    double *R = res ? L.RES : nullptr;
+    double *R = (res == 1 || res == 2 || res_store) ? L.RES : nullptr;
+    double *RC = res == 3 ? coarse->RHS : nullptr;
+    const int64_t pc = res == 3 ? coarse->pitch : 0;
     // PAMG_PP_STAMPS=<file> (a PAMG_STAMPS=1 build): append each launch's per-workgroup phase stamps
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_PP_STAMPS") : nullptr;
     long long *stamps = nullptr;
@@ -1931,7 +1963,7 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
 #define PAMG_FPP(TS, NT, RB_, K_)                                                                                    \
     hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, out_end2, L.RHS, \
                        L.stc,                                                                                         \
-                       L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.cpos, L.nup, L.pitch, l1, rdt, res, R)
+                       L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.cpos, L.nup, L.pitch, l1, rdt, res, R, RC, pc)
 #define PAMG_FPPK(TS, NT)                                          \
     if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \
     else { if (K == 2) PAMG_FPP(TS, NT, false, 2); else PAMG_FPP(TS, NT, false, 1); }

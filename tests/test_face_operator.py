@@ -295,32 +295,38 @@ def test_face_corrected_cycle_passes_equal_per_step(mesh, S, L, solver, ns, spli
     """The corrected cycle on the face operator with its smoother calls below the coarsest level as two-sweep
     passes (k_face_pp, the call's result stored as tnew -- and as tnew_nonlin in the call's last cycle -- and
     the fine residual after the cycle only in the call's last cycle) leaves the per-step sequence's state bit
-    for bit (bench.py's extra.op1_cycle1 configuration first), and its level-1 calls are the passes."""
+    for bit (bench.py's extra.op1_cycle1 configuration first), and its level-1 calls are the passes. The residual
+    and restrictor of a streaming level run as one sweep-less pass (k_face_pp res 3, the residual stored only
+    where the state keeps it); PAMG_FACE_RR=0 keeps them as their own launches -- the same state too."""
     import pamg
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
 
     def run(split):
         g = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, op=1, cycle=1)
-        g.timing_enable(1)   # PAMG_K_SMOOTH_L1
+        g.timing_enable(1 | 8)   # PAMG_K_SMOOTH_L1, PAMG_K_RESTRICT
         g.timing_reset()
         for n in split:
             g.begin_timestep()
             g.vcycle(n)
         st, ov = g.state(), g.overlap()
-        issued = g.timing()["smooth_L1"]["issued"]
+        tm = g.timing()
         g.close()
-        return st, ov, issued
+        return st, ov, tm["smooth_L1"]["issued"], tm["restrict"]["issued"]
 
     for split in splits:
         monkeypatch.setenv("PAMG_FACE_CORR_PP", "0")
-        rs, rov, _ = run(split)
+        rs, rov, _, _ = run(split)
         monkeypatch.setenv("PAMG_FACE_CORR_PP", "1")
-        gs, gov, issued = run(split)
-        assert_identical(gs, rs)
-        for x, y in zip(gov, rov):
-            np.testing.assert_array_equal(x, y)
-        if 4 ** S == 1024 or 4 ** S == 256:   # level 1 streams: two calls per cycle, ceil(ns / 2) passes each
-            assert issued == sum(split) * 2 * ((ns + 1) // 2), issued
+        for rr in ("0", "1"):
+            monkeypatch.setenv("PAMG_FACE_RR", rr)
+            gs, gov, issued, nrestrict = run(split)
+            assert_identical(gs, rs)
+            for x, y in zip(gov, rov):
+                np.testing.assert_array_equal(x, y)
+            if 4 ** S == 1024 or 4 ** S == 256:   # level 1 streams: two calls per cycle, ceil(ns / 2) passes each
+                assert issued == sum(split) * 2 * ((ns + 1) // 2), issued
+                # the fused residual-restrictor: level 1's restrictor is no launch of its own
+                assert nrestrict <= (L - 2 if rr == "1" else L - 1) * sum(split), (rr, nrestrict)
 
 
 @pytest.mark.gpu
