@@ -688,7 +688,9 @@ int face_residual(pamg_handle *h, int l, bool neg);
 // the call changes tnew -- computed by the call's first tile sweep from the iterate and snapshot it
 // loads anyway (the residual's own launch read tnew and RHS again), or by its own launch when the call
 // runs another form
-int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, bool res = false) {
+// both (not with dead_last): the call's result also into tnew -- the corrected cycle's tnew := tnew_nonlin after
+// the call (smooth_to_tnew), made by the chain's final stores instead of a copy launch
+int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, bool res = false, bool both = false) {
     Level &L = h->lv[l];
     h->tnn_level = l;
     h->overlap_static_l1 = false;
@@ -749,7 +751,8 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
             Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
             h->chain_pending = true;
             HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags,
-                                        L.chain_nb_off, L.chain_nb_list, h->chain_tmo, run, sweeps, dead_last ? 2 : 1,
+                                        L.chain_nb_off, L.chain_nb_list, h->chain_tmo, run, sweeps,
+                                        dead_last ? 2 : both ? 3 : 1,
                                         h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, src_is_T, f0, guard ? 1 : 0));
         }
         // fail safe: a launch whose workgroups were not all resident (a CU-masked stream, another stream's or
@@ -771,6 +774,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
         HIPCHK(h, launch_face_wave(h->stream, L, h->U, g, h->tov, h->tov_b, h->tovo, g0, g1, tag0, h->wave_flags,
                                    h->wave_order, h->chain_tmo, run, sweeps, dead_last ? 2 : 1, h->p.solver == 3,
                                    l == 1, rdt, h->slots, src_is_T));
+        if (both) HIPCHK(h, launch_copy(h->stream, L.TNN, L.T, 3 * L.pitch));
         return PAMG_OK;
     }
     for (int s = 0; s < run; ++s) {
@@ -786,6 +790,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
                                           s == 0 && src_is_T, r ? L.RES : nullptr));
         if (s + 1 < sweeps) CHK(halo(h, l, buf[(sweeps - 2 - s) & 1]));   // the next sweep's remote words
     }
+    if (both) HIPCHK(h, launch_copy(h->stream, L.TNN, L.T, 3 * L.pitch));
     return PAMG_OK;
 }
 
@@ -1099,7 +1104,7 @@ bool face_pp_ok(pamg_handle *h, int l) {
            (h->p.solver != 3 || L.words_up);
 }
 
-struct PPPass { int K, res; double *in, *pre, *mid, *end, *end2; };
+struct PPPass { int K, res; double *in, *pre, *mid, *end, *end2; bool interp = false; };
 
 // the passes of a stream of `total` sweeps from src with get_residual after sweep r for each r in res_at
 // (0 < r < total), ending with the final stores fin (1: tnew = the iterate before the last sweep,
@@ -1110,7 +1115,7 @@ int face_pp_plan(pamg_handle *h, int l, int total, double *src, const std::vecto
     Level &L = h->lv[l];
     plan.clear();
     for (int s = 0; s < total; s += 2)
-        plan.push_back(PPPass{std::min(2, total - s), 0, nullptr, nullptr, nullptr, nullptr, nullptr});
+        plan.push_back(PPPass{std::min(2, total - s), 0, nullptr, nullptr, nullptr, nullptr, nullptr, false});
     for (int r : res_at) {
         if (r <= 0 || r >= total) { h->err = "internal: face stream residual point"; return PAMG_ERR_STATE; }
         PPPass &q = plan[r / 2];
@@ -1138,8 +1143,8 @@ int face_pp_plan(pamg_handle *h, int l, int total, double *src, const std::vecto
     for (int p = 0; p < P; ++p) {
         plan[p].in = in[p];
         if (p + 1 < P) plan[p].end = in[p + 1];
-        if (plan[p].in == plan[p].end || plan[p].in == plan[p].mid || plan[p].in == plan[p].pre ||
-            plan[p].in == plan[p].end2) {
+        if (plan[p].in && (plan[p].in == plan[p].end || plan[p].in == plan[p].mid || plan[p].in == plan[p].pre ||
+                           plan[p].in == plan[p].end2)) {   // (in null: a start from zero reads nothing)
             h->err = "internal: a face pass writes its own input";
             return PAMG_ERR_STATE;
         }
@@ -1152,12 +1157,14 @@ int face_pp_emit(pamg_handle *h, int l, const PPPass &q) {
     const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
     // iterate and RHS in, the outputs and the residual out (the halo gathers of the neighbours' boundary
     // sub-elements are overhead, not counted)
-    const double by = (48.0 + 24.0 * ((q.pre != nullptr) + (q.mid != nullptr) + (q.end != nullptr) + (q.end2 != nullptr) +
-                                      (q.res != 0))) * (double)L.N + 168.0 * h->U;
+    // (a start from zero reads no iterate; the folded interpolation reads the coarse level's, 6 B per sub-element)
+    const double by = (24.0 * (q.in != nullptr) + 24.0 + (q.interp ? 6.0 : 0.0) +
+                       24.0 * ((q.pre != nullptr) + (q.mid != nullptr) + (q.end != nullptr) + (q.end2 != nullptr) +
+                               (q.res != 0))) * (double)L.N + 168.0 * h->U;
     if (q.res) h->rhsn_valid = false;
     Span sp(h, kid, by);
     HIPCHK(h, launch_face_pp(h->stream, L, q.K, q.in, q.pre, q.mid, q.end, h->p.solver == 3, l == 1, 1 / h->p.dt, q.res,
-                             q.end2));
+                             q.end2, q.interp ? &h->lv[l + 1] : nullptr, false, q.interp));
     return PAMG_OK;
 }
 
@@ -1325,17 +1332,23 @@ bool face_corrected_pp_ok(pamg_handle *h) {
     return false;
 }
 
-// one smoother call of the corrected cycle on level l < L: tnew := the result of n_smooth sweeps from tnew
-int face_corr_call(pamg_handle *h, int l, bool last) {
+// one smoother call of the corrected cycle on level l < L: tnew := the result of n_smooth sweeps from tnew;
+// streaming levels only (face_pp_ok): from_zero -- from a zero iterate (the cycle's memset of a coarse level
+// folded: the first pass reads no iterate), interp -- from tnew plus the prolonged coarse correction (the
+// cycle's interp_add folded into the first pass, which adds it to every value it loads: bitwise the
+// correction stored and read back; the corrected iterate itself is overwritten unread by the call's result)
+int face_corr_call(pamg_handle *h, int l, bool last, bool from_zero = false, bool interp = false) {
     const int ns = h->p.n_smooth;
     if (!face_pp_ok(h, l)) {
+        if (from_zero || interp) { h->err = "internal: a folded face call on a level that does not stream"; return PAMG_ERR_STATE; }
         CHK(smooth_to_tnew(h, l, ns));
         return PAMG_OK;
     }
     h->tnn_level = l;
     h->overlap_static_l1 = false;
     std::vector<PPPass> plan;
-    CHK(face_pp_plan(h, l, ns, h->lv[l].T, {}, last ? 3 : 2, plan));
+    CHK(face_pp_plan(h, l, ns, from_zero ? nullptr : h->lv[l].T, {}, last ? 3 : 2, plan));
+    plan[0].interp = interp;
     for (const PPPass &q : plan) CHK(face_pp_emit(h, l, q));
     return PAMG_OK;
 }
@@ -1360,14 +1373,16 @@ int face_res_restrict(pamg_handle *h, int l, bool last) {
 int vcycle_corrected_face_pp(pamg_handle *h, int n) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     h->overlap_static_l1 = false;
-    // PAMG_FACE_RR=0 (A/B): the residual and the restrictor as their own launches
-    const char *rr_env = getenv("PAMG_FACE_RR");
-    const bool rr = !(rr_env && atoi(rr_env) == 0);
+    // PAMG_FACE_RR=0 (A/B): the residual and the restrictor as their own launches; PAMG_FACE_FOLD=0: a coarse
+    // level's memset and the interpolation as their own launches
+    const char *rr_env = getenv("PAMG_FACE_RR"), *fold_env = getenv("PAMG_FACE_FOLD");
+    const bool rr = !(rr_env && atoi(rr_env) == 0), fold = !(fold_env && atoi(fold_env) == 0);
     for (int c = 0; c < n; ++c) {
         const bool last = c + 1 == n;
         for (int l = 1; l < L; ++l) {
-            if (l > 1) HIPCHK(h, hipMemsetAsync(h->lv[l].T, 0, 3 * (size_t)h->lv[l].pitch * sizeof(double), h->stream));
-            CHK(face_corr_call(h, l, last));
+            const bool fz = l > 1 && fold && face_pp_ok(h, l);
+            if (l > 1 && !fz) HIPCHK(h, hipMemsetAsync(h->lv[l].T, 0, 3 * (size_t)h->lv[l].pitch * sizeof(double), h->stream));
+            CHK(face_corr_call(h, l, last, fz));
             if (rr && face_pp_ok(h, l)) {
                 CHK(face_res_restrict(h, l, last));
             } else {
@@ -1377,8 +1392,16 @@ int vcycle_corrected_face_pp(pamg_handle *h, int n) {
         }
         Level &C = h->lv[L];
         HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));   // from zero
-        CHK(smooth_to_tnew(h, L, ns * h->p.n_coarse));
+        if (fold && ns * h->p.n_coarse > 0 && face_fusable(h, L)) {
+            CHK(face_call(h, L, true, ns * h->p.n_coarse, false, false, true));   // tnew := the result: the final stores
+        } else {
+            CHK(smooth_to_tnew(h, L, ns * h->p.n_coarse));
+        }
         for (int l = L - 1; l >= 1; --l) {
+            if (fold && face_pp_ok(h, l)) {
+                CHK(face_corr_call(h, l, last, false, true));
+                continue;
+            }
             {
                 Span sp(h, PAMG_K_PROLONG, 216.0 * (double)h->lv[l + 1].N);
                 HIPCHK(h, launch_interp_add(h->stream, h->lv[l], h->lv[l + 1]));

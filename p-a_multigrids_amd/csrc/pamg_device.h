@@ -60,6 +60,19 @@ __device__ __forceinline__ double div3(double x) {
     return __builtin_fma(r, t, q0);
 }
 
+// The corrected cycle's correction of child q (0..3) of a coarse sub-element with values y (k_interp_add: the
+// P1 interpolation the prolongator's cascade encodes, splitting.F90:59-88); the one definition the fused
+// forms share, so that each adds the same bits
+__device__ __forceinline__ void interp_corr(int q, const double y[3], double add[3]) {
+    const double m20 = 0.5 * y[2] + 0.5 * y[0], m12 = 0.5 * y[1] + 0.5 * y[2], m01 = 0.5 * y[0] + 0.5 * y[1];
+    switch (q) {
+        case 0: add[0] = m20; add[1] = m12; add[2] = y[2]; break;
+        case 1: add[0] = m12; add[1] = m20; add[2] = m01; break;
+        case 2: add[0] = y[0]; add[1] = m01; add[2] = m20; break;
+        default: add[0] = m01; add[1] = y[1]; add[2] = m12; break;
+    }
+}
+
 struct Stc {
     double c, K[9], w[3];
 };

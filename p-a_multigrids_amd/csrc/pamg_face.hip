@@ -621,14 +621,20 @@ __device__ __forceinline__ void pp_stamp(int i) {
     if (PAMG_STAMPS && g_pp_stamps && threadIdx.x == 0) g_pp_stamps[(int64_t)blockIdx.x * kPPStamps + i] = wall_clock64();
 }
 
-template <int TS, int NT, bool RB, int K>
-__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
+// FOLD: the instance that folds the corrected cycle's interpolation (Tc) or a coarse level's zero start (A null) into
+// its loads -- a template parameter, so that the passes without either keep their registers (the folded loads
+// spilled 52 B per lane in the level-1 two-sweep instance)
+#ifndef PAMG_FACE_PP_FOLD_WAVES
+#define PAMG_FACE_PP_FOLD_WAVES PAMG_FACE_PP_WAVES
+#endif
+template <int TS, int NT, bool RB, int K, bool FOLD = false>
+__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD ? PAMG_FACE_PP_FOLD_WAVES : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, double *out_end2,
     const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
     const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
     const double2 *__restrict__ bcv, const int *__restrict__ cpos, int nup, int64_t pitch, int level1, double rdt,
-    int res, double *RESout, double *RHSc, int64_t pitch_c) {
+    int res, double *RESout, double *RHSc, int64_t pitch_c, const double *__restrict__ Tc) {
     constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
     // red-black: the colour passes run over colour lists (Level::cpos), every lane with an item of the colour
     constexpr int NUP = M * (M + 1) / 2, KU = RB ? (NUP + NT - 1) / NT : PER, KD = RB ? (TS - NUP + NT - 1) / NT : 0;
@@ -680,24 +686,42 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
     const int hq = 3 * ((fu - 1) * M + spu - 1);   // the slot's first word in a snapshot
     int4 ge = make_int4(-1, -1, -1, -1);
     if (gon) ge = gtab[(u * 3 + fu - 1) * M + spu - 1];
+    // the start iterate at global position g: A's value, plus the prolonged coarse correction where Tc is given (the
+    // corrected cycle's interp_add, k_interp_add's arithmetic, folded into the first pass of the smoother call that
+    // follows it), or zero where A is null (a coarse level's call from zero: the cycle's memset folded)
+    auto ldv = [&](int64_t g, double v[3]) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = !FOLD || A ? A[c * pitch + g] : 0.0;
+        if (FOLD && Tc) {
+            const int64_t cg = g >> 2;
+            const double y[3] = {Tc[cg], Tc[pitch_c + cg], Tc[2 * pitch_c + cg]};
+            double add[3];
+            interp_corr((int)(g & 3), y, add);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) v[c] = v[c] + add[c];
+        }
+    };
     double xe[3] = {0.0, 0.0, 0.0}, be[3] = {0.0, 0.0, 0.0}, yv[3][3];
     int4 nbe = make_int4(0, 0, 0, 0);
     if (gon && ge.x >= 0) {
         nbe = fnb[ge.x & (TS - 1)];
+        ldv(ge.x, xe);
+        if (K == 2)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            xe[c] = A[c * pitch + ge.x];
-            if (K == 2) be[c] = RHS[c * pitch + ge.x];
-        }
+            for (int c = 0; c < 3; ++c) be[c] = RHS[c * pitch + ge.x];
         if constexpr (K == 2) {
             const int yy[3] = {ge.y, ge.z, ge.w};
 #pragma unroll
-            for (int fi = 0; fi < 3; ++fi)
+            for (int fi = 0; fi < 3; ++fi) {
+                if (yy[fi] >= 0) {
+                    ldv(yy[fi], yv[fi]);
+                } else {
 #pragma unroll
-                for (int c = 0; c < 3; ++c)
-                    yv[fi][c] = yy[fi] >= 0 ? A[c * pitch + yy[fi]]
-                                : yy[fi] <= -(1 + TS) ? bcpair((-(yy[fi] + 1 + TS)) / 3, (-(yy[fi] + 1 + TS)) % 3 + 1, c)
-                                                      : 0.0;   // this tile's own value: from LDS below
+                    for (int c = 0; c < 3; ++c)
+                        yv[fi][c] = yy[fi] <= -(1 + TS) ? bcpair((-(yy[fi] + 1 + TS)) / 3, (-(yy[fi] + 1 + TS)) % 3 + 1, c)
+                                                        : 0.0;   // this tile's own value: from LDS below
+                }
+            }
         }
     }
     // the thread's items: red-black -- KU up and KD down positions from the colour lists; Jacobi -- its PER
@@ -724,9 +748,18 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : PAMG_
 #pragma unroll
     for (int p = t; p < TS / 2; p += NT) {   // the iterate and the RHS into LDS, adjacent pairs
         const int j = 2 * p;
+        double a0[3] = {0.0, 0.0, 0.0}, a1[3] = {0.0, 0.0, 0.0};
+        if (FOLD && Tc) {   // ldv's correction: both children of the pair share their coarse sub-element
+            const int64_t cg = (s0 + j) >> 2;
+            const double y[3] = {Tc[cg], Tc[pitch_c + cg], Tc[2 * pitch_c + cg]};
+            interp_corr(j & 3, y, a0);
+            interp_corr((j + 1) & 3, y, a1);
+        }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const double2 v = ld2(A + c * pitch + s0 + j), r = BL ? ld2(RHS + c * pitch + s0 + j) : make_double2(0.0, 0.0);
+            double2 v = !FOLD || A ? ld2(A + c * pitch + s0 + j) : make_double2(0.0, 0.0);
+            if (FOLD && Tc) v = make_double2(v.x + a0[c], v.y + a1[c]);
+            const double2 r = BL ? ld2(RHS + c * pitch + s0 + j) : make_double2(0.0, 0.0);
             X[c][j] = v.x;
             X[c][j + 1] = v.y;
             if (BL) {
@@ -1593,11 +1626,14 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
         stamp(3);
     }
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew, the dead last sweep's :550)
+    for (int k = 0; k < PER; ++k) {   // tnew_nonlin (store 2: tnew, the dead last sweep's :550; 3: both)
         const int j = t + NT * k;
         if (j < E && s0 + j < N)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+            for (int c = 0; c < 3; ++c) {
+                if (store != 2) TNN[c * pitch + s0 + j] = X[c][j];
+                if (store >= 2) T[c * pitch + s0 + j] = X[c][j];
+            }
     }
     if (guard) chain_leave(tmo + 1);
 }
@@ -1789,9 +1825,12 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
         });
         if (store == 1 && sw + 2 == run) tstore();   // the last sweep's tnew := tnew_nonlin (its start)
     }
-    for (int j = pa + ln; j < pb; j += 64)   // tnew_nonlin (store 2: tnew, the dead last sweep's :550)
+    for (int j = pa + ln; j < pb; j += 64)   // tnew_nonlin (store 2: tnew, the dead last sweep's :550; 3: both)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) (store == 2 ? T : TNN)[c * pitch + s0 + j] = X[c][j];
+        for (int c = 0; c < 3; ++c) {
+            if (store != 2) TNN[c * pitch + s0 + j] = X[c][j];
+            if (store >= 2) T[c * pitch + s0 + j] = X[c][j];
+        }
     if (guard) chain_leave(tmo + 1);
 }
 
@@ -1931,7 +1970,7 @@ static hipError_t launch_coresident(const void *f, int grid, int nt, void **args
 // k_face_pp: K sweeps of a whole-un_ele-tile level in one launch (face_tile_shape; single domain)
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
                           double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2, const Level *coarse,
-                          bool res_store) {
+                          bool res_store, bool interp) {
     if (L.N == 0) return hipSuccess;
     const int m = L.nsub == 256 ? 16 : L.nsub == 1024 ? 32 : 64;
     if (!face_tile_shape(L) || !L.fnb || !L.gtab || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)) ||
@@ -1942,13 +1981,16 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
     // level is this one's quarter (4 children per coarse sub-element, the same un_eles)
     if (res == 3 && (K != 1 || out_pre || out_end || out_end2 || !coarse || !coarse->RHS || coarse->N * 4 != L.N))
         return hipErrorInvalidValue;
-    if (res != 3 && (coarse || res_store)) return hipErrorInvalidValue;
+    if (res != 3 && (res_store || (coarse != nullptr) != interp)) return hipErrorInvalidValue;
+    // interp: the start iterate in + the prolonged correction of the coarse level's T; in null: a start from zero
+    if ((interp && (res == 3 || !in || !coarse->T || coarse->N * 4 != L.N)) || (!in && res)) return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
     const dim3 g((unsigned)(L.N / L.nsub));
     const int l1 = level1 ? 1 : 0;
     double *R = (res == 1 || res == 2 || res_store) ? L.RES : nullptr;
     double *RC = res == 3 ? coarse->RHS : nullptr;
-    const int64_t pc = res == 3 ? coarse->pitch : 0;
+    const double *TC = interp ? coarse->T : nullptr;
+    const int64_t pc = coarse ? coarse->pitch : 0;
     // PAMG_PP_STAMPS=<file> (a PAMG_STAMPS=1 build): append each launch's per-workgroup phase stamps
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_PP_STAMPS") : nullptr;
     long long *stamps = nullptr;
@@ -1960,10 +2002,13 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
                                                         hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return e;
     }
-#define PAMG_FPP(TS, NT, RB_, K_)                                                                                    \
-    hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, out_end2, L.RHS, \
-                       L.stc,                                                                                         \
-                       L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.cpos, L.nup, L.pitch, l1, rdt, res, R, RC, pc)
+    const bool fold = interp || !in;
+#define PAMG_FPP1(TS, NT, RB_, K_, F_)                                                                                     \
+    hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_, F_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, out_end2, L.RHS, \
+                       L.stc,                                                                                            \
+                       L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.cpos, L.nup, L.pitch, l1, rdt, res, R, RC, pc, TC)
+#define PAMG_FPP(TS, NT, RB_, K_) \
+    do { if (fold) PAMG_FPP1(TS, NT, RB_, K_, true); else PAMG_FPP1(TS, NT, RB_, K_, false); } while (0)
 #define PAMG_FPPK(TS, NT)                                          \
     if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \
     else { if (K == 2) PAMG_FPP(TS, NT, false, 2); else PAMG_FPP(TS, NT, false, 1); }
@@ -1976,6 +2021,7 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
     else return hipErrorInvalidValue;   // (4,096: the iterate and RHS exceed the LDS)
 #undef PAMG_FPPK
 #undef PAMG_FPP
+#undef PAMG_FPP1
     hipError_t e = hipGetLastError();
     if (stamp_path) {
         std::vector<long long> hst(nst);
@@ -2012,7 +2058,9 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
                              int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T,
                              unsigned f0, int guard) {
     if (L.N == 0 || run <= 0) return hipSuccess;
-    if (!face_chain_fits(L.nsub, U, cus) || !L.fnb) return hipErrorInvalidValue;
+    // store 1: tnew := the iterate before the last sweep, tnew_nonlin := the last; 2: tnew := the last (a dead
+    // last sweep); 3: both := the last (the corrected cycle's coarsest call, tnew := tnew_nonlin after it)
+    if (!face_chain_fits(L.nsub, U, cus) || !L.fnb || store < 1 || store > 3) return hipErrorInvalidValue;
     const int g = std::max(1, std::min(cus, U));
     const int k = (U + g - 1) / g;
     const int grid = (U + k - 1) / k;

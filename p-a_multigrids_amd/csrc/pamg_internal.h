@@ -401,7 +401,7 @@ bool face_tile_shape(const Level &L);
 // the start iterate, the iterate after sweep 1, after the last sweep
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
                           double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2 = nullptr,
-                          const Level *coarse = nullptr, bool res_store = false);
+                          const Level *coarse = nullptr, bool res_store = false, bool interp = false);
 // guard: the workgroups check that they are all resident before touching the state; if not, none does and
 // the launch counts an abort in tmo[3] (tmo[1..2] the guard's own words) -- the host runs the call another way
 // the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of

@@ -185,15 +185,9 @@ __global__ __launch_bounds__(kBlock) void k_interp_add(double *T, const double *
     if (f >= 4 * Nc) return;
     const int64_t c = f >> 2;
     const int q = (int)(f & 3);
-    const double y0 = Tc[c], y1 = Tc[pitch_c + c], y2 = Tc[2 * pitch_c + c];
-    const double m20 = 0.5 * y2 + 0.5 * y0, m12 = 0.5 * y1 + 0.5 * y2, m01 = 0.5 * y0 + 0.5 * y1;
+    const double y[3] = {Tc[c], Tc[pitch_c + c], Tc[2 * pitch_c + c]};
     double add[3];
-    switch (q) {   // the P1 interpolation of the prolongator cascade (splitting.F90:59-88)
-        case 0: add[0] = m20; add[1] = m12; add[2] = y2; break;
-        case 1: add[0] = m12; add[1] = m20; add[2] = m01; break;
-        case 2: add[0] = y0; add[1] = m01; add[2] = m20; break;
-        default: add[0] = m01; add[1] = y1; add[2] = m12; break;
-    }
+    interp_corr(q, y, add);   // the P1 interpolation of the prolongator cascade (splitting.F90:59-88)
 #pragma unroll
     for (int i = 0; i < 3; ++i) T[i * pitch_f + f] = T[i * pitch_f + f] + add[i];
 }

@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 5: the corrected face cycle's coarsest call storing tnew itself (no copy): the face tests, the probe A/B
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/r5u; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_face_operator.py > $O/t_face.log 2>&1 || { tail -30 $O/t_face.log; exit 1; }
+tail -1 $O/t_face.log
+for i in 1 2; do
+  for f in 0 1; do
+    PAMG_FACE_FOLD=$f timeout -k 10 200 python scripts/face_probe.py 5 1 > $O/probe_fold${f}_$i.txt 2>&1 || { tail $O/probe_fold${f}_$i.txt; exit 1; }
+    echo "fold=$f rep $i"; grep -v amdgpu.ids $O/probe_fold${f}_$i.txt
+  done
+done
+PAMG_FACE_FOLD=1 timeout -k 10 200 python scripts/face_probe.py 5 0 > $O/probe_c0.txt 2>&1 || { tail $O/probe_c0.txt; exit 1; }
+grep -v amdgpu.ids $O/probe_c0.txt
+echo "all ok"

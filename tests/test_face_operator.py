@@ -297,7 +297,9 @@ def test_face_corrected_cycle_passes_equal_per_step(mesh, S, L, solver, ns, spli
     the fine residual after the cycle only in the call's last cycle) leaves the per-step sequence's state bit
     for bit (bench.py's extra.op1_cycle1 configuration first), and its level-1 calls are the passes. The residual
     and restrictor of a streaming level run as one sweep-less pass (k_face_pp res 3, the residual stored only
-    where the state keeps it); PAMG_FACE_RR=0 keeps them as their own launches -- the same state too."""
+    where the state keeps it), and a streaming level's memset (the call from zero) and interpolation (added to
+    the values the call's first pass loads) fold into its calls; PAMG_FACE_RR=0 / PAMG_FACE_FOLD=0 keep them as
+    their own launches -- the same state every way."""
     import pamg
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
 
@@ -317,8 +319,9 @@ def test_face_corrected_cycle_passes_equal_per_step(mesh, S, L, solver, ns, spli
         monkeypatch.setenv("PAMG_FACE_CORR_PP", "0")
         rs, rov, _, _ = run(split)
         monkeypatch.setenv("PAMG_FACE_CORR_PP", "1")
-        for rr in ("0", "1"):
+        for rr, fold in (("0", "0"), ("1", "0"), ("1", "1")):
             monkeypatch.setenv("PAMG_FACE_RR", rr)
+            monkeypatch.setenv("PAMG_FACE_FOLD", fold)
             gs, gov, issued, nrestrict = run(split)
             assert_identical(gs, rs)
             for x, y in zip(gov, rov):
