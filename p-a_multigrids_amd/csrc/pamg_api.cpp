@@ -1104,7 +1104,15 @@ bool face_pp_ok(pamg_handle *h, int l) {
            (h->p.solver != 3 || L.words_up);
 }
 
-struct PPPass { int K, res; double *in, *pre, *mid, *end, *end2; bool interp = false; };
+// a pass of a face stream (face_pp_plan); rhsc: its residual also restricted into this buffer (res_drop: and not
+// stored), interp: the coarse correction added to its loads (PPCoarse)
+struct PPPass {
+    int K, res;
+    double *in, *pre, *mid, *end, *end2;
+    bool interp = false;
+    double *rhsc = nullptr;
+    bool res_drop = false;
+};
 
 // the passes of a stream of `total` sweeps from src with get_residual after sweep r for each r in res_at
 // (0 < r < total), ending with the final stores fin (1: tnew = the iterate before the last sweep,
@@ -1115,7 +1123,7 @@ int face_pp_plan(pamg_handle *h, int l, int total, double *src, const std::vecto
     Level &L = h->lv[l];
     plan.clear();
     for (int s = 0; s < total; s += 2)
-        plan.push_back(PPPass{std::min(2, total - s), 0, nullptr, nullptr, nullptr, nullptr, nullptr, false});
+        plan.push_back(PPPass{std::min(2, total - s), 0, nullptr, nullptr, nullptr, nullptr, nullptr});
     for (int r : res_at) {
         if (r <= 0 || r >= total) { h->err = "internal: face stream residual point"; return PAMG_ERR_STATE; }
         PPPass &q = plan[r / 2];
@@ -1158,13 +1166,18 @@ int face_pp_emit(pamg_handle *h, int l, const PPPass &q) {
     // iterate and RHS in, the outputs and the residual out (the halo gathers of the neighbours' boundary
     // sub-elements are overhead, not counted)
     // (a start from zero reads no iterate; the folded interpolation reads the coarse level's, 6 B per sub-element)
-    const double by = (24.0 * (q.in != nullptr) + 24.0 + (q.interp ? 6.0 : 0.0) +
+    const double by = (24.0 * (q.in != nullptr) + 24.0 + (q.interp ? 6.0 : 0.0) + (q.rhsc ? 6.0 : 0.0) +
                        24.0 * ((q.pre != nullptr) + (q.mid != nullptr) + (q.end != nullptr) + (q.end2 != nullptr) +
-                               (q.res != 0))) * (double)L.N + 168.0 * h->U;
+                               (q.res != 0 && !q.res_drop))) * (double)L.N + 168.0 * h->U;
     if (q.res) h->rhsn_valid = false;
     Span sp(h, kid, by);
+    PPCoarse pc;
+    pc.coarse = (q.interp || q.rhsc) ? &h->lv[l + 1] : nullptr;
+    pc.rhsc = q.rhsc;
+    pc.res_store = !q.res_drop;
+    pc.interp = q.interp;
     HIPCHK(h, launch_face_pp(h->stream, L, q.K, q.in, q.pre, q.mid, q.end, h->p.solver == 3, l == 1, 1 / h->p.dt, q.res,
-                             q.end2, q.interp ? &h->lv[l + 1] : nullptr, false, q.interp));
+                             q.end2, pc.coarse ? &pc : nullptr));
     return PAMG_OK;
 }
 
@@ -1218,15 +1231,36 @@ int vcycle_face_pp(pamg_handle *h, int n) {
     std::vector<PPPass> plan;
     CHK(face_pp_plan(h, 1, per * n + 1, h->lv[1].T, res_at, 1, plan));
     h->overlap_static_l1 = false;
+    // the restrictor folded into the pass that computes the residual (PAMG_FACE_RR=0: its own launch). The cycle
+    // restricts the PREVIOUS cycle's residual (:336 before :338), so the pass that computes cycle c's residual
+    // restricts it into level 2's second RHS buffer (RHSN_alt, unused by the face cycle) and cycle c + 1 swaps the
+    // two instead of launching the restrictor; that residual is then not stored either (only the restrictor reads
+    // it) -- except the call's last cycle's, which is the state, and which the next call's first cycle restricts
+    const char *rr_env = getenv("PAMG_FACE_RR");
+    Level &L2 = h->lv[2];
+    const bool rf = !(rr_env && atoi(rr_env) == 0) && h->p.multi_levels >= 2 && L2.RHSN_alt;
+    double *const rhs2_home = L2.RHS;
     size_t p = 0;
     for (int c = 0; c < n; ++c) {
         h->tnn_level = 1;
-        CHK(restrict_(h, 1));   // :336 -- level 1's residual of the previous cycle, before this cycle's is written
+        if (c == 0 || !rf) CHK(restrict_(h, 1));   // :336 -- level 1's residual of the previous cycle, before this cycle's is written
+        else std::swap(L2.RHS, L2.RHSN_alt);       // the restriction of it, made by the pass that computed it
         const size_t pr = (size_t)res_at[c] / 2;   // the pass that writes this cycle's residual
-        for (; p <= pr; ++p) CHK(face_pp_emit(h, 1, plan[p]));
+        for (; p <= pr; ++p) {
+            PPPass q = plan[p];
+            if (p == pr && rf && c + 1 < n) {
+                q.rhsc = L2.RHSN_alt;
+                q.res_drop = true;
+            }
+            CHK(face_pp_emit(h, 1, q));
+        }
         CHK(face_pp_level(h, 2, c + 1 == n));
     }
     for (; p < plan.size(); ++p) CHK(face_pp_emit(h, 1, plan[p]));
+    if (L2.RHS != rhs2_home) {   // level 2's RHS back in its own buffer
+        HIPCHK(h, hipMemcpyAsync(L2.RHSN_alt, L2.RHS, 3 * (size_t)L2.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+        std::swap(L2.RHS, L2.RHSN_alt);
+    }
     // the halo the per-step sequence leaves: level 1's last smoother call's words, from its tnew (:555)
     HIPCHK(h, launch_face_words(h->stream, h->lv[1], h->U, h->tov, h->tovo));
     h->tnn_level = 1;
@@ -1365,8 +1399,12 @@ int face_res_restrict(pamg_handle *h, int l, bool last) {
     h->overlap_static_l1 = false;
     const bool store = l > 1 && last;
     Span sp(h, PAMG_K_RESIDUAL, (48.0 + (store ? 24.0 : 0.0)) * (double)L.N + 24.0 * (double)h->lv[l + 1].N + 168.0 * h->U);
+    PPCoarse pc;
+    pc.coarse = &h->lv[l + 1];
+    pc.rhsc = h->lv[l + 1].RHS;
+    pc.res_store = store;
     HIPCHK(h, launch_face_pp(h->stream, L, 1, L.T, nullptr, nullptr, nullptr, h->p.solver == 3, l == 1, 1 / h->p.dt, 3,
-                             nullptr, &h->lv[l + 1], store));
+                             nullptr, &pc));
     return PAMG_OK;
 }
 

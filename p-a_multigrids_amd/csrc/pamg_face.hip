@@ -839,35 +839,24 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
         const int wb = 3 * face_pattern(inb[k]);
         face_apply<MODE>(R, xin, x, bb, inb[k], u, hv, [&](int i) { return MODE == 3 ? 0.0 : WD[wb + i]; }, level1, rdt, r);
     };
-    auto residual = [&](int snap) {   // get_residual (A x - RHS) of the tile's iterate with snapshot snap
-#pragma unroll
-        for (int k = 0; k < KU + KD; ++k) {
-            if (ij[k] < 0) continue;
-            double r[3];
-            item(std::integral_constant<int, 3>{}, k, snap, r);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) RESout[c * pitch + s0 + ij[k]] = r[c];
-        }
-        __syncthreads();   // every read of the iterate before the passes rewrite it
-    };
-    // res 3 (the corrected cycle's residual and restrictor, :336-338, in one pass): get_residual RHS - A x of the
-    // start iterate, and the restrictor of it into the coarse RHS RHSc (k_restrict_tile's: the coarse
-    // sub-element cc of this tile takes component i from child pick_i = 4 cc + {2, 3, 0}[i], the mean of that
-    // child's three residual components, in k_restrict_tile's order) -- so child 4 cc + 1 is not evaluated unless
-    // the residual itself is stored (RESout: a level whose residual is read after the call)
-    auto residual_restrict = [&]() {
+    // get_residual of the tile's iterate with snapshot snap: MODE 3 A x - RHS (res 1 / 2, the reference cycle's), 4
+    // RHS - A x (res 3, the corrected cycle's). Stored into RESout where given; restricted into RHSc where given
+    // (k_restrict_tile's restrictor: the coarse sub-element cc of this tile takes component i from child pick_i =
+    // 4 cc + {2, 3, 0}[i], the mean of that child's three residual components, in k_restrict_tile's order -- so
+    // each item writes its coarse value itself, and child 4 cc + 1 is not evaluated unless RESout is stored)
+    auto residual = [&](auto mc, int snap) {
         const int64_t c0 = s0 >> 2;
 #pragma unroll
         for (int k = 0; k < KU + KD; ++k) {
             const int j = ij[k];
             if (j < 0 || (!RESout && (j & 3) == 1)) continue;
             double r[3];
-            item(std::integral_constant<int, 4>{}, k, 0, r);
+            item(mc, k, snap, r);
             if (RESout)
 #pragma unroll
                 for (int c = 0; c < 3; ++c) RESout[c * pitch + s0 + j] = r[c];
             const int q = j & 3;
-            if (q != 1) RHSc[(q == 2 ? 0 : q == 3 ? 1 : 2) * pitch_c + c0 + (j >> 2)] = div3(r[0] + r[1] + r[2]);
+            if (RHSc && q != 1) RHSc[(q == 2 ? 0 : q == 3 ? 1 : 2) * pitch_c + c0 + (j >> 2)] = div3(r[0] + r[1] + r[2]);
         }
     };
     auto sweep = [&](int snap) {
@@ -912,16 +901,22 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
             for (int c = 0; c < 3; ++c) st2(o + c * pitch + s0 + j, make_double2(X[c][j], X[c][j + 1]));
         }
     };
-    if (res == 3) {   // get_residual (RHS - A x) restricted: no sweep, no stores of the iterate
-        residual_restrict();
+    if (res == 3) {   // the corrected cycle's get_residual and restrictor (:336-338): no sweep, no stores of the iterate
+        residual(std::integral_constant<int, 4>{}, 0);
         return;
     }
-    if (res == 1) residual(0);
+    if (res == 1) {
+        residual(std::integral_constant<int, 3>{}, 0);
+        __syncthreads();   // every read of the iterate before the passes rewrite it
+    }
     sweep(0);
     pp_stamp(3);
     if constexpr (K == 2) {
         if (out_mid) store(out_mid);
-        if (res == 2) residual(1);
+        if (res == 2) {
+            residual(std::integral_constant<int, 3>{}, 1);
+            __syncthreads();
+        }
         sweep(1);
     }
     pp_stamp(4);
@@ -1969,28 +1964,31 @@ static hipError_t launch_coresident(const void *f, int grid, int nt, void **args
 
 // k_face_pp: K sweeps of a whole-un_ele-tile level in one launch (face_tile_shape; single domain)
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
-                          double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2, const Level *coarse,
-                          bool res_store, bool interp) {
+                          double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2, const PPCoarse *pcx) {
     if (L.N == 0) return hipSuccess;
     const int m = L.nsub == 256 ? 16 : L.nsub == 1024 ? 32 : 64;
     if (!face_tile_shape(L) || !L.fnb || !L.gtab || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)) ||
         (out_end2 && (out_end2 == in || !out_end)) ||
         (rb && (!L.cpos || L.nup != m * (m + 1) / 2)))
         return hipErrorInvalidValue;
-    // res 3: the residual restricted into the coarse RHS, one sweep-less pass (K 1, no iterate outputs); the coarse
-    // level is this one's quarter (4 children per coarse sub-element, the same un_eles)
-    if (res == 3 && (K != 1 || out_pre || out_end || out_end2 || !coarse || !coarse->RHS || coarse->N * 4 != L.N))
+    // the coarse level (pcx): this one's quarter, the same un_eles, 4 children per coarse sub-element
+    const Level *C = pcx ? pcx->coarse : nullptr;
+    if (pcx && (!C || C->N * 4 != L.N)) return hipErrorInvalidValue;
+    const bool interp = pcx && pcx->interp;
+    double *RC = pcx ? pcx->rhsc : nullptr;
+    // res 3: the residual restricted into the coarse RHS, one sweep-less pass (K 1, no iterate outputs); a
+    // restriction needs a residual; interp: the start iterate in + the prolonged correction of the coarse level's T;
+    // in null: a start from zero
+    if ((res == 3 && (K != 1 || out_pre || out_end || out_end2 || !RC)) || (RC && !res) ||
+        (interp && (res == 3 || !in || !C->T)) || (!in && res))
         return hipErrorInvalidValue;
-    if (res != 3 && (res_store || (coarse != nullptr) != interp)) return hipErrorInvalidValue;
-    // interp: the start iterate in + the prolonged correction of the coarse level's T; in null: a start from zero
-    if ((interp && (res == 3 || !in || !coarse->T || coarse->N * 4 != L.N)) || (!in && res)) return hipErrorInvalidValue;
     const HaloPlan &P = L.halo;
     const dim3 g((unsigned)(L.N / L.nsub));
     const int l1 = level1 ? 1 : 0;
-    double *R = (res == 1 || res == 2 || res_store) ? L.RES : nullptr;
-    double *RC = res == 3 ? coarse->RHS : nullptr;
-    const double *TC = interp ? coarse->T : nullptr;
-    const int64_t pc = coarse ? coarse->pitch : 0;
+    double *R = res && (!pcx || pcx->res_store) ? L.RES : nullptr;
+    if (res && !R && !RC) return hipErrorInvalidValue;
+    const double *TC = interp ? C->T : nullptr;
+    const int64_t pc = C ? C->pitch : 0;
     // PAMG_PP_STAMPS=<file> (a PAMG_STAMPS=1 build): append each launch's per-workgroup phase stamps
     static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_PP_STAMPS") : nullptr;
     long long *stamps = nullptr;

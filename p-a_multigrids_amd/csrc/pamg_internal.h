@@ -399,9 +399,18 @@ bool face_tile_shape(const Level &L);
 // from it, the second sweep's computed in the launch); res 1 / 2: get_residual into L.RES of the start
 // iterate / the iterate after the first sweep; out_pre / out_mid / out_end (any may be null, none `in`):
 // the start iterate, the iterate after sweep 1, after the last sweep
+// k_face_pp's folds of the coarse level (launch_face_pp): rhsc -- the pass's residual restricted into this buffer (the
+// coarse level's layout), res_store -- the residual itself stored too (L.RES), interp -- the coarse level's T
+// prolonged and added to every value the pass loads
+struct PPCoarse {
+    const Level *coarse = nullptr;
+    double *rhsc = nullptr;
+    bool res_store = true;
+    bool interp = false;
+};
 hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in, double *out_pre, double *out_mid,
                           double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2 = nullptr,
-                          const Level *coarse = nullptr, bool res_store = false, bool interp = false);
+                          const PPCoarse *pc = nullptr);
 // guard: the workgroups check that they are all resident before touching the state; if not, none does and
 // the launch counts an abort in tmo[3] (tmo[1..2] the guard's own words) -- the host runs the call another way
 // the persistent chain of one face-operator smoother call (single domain; face_chain_fits): `run` of

@@ -232,27 +232,37 @@ def test_face_two_sweep_passes_equal_one_sweep_launches(mesh, S, L, solver, ns, 
     second sweep's halo computed in the launch from the neighbours' boundary sub-elements and their down
     neighbours; level 1 one stream over the call's cycles) leaves the state of the one-sweep launches, bit
     for bit -- levels of 256, 1,024 and 4,096 sub-elements per un_ele, red-black and Jacobi, odd and even
-    stream lengths, residuals at a pass's start and in its middle, calls split over time steps."""
+    stream lengths, residuals at a pass's start and in its middle, calls split over time steps. Level 1's
+    restrictor is folded into the pass that computes the residual it restricts (the next cycle's level-2 RHS, the
+    cycle's residual itself stored only in the call's last cycle; PAMG_FACE_RR=0 keeps its own launch): both
+    forms, the same state; with the fold, level 1's restrictor is launched once per call."""
     import pamg
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
 
     def run(split):
         g = pamg.SemiImplicitIterative(m, S, L, n_smooth=ns, solver=solver, op=1)
+        g.timing_enable(8)   # PAMG_K_RESTRICT
+        g.timing_reset()
         for n in split:
             g.begin_timestep()
             g.vcycle(n)
         st, ov = g.state(), g.overlap()
+        nr = g.timing()["restrict"]["issued"]
         g.close()
-        return st, ov
+        return st, ov, nr
 
     for split in splits:
         monkeypatch.setenv("PAMG_FACE_PP", "0")
-        rs, rov = run(split)
+        rs, rov, nr0 = run(split)
         monkeypatch.setenv("PAMG_FACE_PP", "3")   # both level sizes that can stream
-        gs, gov = run(split)
-        assert_identical(gs, rs)
-        for x, y in zip(gov, rov):
-            np.testing.assert_array_equal(x, y)
+        for rr in ("0", "1"):
+            monkeypatch.setenv("PAMG_FACE_RR", rr)
+            gs, gov, nr = run(split)
+            assert_identical(gs, rs)
+            for x, y in zip(gov, rov):
+                np.testing.assert_array_equal(x, y)
+            if rr == "1" and 4 ** S in (256, 1024) and L >= 2 and ns >= 2:   # level 1 streams
+                assert nr == nr0 - (sum(split) - len(split)), (nr, nr0, split)
 
 
 @pytest.mark.gpu
