@@ -1648,6 +1648,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 // bitwise k_face_chain (tests/test_face_operator.py). Needs every halo sub-element to be an up one
 // (words_up) and q un_eles' colour lists in 64 lanes (level 3 at n_split = 5: 2 x 15, 2 x 21, 2 x 28).
 constexpr int kPW = kChainNT / 64;   // waves of a chain workgroup
+constexpr int kPWStamps = 6;         // per-wave phase stamps a sweep (PAMG_CHAIN_STAMPS)
 __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double *TNN, const double *SRC,
                                                                const double *__restrict__ RHS,
                                                                const double *__restrict__ stc, const int4 *__restrict__ fnb,
@@ -1661,7 +1662,6 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                                                                long long *stamps, int guard) {
     (void)omega;
     (void)early;
-    (void)stamps;
     if (guard && !chain_enter(tmo + 1, tmo + 3)) {   // not co-resident: leave the state to the host's fallback
         chain_leave(tmo + 1);
         return;
@@ -1739,6 +1739,11 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
         double *tout = sw + 1 < total ? (((total - 2 - sw) & 1) ? buf1 : buf0) : nullptr;
+        // PAMG_CHAIN_STAMPS: per-wave phase stamps of workgroups 0..7 (kPWStamps a sweep)
+        auto stamp = [&](int i) {
+            if (stamps && ln == 0 && w < 8) stamps[(((int64_t)w * kPW + v) * run + sw) * kPWStamps + i] = wall_clock64();
+        };
+        stamp(0);
         // opaque per sweep (as k_face_chain's): the items stay in their registers instead of being
         // rematerialized or hoisted around the passes
         asm volatile("" : "+v"(I0.j[0]), "+v"(I0.nb[0].x), "+v"(I0.nb[0].y), "+v"(I0.nb[0].z), "+v"(I0.nb[0].w));
@@ -1751,6 +1756,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
 #pragma unroll
             for (int c = 0; c < 3; ++c) X[c][I0.j[0]] = r[c];
         });
+        stamp(1);
         if (sw > 0) {   // every wave of this and of the neighbouring workgroups has published sweep sw - 1
             const int tot = (nn + 1) * kPW;
             for (int base = 0; base < tot; base += 64) {
@@ -1773,6 +1779,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                 }
             }
         }
+        stamp(2);
         // the snapshot of the wave's un_eles (sc1: through to the coherent level)
         if (snap_pre) {   // at most two 16-byte loads a lane, their offsets computed once for the call
             asm volatile("" : "+v"(so[0]), "+v"(so[1]));
@@ -1800,6 +1807,10 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                 HI[idx] = ld_coh(tin + (u0 + uk) * slots * 3 + (int64_t)mf * slots + off);
             }
         }
+        if (stamps) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            stamp(3);
+        }
         // the ups with words, their next-sweep words written through at once
         HaloArgs Hn = H;
         Hn.tov = tout;
@@ -1814,10 +1825,15 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                 __hip_atomic_store((g_u32 *)flags + (size_t)w * kPW + v, f0 + (unsigned)(sw + 1), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
+        stamp(4);
         items_pass<1>(ID, ixin, ihv, irec, level1, rdt, [&](int, const double r[3]) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) X[c][ID.j[0]] = r[c];
         });
+        if (stamps) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            stamp(5);
+        }
         if (store == 1 && sw + 2 == run) tstore();   // the last sweep's tnew := tnew_nonlin (its start)
     }
     for (int j = pa + ln; j < pb; j += 64)   // tnew_nonlin (store 2: tnew, the dead last sweep's :550; 3: both)
@@ -2074,7 +2090,10 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     // PAMG_CHAIN_STAMPS=<file>: append every launch's per-sweep phase stamps of workgroups 0..7
     static const char *stamp_path = getenv("PAMG_CHAIN_STAMPS");
     long long *stamps = nullptr;
-    const size_t nst = (size_t)8 * run * 4;
+    // the per-wave chain stamps every wave of workgroups 0..7 (kPWStamps a sweep), the workgroup chain
+    // thread 0 of each (4 a sweep); the header's sign tells them apart
+    const size_t nst_pw = (size_t)8 * kPW * run * kPWStamps;
+    const size_t nst = std::max((size_t)8 * run * 4, nst_pw);
     if (stamp_path) {
         hipError_t e = hipMalloc(&stamps, nst * sizeof(long long));
         if (e != hipSuccess) return e;
@@ -2110,7 +2129,7 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     // workgroup form (read per launch: a test switches it within a process)
     const char *pw_env = getenv("PAMG_CHAIN_PW");
     const int qpw = (k + kPW - 1) / kPW;
-    if (!(pw_env && atoi(pw_env) == 0) && rb && lrec && early == 3 && !stamp_path && uni && L.nsub <= 64 &&
+    if (!(pw_env && atoi(pw_env) == 0) && rb && lrec && early == 3 && uni && L.nsub <= 64 &&
         qpw * std::max(nui, std::max(L.nup - nui, L.ndn)) <= 64)
         f = (const void *)k_face_chain_pw;
     hipError_t e = launch_coresident(f, grid, kChainNT, args, s);
@@ -2120,9 +2139,10 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
         if (e == hipSuccess) e = hipMemcpy(h.data(), stamps, nst * sizeof(long long), hipMemcpyDeviceToHost);
         (void)hipFree(stamps);
         if (FILE *fp = fopen(stamp_path, "ab")) {
-            const long long hdr[4] = {run, grid, E, L.nsub};
+            const bool pw = f == (const void *)k_face_chain_pw;
+            const long long hdr[4] = {pw ? -run : run, grid, E, L.nsub};
             fwrite(hdr, sizeof hdr, 1, fp);
-            fwrite(h.data(), sizeof(long long), nst, fp);
+            fwrite(h.data(), sizeof(long long), pw ? nst_pw : (size_t)8 * run * 4, fp);
             fclose(fp);
         }
     }
