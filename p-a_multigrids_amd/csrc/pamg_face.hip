@@ -1648,7 +1648,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
 // bitwise k_face_chain (tests/test_face_operator.py). Needs every halo sub-element to be an up one
 // (words_up) and q un_eles' colour lists in 64 lanes (level 3 at n_split = 5: 2 x 15, 2 x 21, 2 x 28).
 constexpr int kPW = kChainNT / 64;   // waves of a chain workgroup
-constexpr int kPWStamps = 6;         // per-wave phase stamps a sweep (PAMG_CHAIN_STAMPS)
+constexpr int kPWStamps = 7;         // per-wave phase stamps a sweep (PAMG_CHAIN_STAMPS)
 __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double *TNN, const double *SRC,
                                                                const double *__restrict__ RHS,
                                                                const double *__restrict__ stc, const int4 *__restrict__ fnb,
@@ -1661,17 +1661,32 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                                                                int nup, int nui, int early, unsigned f0, int snap_ok,
                                                                long long *stamps, int guard) {
     (void)omega;
-    (void)early;
     if (guard && !chain_enter(tmo + 1, tmo + 3)) {   // not co-resident: leave the state to the host's fallback
         chain_leave(tmo + 1);
         return;
     }
     constexpr int NT = kChainNT;
-    __shared__ double X[3][NT * kChainPer];
-    __shared__ double HI[kChainHalo];
-    __shared__ double RS[kChainRec * kRecW];
+    // one LDS image: the iterate planes (X), the halo snapshot (HI), the records (RS) and a zero word, so that an
+    // item's operands are one index each (pw_face below)
+    constexpr int XP = NT * kChainPer, OHI = 3 * XP, ORS = OHI + kChainHalo, OZ = ORS + kChainRec * kRecW;
+    static_assert(OZ < (1 << 15), "15-bit operand indices");
+    __shared__ double LM[OZ + 1];
+    __shared__ unsigned wgc, wgready, wgpoll;   // the workgroup's published waves, ready sweep, polling claim
     const int t = threadIdx.x, w = blockIdx.x;
     const int v = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+    // flags (early bits 32 / 64; PAMG_CHAIN_WGFLAG, default 2): 0 one flag per wave (flags[16 w + v]), a wave
+    // polls the 16 (nn + 1) flags of its own and the neighbouring workgroups; 1 one flag per workgroup
+    // (flags[16 w]), stored by the last of its 16 waves to publish -- each wave drains its words, then adds to
+    // the LDS counter wgc, the last arriver stores the flag (Guideline 16 R1's counter form) -- and a wave polls
+    // nn + 1 flags; 2 as 1, with one wave of the workgroup polling (the first to arrive, claimed in wgpoll) and
+    // the others waiting on its LDS word wgready
+    const bool wgflag = (early & 32) != 0, leader_poll = (early & 64) != 0;
+    if (t == 0) {
+        wgc = 0;
+        wgready = 0;
+        wgpoll = 0;
+        LM[OZ] = 0.0;
+    }
     const int64_t s0 = (int64_t)w * E;
     const int64_t nsm = (1ll << nsub_log2) - 1;
     const int m = H.m, ke = E >> nsub_log2;
@@ -1680,7 +1695,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
     const int q = (ke + kPW - 1) / kPW;                  // un_eles per wave
     const int ua = std::min(kv, v * q), ub = std::min(kv, ua + q);   // this wave's un_eles [ua, ub)
     const int nsub = 1 << nsub_log2, ndn = nsub - nup, n1 = nup - nui;
-    chain_load_recs(RS, stc, fface, fsx, u0, kv, t, NT);   // the un_eles' records
+    chain_load_recs(LM + ORS, stc, fface, fsx, u0, kv, t, NT);   // the un_eles' records
     // the lane's items: 0 an up sub-element without halo words, 1 one with words, D a down one
     Items<1> I0, I1, ID;
     auto mk = [&](Items<1> &I, int n, int o) {
@@ -1707,16 +1722,79 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
     const int pa = ua << nsub_log2, pb = ub << nsub_log2;   // the wave's tile positions
     for (int j = pa + ln; j < pb; j += 64)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) X[c][j] = SRC[c * pitch + s0 + j];
+        for (int c = 0; c < 3; ++c) LM[c * XP + j] = SRC[c * pitch + s0 + j];
     __syncthreads();   // the records
-    auto ixin = [&](int c, int qq) { return X[c][qq]; };
-    auto ihv = [&](int64_t uu, int mf, int sp, int kk) { return HI[(((int)(uu - u0) * 3 + mf - 1) * m + sp - 1) * 3 + kk]; };
-    auto nohv = [](int64_t, int, int, int) { return 0.0; };
-    auto irec = [&](int j, int4 nb, auto &&f) { chain_rec(RS, j, nb, nsub_log2, u0, f); };
+    // An item's operands, fixed for the call: per sub-element face fi the LM indices of the two values face_apply
+    // reads there (ya, yb: the inner neighbour's components fnode(fi, 1), fnode(fi, 0), or the halo snapshot's
+    // selected words, or the zero word for a coarse level's homogeneous boundary) and whether the face is inner,
+    // packed 15 + 15 + 1 bits -- so a pass issues every LDS read of its item at once instead of a branch per face
+    // with its own reads and waits (the item-1 pass is on the chain's critical path). face_apply's arithmetic on
+    // the same values in the same order: bitwise (tests/test_face_operator.py).
+    auto pack = [&](const Items<1> &I, unsigned P[3]) {
+        const int j = I.j[0] < 0 ? 0 : I.j[0], uk = j >> nsub_log2, jb = uk << nsub_log2;
+        const int nbf[3] = {I.nb[0].x, I.nb[0].y, I.nb[0].z};
+#pragma unroll
+        for (int fi = 0; fi < 3; ++fi) {
+            const int a = fnode(fi, 0), bb = fnode(fi, 1);
+            int ia, ib;
+            if (nbf[fi] >= 0) {
+                ia = bb * XP + jb + nbf[fi];
+                ib = a * XP + jb + nbf[fi];
+            } else {
+                const int sx = (int)LM[ORS + uk * kRecW + 43 + fi];
+                const int h = OHI + ((uk * 3 + fmface(fi) - 1) * m - nbf[fi] - 1) * 3;
+                if (!level1 && (sx & 16)) ia = ib = OZ;
+                else {
+                    ia = h + (sx & 3) - 1;
+                    ib = h + ((sx >> 2) & 3) - 1;
+                }
+            }
+            P[fi] = (unsigned)ia | ((unsigned)ib << 15) | ((nbf[fi] >= 0 ? 1u : 0u) << 30);
+        }
+    };
+    unsigned P0[3], P1[3], PD[3];
+    pack(I0, P0);
+    pack(I1, P1);
+    pack(ID, PD);
+    // one item: face_apply<0 / 1> (the smoother update) of tile position j from its record, its packed operands
+    auto pw_face = [&](int j, const unsigned P[3], const double b[3], double r[3]) {
+        const double *rs = LM + ORS + (j >> nsub_log2) * kRecW;
+        double x[3], y[3][2], wf[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c] = LM[c * XP + j];
+#pragma unroll
+        for (int fi = 0; fi < 3; ++fi) {
+            y[fi][0] = LM[P[fi] & 32767];
+            y[fi][1] = LM[(P[fi] >> 15) & 32767];
+        }
+        Stc S;
+        S.c = rs[0];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) S.K[k] = rs[1 + k];
+        const int pat = (int)((P[0] >> 30) | ((P[1] >> 30) << 1) | ((P[2] >> 30) << 2));
+#pragma unroll
+        for (int fi = 0; fi < 3; ++fi) wf[fi] = (P[fi] >> 30) ? rs[13 + fi] : rs[13 + 3 + fmface(fi) - 1];
+        const double *wd = rs + 19 + 3 * pat;
+        double A[3];
+        apply_A(S, rdt, x, A);
+        double ds[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int fi = 0; fi < 3; ++fi) {
+            const int a = fnode(fi, 0), bb = fnode(fi, 1);
+            const double ya = y[fi][0], yb = y[fi][1];
+            ds[a] = ds[a] + wf[fi] * (((2.0 * x[a] + x[bb]) - 2.0 * ya) - yb);
+            ds[bb] = ds[bb] + wf[fi] * (((x[a] + 2.0 * x[bb]) - ya) - 2.0 * yb);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double ai = A[i] + ds[i];
+            r[i] = x[i] + wd[i] * (b[i] - ai);
+        }
+    };
     auto tstore = [&]() {
         for (int j = pa + ln; j < pb; j += 64)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = X[c][j];
+            for (int c = 0; c < 3; ++c) T[c * pitch + s0 + j] = LM[c * XP + j];
     };
     if (store == 1 && run == 1) tstore();
     const int64_t tin_bytes64 = (N >> nsub_log2) * slots * 3 * 8;
@@ -1736,6 +1814,24 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
             const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
             so[it] = (int)(((u0 + uk) * slots * 3 + (int64_t)mf * slots + off) * 8);
         }
+    // poll flags f[0 .. n) (lane i one) until each is >= want; bounded (the give-up word tmo)
+    auto poll = [&](int n, auto &&flag_of, unsigned want) {
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + ln;
+            const unsigned *f = i < n ? flag_of(i) : nullptr;
+            bool ok = f == nullptr;
+            for (unsigned spins = 0;; ++spins) {
+                if (!ok) ok = __hip_atomic_load((g_u32 *)const_cast<unsigned *>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+                if (__all(ok)) break;
+                if (spins > (1u << 22)) {
+                    if (ln == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    };
+    auto wg_flag = [&](int i) { return flags + (size_t)(i == 0 ? w : nb_list[na + i - 1]) * kPW; };
     for (int sw = 0; sw < run; ++sw) {
         const double *tin = ((total - 1 - sw) & 1) ? buf1 : buf0;
         double *tout = sw + 1 < total ? (((total - 2 - sw) & 1) ? buf1 : buf0) : nullptr;
@@ -1746,39 +1842,44 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
         stamp(0);
         // opaque per sweep (as k_face_chain's): the items stay in their registers instead of being
         // rematerialized or hoisted around the passes
-        asm volatile("" : "+v"(I0.j[0]), "+v"(I0.nb[0].x), "+v"(I0.nb[0].y), "+v"(I0.nb[0].z), "+v"(I0.nb[0].w));
-        asm volatile("" : "+v"(I1.j[0]), "+v"(I1.nb[0].x), "+v"(I1.nb[0].y), "+v"(I1.nb[0].z), "+v"(I1.nb[0].w));
-        asm volatile("" : "+v"(ID.j[0]), "+v"(ID.nb[0].x), "+v"(ID.nb[0].y), "+v"(ID.nb[0].z), "+v"(ID.nb[0].w));
+        asm volatile("" : "+v"(I0.j[0]), "+v"(P0[0]), "+v"(P0[1]), "+v"(P0[2]));
+        asm volatile("" : "+v"(I1.j[0]), "+v"(P1[0]), "+v"(P1[1]), "+v"(P1[2]));
+        asm volatile("" : "+v"(ID.j[0]), "+v"(PD[0]), "+v"(PD[1]), "+v"(PD[2]));
         asm volatile("" : "+v"(hq));
 #pragma unroll
         for (int f = 0; f < 3; ++f) asm volatile("" : "+v"(hr[f].x), "+v"(hr[f].y), "+v"(hr[f].z));
-        items_pass<0>(I0, ixin, nohv, irec, level1, rdt, [&](int, const double r[3]) {
+        if (I0.j[0] >= 0) {
+            double r[3];
+            pw_face(I0.j[0], P0, I0.b[0], r);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) X[c][I0.j[0]] = r[c];
-        });
+            for (int c = 0; c < 3; ++c) LM[c * XP + I0.j[0]] = r[c];
+        }
         stamp(1);
-        if (sw > 0) {   // every wave of this and of the neighbouring workgroups has published sweep sw - 1
-            const int tot = (nn + 1) * kPW;
-            for (int base = 0; base < tot; base += 64) {
-                const int i = base + ln;
-                const unsigned *f = nullptr;
-                if (i < tot) {
-                    const int g = i / kPW;
-                    f = flags + (size_t)(g == 0 ? w : nb_list[na + g - 1]) * kPW + (i - g * kPW);
-                }
-                bool ok = f == nullptr;
-                for (unsigned spins = 0;; ++spins) {
-                    if (!ok) ok = __hip_atomic_load((g_u32 *)const_cast<unsigned *>(f), __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) >= f0 + (unsigned)sw;
-                    if (__all(ok)) break;
-                    if (spins > (1u << 22)) {
-                        if (ln == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
+        if (sw > 0 && wgflag && leader_poll) {   // one wave polls the workgroup flags, the others its LDS word
+            if (__hip_atomic_load(&wgready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)sw) {
+                unsigned old = 0;
+                if (ln == 0) old = __hip_atomic_fetch_max(&wgpoll, (unsigned)sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = __builtin_amdgcn_readfirstlane(old);
+                if (old < (unsigned)sw) {
+                    poll(nn + 1, wg_flag, f0 + (unsigned)sw);
+                    if (ln == 0) __hip_atomic_fetch_max(&wgready, (unsigned)sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    for (unsigned spins = 0;; ++spins) {
+                        if (__hip_atomic_load(&wgready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (unsigned)sw) break;
+                        if (spins > (1u << 24)) {   // the poller gives up after 2^22 polls and still releases this word
+                            if (ln == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
                     }
-                    __builtin_amdgcn_s_sleep(2);
                 }
             }
+        } else if (sw > 0 && wgflag) {   // the workgroup flags of this and of the neighbouring workgroups
+            poll(nn + 1, wg_flag, f0 + (unsigned)sw);
+        } else if (sw > 0) {   // every wave of this and of the neighbouring workgroups has published sweep sw - 1
+            poll((nn + 1) * kPW, [&](int i) { const int g = i / kPW; return wg_flag(g) + (i - g * kPW); }, f0 + (unsigned)sw);
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: the snapshot loads stay below the wait
         stamp(2);
         // the snapshot of the wave's un_eles (sc1: through to the coherent level)
         if (snap_pre) {   // at most two 16-byte loads a lane, their offsets computed once for the call
@@ -1789,8 +1890,8 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                 if (so[it] < 0) continue;
                 const int idx = ha + 2 * ln + 128 * it;
                 const v4u val = __builtin_amdgcn_raw_buffer_load_b128(rs, so[it], 0, kAuxSc1);
-                HI[idx] = __longlong_as_double(((long long)val.y << 32) | val.x);
-                HI[idx + 1] = __longlong_as_double(((long long)val.w << 32) | val.z);
+                LM[OHI + idx] = __longlong_as_double(((long long)val.y << 32) | val.x);
+                LM[OHI + idx + 1] = __longlong_as_double(((long long)val.w << 32) | val.z);
             }
         } else if (snap16) {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(tin), (short)0, tin_bytes, 0x00020000);
@@ -1798,13 +1899,13 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                 const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
                 const int o = (int)(((u0 + uk) * slots * 3 + (int64_t)mf * slots + off) * 8);
                 const v4u val = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kAuxSc1);
-                HI[idx] = __longlong_as_double(((long long)val.y << 32) | val.x);
-                HI[idx + 1] = __longlong_as_double(((long long)val.w << 32) | val.z);
+                LM[OHI + idx] = __longlong_as_double(((long long)val.y << 32) | val.x);
+                LM[OHI + idx + 1] = __longlong_as_double(((long long)val.w << 32) | val.z);
             }
         } else {
             for (int idx = ha + ln; idx < hb; idx += 64) {
                 const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
-                HI[idx] = ld_coh(tin + (u0 + uk) * slots * 3 + (int64_t)mf * slots + off);
+                LM[OHI + idx] = ld_coh(tin + (u0 + uk) * slots * 3 + (int64_t)mf * slots + off);
             }
         }
         if (stamps) {
@@ -1812,35 +1913,51 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
             stamp(3);
         }
         // the ups with words, their next-sweep words written through at once
-        HaloArgs Hn = H;
-        Hn.tov = tout;
-        items_pass<0>(I1, ixin, ihv, irec, level1, rdt, [&](int, const double r[3]) {
+        if (I1.j[0] >= 0) {
+            double r[3];
+            pw_face(I1.j[0], P1, I1.b[0], r);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) X[c][I1.j[0]] = r[c];
-            if (tout) halo_words<true>(Hn, hr, hq, r, sw == 0);
-        });
-        if (tout) {   // drained, then this wave's flag
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (ln == 0)
-                __hip_atomic_store((g_u32 *)flags + (size_t)w * kPW + v, f0 + (unsigned)(sw + 1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            for (int c = 0; c < 3; ++c) LM[c * XP + I1.j[0]] = r[c];
+            if (tout) {
+                HaloArgs Hn = H;
+                Hn.tov = tout;
+                halo_words<true>(Hn, hr, hq, r, sw == 0);
+            }
         }
-        stamp(4);
-        items_pass<1>(ID, ixin, ihv, irec, level1, rdt, [&](int, const double r[3]) {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) X[c][ID.j[0]] = r[c];
-        });
         if (stamps) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            stamp(5);
+            stamp(4);
+        }
+        if (tout) {   // drained, then this wave's flag (wgflag: the workgroup's, by its last wave)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (wgflag) {
+                if (ln == 0 && __hip_atomic_fetch_add(&wgc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1 ==
+                                   (unsigned)kPW * (unsigned)(sw + 1))
+                    __hip_atomic_store((g_u32 *)flags + (size_t)w * kPW, f0 + (unsigned)(sw + 1), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            } else if (ln == 0) {
+                __hip_atomic_store((g_u32 *)flags + (size_t)w * kPW + v, f0 + (unsigned)(sw + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        stamp(5);
+        if (ID.j[0] >= 0) {
+            double r[3];
+            pw_face(ID.j[0], PD, ID.b[0], r);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) LM[c * XP + ID.j[0]] = r[c];
+        }
+        if (stamps) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            stamp(6);
         }
         if (store == 1 && sw + 2 == run) tstore();   // the last sweep's tnew := tnew_nonlin (its start)
     }
     for (int j = pa + ln; j < pb; j += 64)   // tnew_nonlin (store 2: tnew, the dead last sweep's :550; 3: both)
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            if (store != 2) TNN[c * pitch + s0 + j] = X[c][j];
-            if (store >= 2) T[c * pitch + s0 + j] = X[c][j];
+            if (store != 2) TNN[c * pitch + s0 + j] = LM[c * XP + j];
+            if (store >= 2) T[c * pitch + s0 + j] = LM[c * XP + j];
         }
     if (guard) chain_leave(tmo + 1);
 }
@@ -2132,6 +2249,13 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     if (!(pw_env && atoi(pw_env) == 0) && rb && lrec && early == 3 && uni && L.nsub <= 64 &&
         qpw * std::max(nui, std::max(L.nup - nui, L.ndn)) <= 64)
         f = (const void *)k_face_chain_pw;
+    // PAMG_CHAIN_WGFLAG (the per-wave chain's flags, read per launch): 0 one flag per wave, 1 one per workgroup
+    // stored by its last wave to publish, 2 (default) as 1 with one polling wave per workgroup
+    // (profiles/r05_y_chain_wgflag.txt, r05_z_chain_leader_poll.txt)
+    const char *wgf_env = getenv("PAMG_CHAIN_WGFLAG");
+    const int wgf = wgf_env ? atoi(wgf_env) : 2;
+    if (f == (const void *)k_face_chain_pw && wgf >= 1) early |= 32;
+    if (f == (const void *)k_face_chain_pw && wgf >= 2) early |= 64;
     hipError_t e = launch_coresident(f, grid, kChainNT, args, s);
     if (stamp_path) {
         std::vector<long long> h(nst);

@@ -11,25 +11,25 @@ i = 0
 while i < raw.size:
     run, grid, E, nsub = (int(v) for v in raw[i:i + 4])
     i += 4
-    if run < 0:   # per-wave: [8 workgroups][16 waves][run][6]
+    if run < 0:   # per-wave: [8 workgroups][16 waves][run][7]
         run = -run
-        st = raw[i:i + 8 * 16 * run * 6].reshape(8 * 16, run, 6).astype(np.float64) * 10e-3
-        i += 8 * 16 * run * 6
+        st = raw[i:i + 8 * 16 * run * 7].reshape(8 * 16, run, 7).astype(np.float64) * 10e-3
+        i += 8 * 16 * run * 7
         st = st[:min(8, grid) * 16]
         if run < 4:
             continue
         s = st[:, 1:-1]   # steady sweeps (the first has no wait, the last no words)
-        names = ["item0", "wait", "snap", "item1+flag", "downs"]
-        ph = [(s[:, :, k + 1] - s[:, :, k]).mean() for k in range(5)]
-        rest = (st[:, 2:, 0] - st[:, 1:-1, 5]).mean()
+        names = ["item0", "wait", "snap", "item1", "drain+flag", "downs"]
+        ph = [(s[:, :, k + 1] - s[:, :, k]).mean() for k in range(6)]
+        rest = (st[:, 2:, 0] - st[:, 1:-1, 6]).mean()
         per = (st[:, -1, 0] - st[:, 1, 0]).mean() / (run - 2)
         # the sweep's critical hand-off: the last flag of sweep sw among these waves -> the first wait end of sw + 1
-        fl = st[:, 1:-2, 4].max(axis=0)
+        fl = st[:, 1:-2, 5].max(axis=0)
         we = st[:, 2:-1, 2]
         print(f"pw run {run:3d} grid {grid:4d}: per sweep {per:6.2f} us = " +
               " + ".join(f"{n} {v:5.2f}" for n, v in zip(names, ph)) + f" + rest {rest:5.2f}; "
               f"wait end - last flag (these waves): min {(we.min(axis=0) - fl).mean():5.2f} "
-              f"mean {(we.mean(axis=0) - fl).mean():5.2f} us; flag spread {(st[:, 1:-1, 4].max(0) - st[:, 1:-1, 4].min(0)).mean():5.2f} us")
+              f"mean {(we.mean(axis=0) - fl).mean():5.2f} us; flag spread {(st[:, 1:-1, 5].max(0) - st[:, 1:-1, 5].min(0)).mean():5.2f} us")
         continue
     st = raw[i:i + 8 * run * 4].reshape(8, run, 4).astype(np.float64) * 10e-3   # 100 MHz -> us
     i += 8 * run * 4
