@@ -1837,7 +1837,7 @@ void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
         Level &L = h->lv[l];
         dev_free(L.T); dev_free(L.stc); dev_free(L.Ainv); dev_free(L.subinfo); dev_free(L.d_pos); dev_free(L.blocks);
-        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx); dev_free(L.cpos); dev_free(L.gtab);
+        dev_free(L.fnb); dev_free(L.fface); dev_free(L.fsx); dev_free(L.cpos); dev_free(L.gtab); dev_free(L.cnb); dev_free(L.gpat);
         dev_free(L.chain_nb_off); dev_free(L.chain_nb_list); dev_free(L.chain_flags);
         dev_free(L.halo.d_local); dev_free(L.halo.d_bc); dev_free(L.halo.d_remote); dev_free(L.halo.d_recv_dst);
         dev_free(L.halo.d_send); dev_free(L.halo.d_send_b); dev_free(L.halo.d_recv);
@@ -2173,6 +2173,9 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
                 if ((e.x | e.y | e.z) && !fnb[j].w) L.words_up = false;
             }
             CHK(dev_upload(h, &L.cpos, cpos));
+            std::vector<int4> cnb(cpos.size());
+            for (size_t i = 0; i < cpos.size(); ++i) cnb[i] = fnb[cpos[i]];
+            CHK(dev_upload(h, &L.cnb, cnb));
             // the two-sweep passes' gather table (k_face_pp, Level::gtab): for every halo slot of every local
             // un_ele, the neighbour's boundary sub-element e whose words fill it (hface: this un_ele's words
             // into the neighbour; the neighbour's record back: its words into this one, reversed or not) and,
@@ -2205,6 +2208,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
                     if (v < 0) { h->err = "face operator: a face position without its boundary sub-element"; return PAMG_ERR_STATE; }
                 static const int fmface[3] = {1, 3, 2};   // un_ele face under sub-element face fi (pamg_face.hip cFMface)
                 std::vector<int4> gt((size_t)std::max(Ul, 1) * 3 * m, make_int4(-1, 0, 0, 0));
+                std::vector<int> gp(gt.size(), 0);
                 for (int q = 0; q < Ul; ++q)
                     for (int f = 1; f <= 3; ++f) {
                         const int4 g = gf[3 * (size_t)q + f - 1];
@@ -2229,9 +2233,11 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
                                 else y[fi] = -1 - e;   // another rank: k_face_pp is single-domain (never read)
                             }
                             o = make_int4(g.x * ns + e, y[0], y[1], y[2]);
+                            gp[(3 * (size_t)q + f - 1) * m + sp - 1] = (nb.x >= 0) | ((nb.y >= 0) << 1) | ((nb.z >= 0) << 2);
                         }
                     }
                 CHK(dev_upload(h, &L.gtab, gt));
+                CHK(dev_upload(h, &L.gpat, gp));
             }
         }
         HaloPlan &P = L.halo;

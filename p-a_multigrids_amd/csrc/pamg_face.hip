@@ -632,8 +632,9 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, double *out_end2,
     const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
-    const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int4 *__restrict__ hface,
-    const double2 *__restrict__ bcv, const int *__restrict__ cpos, int nup, int64_t pitch, int level1, double rdt,
+    const int *__restrict__ fsx, const int4 *__restrict__ gtab, const int *__restrict__ gpat, const int4 *__restrict__ hface,
+    const double2 *__restrict__ bcv, const int *__restrict__ cpos, const int4 *__restrict__ cnb, int nup, int64_t pitch,
+    int level1, double rdt,
     int res, double *RESout, double *RHSc, int64_t pitch_c, const double *__restrict__ Tc) {
     constexpr int PER = TS / NT, M = TS == 256 ? 16 : TS == 1024 ? 32 : 64, NH = 9 * M;
     // red-black: the colour passes run over colour lists (Level::cpos), every lane with an item of the colour
@@ -685,7 +686,11 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
     const bool gon = fu <= 3 && spu <= M;
     const int hq = 3 * ((fu - 1) * M + spu - 1);   // the slot's first word in a snapshot
     int4 ge = make_int4(-1, -1, -1, -1);
-    if (gon) ge = gtab[(u * 3 + fu - 1) * M + spu - 1];
+    int gp = 0;   // e's face pattern (Level::gpat), loaded beside the entry
+    if (gon) {
+        ge = gtab[(u * 3 + fu - 1) * M + spu - 1];
+        gp = gpat[(u * 3 + fu - 1) * M + spu - 1];
+    }
     // the start iterate at global position g: A's value, plus the prolonged coarse correction where Tc is given (the
     // corrected cycle's interp_add, k_interp_add's arithmetic, folded into the first pass of the smoother call that
     // follows it), or zero where A is null (a coarse level's call from zero: the cycle's memset folded)
@@ -704,7 +709,8 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
     double xe[3] = {0.0, 0.0, 0.0}, be[3] = {0.0, 0.0, 0.0}, yv[3][3];
     int4 nbe = make_int4(0, 0, 0, 0);
     if (gon && ge.x >= 0) {
-        nbe = fnb[ge.x & (TS - 1)];
+        // fnb[e]'s signs, all face_core and face_pattern read of it
+        nbe = make_int4((gp & 1) ? 0 : -1, (gp & 2) ? 0 : -1, (gp & 4) ? 0 : -1, 0);
         ldv(ge.x, xe);
         if (K == 2)
 #pragma unroll
@@ -732,11 +738,13 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
     for (int k = 0; k < KU + KD; ++k) {
         if constexpr (RB) {
             const int i = k < KU ? t + NT * k : NUP + t + NT * (k - KU);
-            ij[k] = (k < KU ? i < NUP : i < TS) ? cpos[i] : -1;
+            const bool in = k < KU ? i < NUP : i < TS;
+            ij[k] = in ? cpos[i] : -1;
+            inb[k] = cnb[in ? i : 0];   // fnb[cpos[i]], loaded beside cpos[i]
         } else {
             ij[k] = 2 * (t + NT * (k / 2)) + (k & 1);
+            inb[k] = fnb[ij[k]];
         }
-        inb[k] = fnb[ij[k] < 0 ? 0 : ij[k]];
     }
     double ib[KU + KD][3];   // the items' RHS (BL = 0)
     if constexpr (!BL)
@@ -2100,9 +2108,9 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
                           double *out_end, bool rb, bool level1, double rdt, int res, double *out_end2, const PPCoarse *pcx) {
     if (L.N == 0) return hipSuccess;
     const int m = L.nsub == 256 ? 16 : L.nsub == 1024 ? 32 : 64;
-    if (!face_tile_shape(L) || !L.fnb || !L.gtab || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)) ||
+    if (!face_tile_shape(L) || !L.fnb || !L.gtab || !L.gpat || (K != 1 && K != 2) || (K == 1 && (out_mid || res == 2)) ||
         (out_end2 && (out_end2 == in || !out_end)) ||
-        (rb && (!L.cpos || L.nup != m * (m + 1) / 2)))
+        (rb && (!L.cpos || !L.cnb || L.nup != m * (m + 1) / 2)))
         return hipErrorInvalidValue;
     // the coarse level (pcx): this one's quarter, the same un_eles, 4 children per coarse sub-element
     const Level *C = pcx ? pcx->coarse : nullptr;
@@ -2137,7 +2145,8 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
 #define PAMG_FPP1(TS, NT, RB_, K_, F_)                                                                                     \
     hipLaunchKernelGGL((k_face_pp<TS, NT, RB_, K_, F_>), g, dim3(NT), 0, s, in, out_pre, out_mid, out_end, out_end2, L.RHS, \
                        L.stc,                                                                                            \
-                       L.fnb, L.fface, L.fsx, L.gtab, P.d_hface, P.d_bcv, L.cpos, L.nup, L.pitch, l1, rdt, res, R, RC, pc, TC)
+                       L.fnb, L.fface, L.fsx, L.gtab, L.gpat, P.d_hface, P.d_bcv, L.cpos, L.cnb, L.nup, L.pitch, l1, rdt, res,  \
+                       R, RC, pc, TC)
 #define PAMG_FPP(TS, NT, RB_, K_) \
     do { if (fold) PAMG_FPP1(TS, NT, RB_, K_, true); else PAMG_FPP1(TS, NT, RB_, K_, false); } while (0)
 #define PAMG_FPPK(TS, NT)                                          \

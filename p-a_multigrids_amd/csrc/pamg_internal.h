@@ -116,12 +116,16 @@ struct Level {
     // the colour lists of the red-black passes: the storage positions of the up sub-elements
     // (fnb.w != 0, ascending), then of the down ones -- nup + ndn = nsub
     int *cpos = nullptr;
+    int4 *cnb = nullptr;   // fnb of the colour lists' positions (cnb[i] = fnb[cpos[i]]): one load, not two in a row
     int nup = 0, ndn = 0;
     // the two-sweep passes (k_face_pp): per (local un_ele, face, halo slot) the gather entry of the
     // neighbour's boundary sub-element e facing the slot -- {e's global index (-1 boundary face, -2 another
     // rank), then per face of e the global index of the value across it, -1 - p for this un_ele's own
     // position p, or -(1 + nsub + 3 bcv index + face - 1) for a boundary word}
     int4 *gtab = nullptr;
+    // per gather entry the face pattern of e (bit fi: e's face fi is inner, fnb's sign): k_face_pp reads it beside the
+    // entry instead of fnb[e] after it
+    int *gpat = nullptr;
     // every sub-element with halo words (HaloPlan::hsub) is an up one: the chain publishes a
     // sweep's words right after its up pass (k_face_chain, early)
     bool words_up = false;

@@ -501,7 +501,9 @@ __device__ __forceinline__ void asm_pair(const double2 xv[3], const double2 bv[3
 }
 
 // LAYOUT 0: a thread per pair. LAYOUT 1: a wave per run of K tiles (K x 128 sub-elements), a lane takes pair
-// `lane` of each tile, every load of the K tiles issued before the first sweep
+// `lane` of each tile, every load of the K tiles issued before the first sweep. (Measured, not kept: a resident
+// grid whose waves walk the tiles w, w + W, ... with the next tile's loads in flight in a second register set --
+// 206 VGPRs, two waves per SIMD -- 0.64-0.70 of 8 TB/s against this launch's 0.70-0.72, profiles/r05_aa_*.)
 template <int LAYOUT, int K>
 __global__ __launch_bounds__(kBlock) void k_sweep_assembled(const double *__restrict__ x, const double *__restrict__ b,
                                                             const double *__restrict__ blk, double *__restrict__ out,
