@@ -608,6 +608,9 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_SNAP1
 #define PAMG_FACE_PP_SNAP1 1
 #endif
+#ifndef PAMG_FACE_PP_GHOST_EARLY
+#define PAMG_FACE_PP_GHOST_EARLY 1
+#endif
 // NT: red-black passes with fewer threads than up sub-elements run a second up item on some threads. For
 // the 256-sub-element un_ele 192 threads (136 ups, one each) measured faster than 128 (0.71 vs 0.73 ms of
 // coarse launches per cycle); for the 1,024 one 576 threads (528 ups) measured slower than 512 (level-1
@@ -651,6 +654,9 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
     // 51,648 B of LDS: three workgroups per CU instead of two (phase stamps, profiles/r05_n_pp_stamps.txt: 512 of
     // the 768 slots were ever resident)
     constexpr bool SNAP1 = PAMG_FACE_PP_SNAP1 != 0 && K == 2;
+    // PAMG_FACE_PP_GHOST_EARLY (a build macro, A/B): the ghost update's operands in this tile gathered from memory
+    // like the others, and the update run before the tile's barrier (see ghost below)
+    constexpr bool GEARLY = PAMG_FACE_PP_GHOST_EARLY != 0 && K == 2;
     constexpr int OX = 0, OB = 3 * TS, OH = (BL ? 6 : 3) * TS, OW = OH + (SNAP1 ? 1 : K) * NH;
     __shared__ double LDSM[OW + 24];
     double (*X)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OX);
@@ -721,6 +727,8 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
             for (int fi = 0; fi < 3; ++fi) {
                 if (yy[fi] >= 0) {
                     ldv(yy[fi], yv[fi]);
+                } else if (GEARLY && yy[fi] > -(1 + TS)) {
+                    ldv(s0 - 1 - yy[fi], yv[fi]);   // this tile's own start value, as its bulk load forms it
                 } else {
 #pragma unroll
                     for (int c = 0; c < 3; ++c)
@@ -791,21 +799,21 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
         load_face_rec(stc, fface, fsx, v, Rv);
         wdv = fface + v * kFaceStride + kFaceWD + 3 * face_pattern(nbe);
     }
-    __syncthreads();
-    pp_stamp(1);
     double hn[3] = {0.0, 0.0, 0.0};   // SNAP1: this thread's slot of the second sweep's snapshot
-    if constexpr (K == 2) {
-        // the neighbour's boundary sub-element e after the first sweep (an up one: its sweep reads its down
-        // neighbours, unchanged since the previous sweep, and the snapshot across its faces): the second
-        // sweep's snapshot -- face_core on v's record and the values gathered above
+    // the neighbour's boundary sub-element e after the first sweep (an up one: its sweep reads its down
+    // neighbours, unchanged since the previous sweep, and the snapshot across its faces): the second
+    // sweep's snapshot -- face_core on v's record and the values gathered above. GEARLY: every operand came from
+    // memory, so the update runs as soon as they arrive, before the tile's barrier (no LDS read, no second barrier)
+    auto ghost = [&]() {
         if (gon) {
             if (ge.x >= 0) {
                 const int yy[3] = {ge.y, ge.z, ge.w};
+                if (!GEARLY)
 #pragma unroll
-                for (int fi = 0; fi < 3; ++fi)
-                    if (yy[fi] < 0 && yy[fi] > -(1 + TS))
+                    for (int fi = 0; fi < 3; ++fi)
+                        if (yy[fi] < 0 && yy[fi] > -(1 + TS))
 #pragma unroll
-                        for (int c = 0; c < 3; ++c) yv[fi][c] = X[c][-1 - yy[fi]];
+                            for (int c = 0; c < 3; ++c) yv[fi][c] = X[c][-1 - yy[fi]];
                 double r[3];
                 // (the component of a halo word is a run-time selector: picked by selects, so that yv stays in
                 // registers)
@@ -822,9 +830,15 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
                 for (int c = 0; c < 3; ++c) HI(1)[hq + c] = HI(0)[hq + c];   // boundary words: constant
             }
         }
+    };
+    if constexpr (K == 2 && GEARLY) ghost();
+    __syncthreads();
+    pp_stamp(1);
+    if constexpr (K == 2 && !GEARLY) {
+        ghost();
         __syncthreads();   // the ghost updates read the start iterate (X) before the sweeps rewrite it
-        pp_stamp(2);
     }
+    if constexpr (K == 2) pp_stamp(2);
     // SNAP1: the second sweep's snapshot into the image, after the first sweep's last read of it (boundary words: constant)
     auto snap_next = [&]() {
         if (SNAP1 && gon && ge.x >= 0)
