@@ -1888,7 +1888,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                 } else {
                     for (unsigned spins = 0;; ++spins) {
                         if (__hip_atomic_load(&wgready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (unsigned)sw) break;
-                        if (spins > (1u << 24)) {   // the poller gives up after 2^22 polls and still releases this word
+                        if (spins > (1u << 27)) {   // the poller gives up after 2^22 polls (>= 4 s) and still releases this word
                             if (ln == 0) __hip_atomic_store((g_u32 *)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             break;
                         }

@@ -467,7 +467,10 @@ __global__ __launch_bounds__(kBlock) void k_to_aos(const double *__restrict__ so
 // rounds, one process each): every variant 0.240-0.259 ms per launch = 5.4-5.9 TB/s, the spread between
 // processes of one variant (their allocations' placement) as large as between variants -- the stream count
 // is not what bounds it; 0.70-0.73 of 8 TB/s is ~93 % of the guide's measured 6.3 TB/s streaming copy.
-// Default 12 (tiled, two tiles per wave: the best mean, 0.246 ms).
+// Then 12 (tiled, two tiles per wave: the best mean, 0.246 ms). Default 41 (round 5): the tiled blocks and the x / b
+// pieces of a wave's tile all through LDS-DMA (global_load_lds_dwordx4, 18 wave-instructions of 1 KiB, no VGPR
+// destination), 0.749-0.755 of 8 TB/s against 0.716-0.724 for 12 and 0.709-0.724 for the blocks alone through LDS
+// (31), three interleaved process triples (profiles/r05_ad_asm_ldsdma.txt).
 constexpr int kAsmTile = 128;
 __device__ __forceinline__ int64_t asm_index(int layout, int64_t pitch, int q, int64_t s) {
     return layout == 0 ? q * pitch + s : (s / kAsmTile) * (12 * kAsmTile) + q * kAsmTile + (s % kAsmTile);
@@ -518,6 +521,86 @@ __global__ __launch_bounds__(kBlock) void k_sweep_assembled(const double *__rest
 #pragma unroll
         for (int q = 0; q < 12; ++q) a[q] = ld2(blk + q * pitch + s);
         asm_pair(xv, bv, a, out, pitch, s);
+    } else if constexpr (LAYOUT == 4) {
+        // every stream through LDS-DMA: the twelve block pieces and the six x / b pieces of the wave's tile (18 KiB,
+        // 18 wave-instructions, no VGPR destination); a partial last tile loads x and b into registers
+        constexpr int NP = 18;
+        __shared__ double LB[(kBlock / 64) * NP * kAsmTile];
+        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int64_t tile = (int64_t)blockIdx.x * (kBlock / 64) + wv;
+        const int64_t ntiles = (2 * npairs + kAsmTile - 1) / kAsmTile;
+        if (tile >= ntiles) return;
+        const int64_t s = tile * kAsmTile + 2 * lane;
+        const bool full = (tile + 1) * kAsmTile <= 2 * npairs;
+        double *l = LB + wv * NP * kAsmTile;
+        const double *t = blk + tile * (12 * kAsmTile) + 2 * lane;
+        constexpr int aux = (PAMG_NT & 1) ? 2 : 0;
+#pragma unroll
+        for (int q = 0; q < 12; ++q)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(t + q * kAsmTile),
+                                             (__attribute__((address_space(3))) void *)(l + q * kAsmTile), 16, 0, aux);
+        double2 xv[3], bv[3];
+        if (full) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(x + c * pitch + s),
+                                                 (__attribute__((address_space(3))) void *)(l + (12 + c) * kAsmTile), 16, 0, aux);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(b + c * pitch + s),
+                                                 (__attribute__((address_space(3))) void *)(l + (15 + c) * kAsmTile), 16, 0, aux);
+            }
+        } else if (s < 2 * npairs) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { xv[c] = ld2(x + c * pitch + s); bv[c] = ld2(b + c * pitch + s); }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (s >= 2 * npairs) return;
+        const double *lr = l + 2 * lane;
+        double2 a[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) a[q] = *reinterpret_cast<const double2 *>(lr + q * kAsmTile);
+        if (full)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                xv[c] = *reinterpret_cast<const double2 *>(lr + (12 + c) * kAsmTile);
+                bv[c] = *reinterpret_cast<const double2 *>(lr + (15 + c) * kAsmTile);
+            }
+        asm_pair(xv, bv, a, out, pitch, s);
+    } else if constexpr (LAYOUT == 3) {
+        // the tiled blocks through LDS-DMA (global_load_lds_dwordx4: a plane piece of a tile is 64 lanes x 16 B, one
+        // wave-instruction, no VGPR destination), x and b into registers; then each lane reads its 16 B of every
+        // piece from LDS (lane-linear: conflict-free ds_read_b128)
+        __shared__ double LB[(kBlock / 64) * K * 12 * kAsmTile];
+        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + wv;
+        const int64_t ntiles = (2 * npairs + kAsmTile - 1) / kAsmTile;
+        double2 xv[K][3], bv[K][3];
+        int64_t sk[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t tile = w * K + k;
+            sk[k] = tile * kAsmTile + 2 * lane;
+            if (tile >= ntiles) continue;
+            const double *t = blk + tile * (12 * kAsmTile) + 2 * lane;
+            double *l = LB + (wv * K + k) * 12 * kAsmTile;
+#pragma unroll
+            for (int q = 0; q < 12; ++q)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(t + q * kAsmTile),
+                                                 (__attribute__((address_space(3))) void *)(l + q * kAsmTile), 16, 0,
+                                                 (PAMG_NT & 1) ? 2 : 0);
+            if (sk[k] < 2 * npairs)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { xv[k][c] = ld2(x + c * pitch + sk[k]); bv[k][c] = ld2(b + c * pitch + sk[k]); }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (sk[k] >= 2 * npairs) continue;
+            const double *l = LB + (wv * K + k) * 12 * kAsmTile + 2 * lane;
+            double2 a[12];
+#pragma unroll
+            for (int q = 0; q < 12; ++q) a[q] = *reinterpret_cast<const double2 *>(l + q * kAsmTile);
+            asm_pair(xv[k], bv[k], a, out, pitch, sk[k]);
+        }
     } else {
         const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
         const int lane = threadIdx.x & 63;
@@ -874,7 +957,7 @@ hipError_t launch_to_aos(hipStream_t s, const Level &L, const double *soa, doubl
 // PAMG_ASM_LAYOUT=<layout><K> (A/B runs; read once): the layout of the assembled blocks and, tiled, the
 // tiles per wave
 int asm_layout() {
-    static const int v = getenv("PAMG_ASM_LAYOUT") ? atoi(getenv("PAMG_ASM_LAYOUT")) : 12;
+    static const int v = getenv("PAMG_ASM_LAYOUT") ? atoi(getenv("PAMG_ASM_LAYOUT")) : 41;
     return v;
 }
 
@@ -903,6 +986,17 @@ hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, do
     const int K = v % 10;
     const int64_t ntiles = (L.N + kAsmTile - 1) / kAsmTile, waves = (ntiles + K - 1) / K;
     const unsigned grid = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
+    if (v / 10 == 4) {   // tiled, every stream through LDS-DMA (A/B: PAMG_ASM_LAYOUT=41)
+        const unsigned g4 = (unsigned)((ntiles + kBlock / 64 - 1) / (kBlock / 64));
+        hipLaunchKernelGGL((k_sweep_assembled<4, 1>), dim3(g4), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out, L.pitch, npairs);
+        return hipGetLastError();
+    }
+    if (v / 10 == 3) {   // tiled, the blocks through LDS-DMA (A/B: PAMG_ASM_LAYOUT=31 / 32)
+        if (K == 1) hipLaunchKernelGGL((k_sweep_assembled<3, 1>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out, L.pitch, npairs);
+        else if (K == 2) hipLaunchKernelGGL((k_sweep_assembled<3, 2>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out, L.pitch, npairs);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     switch (K) {
         case 1: hipLaunchKernelGGL((k_sweep_assembled<1, 1>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
                                    L.pitch, npairs); break;
