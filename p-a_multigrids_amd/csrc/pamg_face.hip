@@ -611,6 +611,9 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_GHOST_EARLY
 #define PAMG_FACE_PP_GHOST_EARLY 1
 #endif
+#ifndef PAMG_FACE_PP_GLDS
+#define PAMG_FACE_PP_GLDS 1
+#endif
 // NT: red-black passes with fewer threads than up sub-elements run a second up item on some threads. For
 // the 256-sub-element un_ele 192 threads (136 ups, one each) measured faster than 128 (0.71 vs 0.73 ms of
 // coarse launches per cycle); for the 1,024 one 576 threads (528 ups) measured slower than 512 (level-1
@@ -761,8 +764,26 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
 #pragma unroll
             for (int c = 0; c < 3; ++c) ib[k][c] = RHS[c * pitch + s0 + (ij[k] < 0 ? 0 : ij[k])];
     (void)nup;
+    // PAMG_FACE_PP_GLDS: a start iterate taken as it is (no interpolation folded in, no zero start) and not stored
+    // (out_pre) goes to LDS by LDS-DMA with the RHS -- a wave's 64 pairs of a plane are one 1 KiB global_load_lds_dwordx4
+    // into X / B (lane-linear), no VGPR round trip; the __syncthreads below waits for them
+    const bool glds = PAMG_FACE_PP_GLDS && BL && !out_pre && !(FOLD && (Tc || !A));
+    if (glds) {
+        constexpr int aux = (PAMG_NT & 1) ? 2 : 0;
+        const int lane = t & 63;
+        for (int p0 = t - lane; p0 < TS / 2; p0 += NT) {   // wave-uniform: the wave's first pair
+            const int j0 = 2 * p0;
 #pragma unroll
-    for (int p = t; p < TS / 2; p += NT) {   // the iterate and the RHS into LDS, adjacent pairs
+            for (int c = 0; c < 3; ++c) {
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(A + c * pitch + s0 + j0 + 2 * lane),
+                                                 (__attribute__((address_space(3))) void *)(&X[c][j0]), 16, 0, aux);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(RHS + c * pitch + s0 + j0 + 2 * lane),
+                                                 (__attribute__((address_space(3))) void *)(&B[c][j0]), 16, 0, aux);
+            }
+        }
+    }
+#pragma unroll
+    for (int p = glds ? TS : t; p < TS / 2; p += NT) {   // the iterate and the RHS into LDS, adjacent pairs
         const int j = 2 * p;
         double a0[3] = {0.0, 0.0, 0.0}, a1[3] = {0.0, 0.0, 0.0};
         if (FOLD && Tc) {   // ldv's correction: both children of the pair share their coarse sub-element

@@ -624,6 +624,8 @@ __global__ __launch_bounds__(kBlock) void k_sweep_assembled(const double *__rest
 
 // Matrix-free form of the same sweep (the reference's own structure: one
 // stencil per un_ele, ShapFun_unstruc.F90:304-335): 72 B per sub-element.
+// (Measured, not kept: x and b through LDS-DMA, 0.737-0.753 of 8 TB/s against 0.747-0.772 with these register
+// loads, profiles/r05_ae_face_pp_glds.txt -- unlike the assembled sweep's 18 streams, this sweep's six gain nothing.)
 __global__ __launch_bounds__(kBlock) void k_sweep_stencil(const double *__restrict__ x, const double *__restrict__ b,
                                                           const double *__restrict__ stc, double *__restrict__ out,
                                                           int64_t pitch, int64_t npairs, int nsub_log2, double rdt) {
