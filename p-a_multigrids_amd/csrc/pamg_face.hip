@@ -764,46 +764,71 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD 
 #pragma unroll
             for (int c = 0; c < 3; ++c) ib[k][c] = RHS[c * pitch + s0 + (ij[k] < 0 ? 0 : ij[k])];
     (void)nup;
-    // PAMG_FACE_PP_GLDS: a start iterate taken as it is (no interpolation folded in, no zero start) and not stored
-    // (out_pre) goes to LDS by LDS-DMA with the RHS -- a wave's 64 pairs of a plane are one 1 KiB global_load_lds_dwordx4
-    // into X / B (lane-linear), no VGPR round trip; the __syncthreads below waits for them
-    const bool glds = PAMG_FACE_PP_GLDS && BL && !out_pre && !(FOLD && (Tc || !A));
-    if (glds) {
+    // PAMG_FACE_PP_GLDS: unless the start iterate is stored (out_pre), the RHS -- and the start iterate when it is read
+    // (not a start from zero) -- go to LDS by LDS-DMA: a wave's 64 pairs of a plane are one 1 KiB global_load_lds_dwordx4
+    // into X / B (lane-linear), no VGPR round trip; in the folded instance an interpolation is then added to X in place
+    // by the pair's own thread (after its wave's wait: its lane wrote that pair), v + a as in the register path; the
+    // __syncthreads below waits for the rest
+    const bool gr = PAMG_FACE_PP_GLDS && BL && !out_pre, ga = gr && (!FOLD || A);
+    if (gr) {
         constexpr int aux = (PAMG_NT & 1) ? 2 : 0;
         const int lane = t & 63;
         for (int p0 = t - lane; p0 < TS / 2; p0 += NT) {   // wave-uniform: the wave's first pair
             const int j0 = 2 * p0;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(A + c * pitch + s0 + j0 + 2 * lane),
-                                                 (__attribute__((address_space(3))) void *)(&X[c][j0]), 16, 0, aux);
+                if (ga)
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(A + c * pitch + s0 + j0 + 2 * lane),
+                                                     (__attribute__((address_space(3))) void *)(&X[c][j0]), 16, 0, aux);
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(RHS + c * pitch + s0 + j0 + 2 * lane),
                                                  (__attribute__((address_space(3))) void *)(&B[c][j0]), 16, 0, aux);
             }
         }
+        if (FOLD && ga && Tc) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    if constexpr (!FOLD) {
 #pragma unroll
-    for (int p = glds ? TS : t; p < TS / 2; p += NT) {   // the iterate and the RHS into LDS, adjacent pairs
-        const int j = 2 * p;
-        double a0[3] = {0.0, 0.0, 0.0}, a1[3] = {0.0, 0.0, 0.0};
-        if (FOLD && Tc) {   // ldv's correction: both children of the pair share their coarse sub-element
-            const int64_t cg = (s0 + j) >> 2;
-            const double y[3] = {Tc[cg], Tc[pitch_c + cg], Tc[2 * pitch_c + cg]};
-            interp_corr(j & 3, y, a0);
-            interp_corr((j + 1) & 3, y, a1);
-        }
+        for (int p = gr ? TS : t; p < TS / 2; p += NT) {   // the iterate and the RHS into LDS, adjacent pairs
+            const int j = 2 * p;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            double2 v = !FOLD || A ? ld2(A + c * pitch + s0 + j) : make_double2(0.0, 0.0);
-            if (FOLD && Tc) v = make_double2(v.x + a0[c], v.y + a1[c]);
-            const double2 r = BL ? ld2(RHS + c * pitch + s0 + j) : make_double2(0.0, 0.0);
-            X[c][j] = v.x;
-            X[c][j + 1] = v.y;
-            if (BL) {
-                B[c][j] = r.x;
-                B[c][j + 1] = r.y;
+            for (int c = 0; c < 3; ++c) {
+                const double2 v = ld2(A + c * pitch + s0 + j);
+                const double2 r = BL ? ld2(RHS + c * pitch + s0 + j) : make_double2(0.0, 0.0);
+                X[c][j] = v.x;
+                X[c][j + 1] = v.y;
+                if (BL) {
+                    B[c][j] = r.x;
+                    B[c][j + 1] = r.y;
+                }
+                if (out_pre) st2(out_pre + c * pitch + s0 + j, v);
             }
-            if (out_pre) st2(out_pre + c * pitch + s0 + j, v);
+        }
+    } else {
+#pragma unroll
+        for (int p = ga && !Tc ? TS : t; p < TS / 2; p += NT) {   // the iterate (and the RHS) into LDS, adjacent pairs
+            const int j = 2 * p;
+            double a0[3] = {0.0, 0.0, 0.0}, a1[3] = {0.0, 0.0, 0.0};
+            if (Tc) {   // ldv's correction: both children of the pair share their coarse sub-element
+                const int64_t cg = (s0 + j) >> 2;
+                const double y[3] = {Tc[cg], Tc[pitch_c + cg], Tc[2 * pitch_c + cg]};
+                interp_corr(j & 3, y, a0);
+                interp_corr((j + 1) & 3, y, a1);
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double2 v;
+                if (ga) v = make_double2(X[c][j], X[c][j + 1]);   // Tc: the DMA's value
+                else v = A ? ld2(A + c * pitch + s0 + j) : make_double2(0.0, 0.0);
+                if (Tc) v = make_double2(v.x + a0[c], v.y + a1[c]);
+                X[c][j] = v.x;
+                X[c][j + 1] = v.y;
+                if (BL && !gr) {
+                    const double2 r = ld2(RHS + c * pitch + s0 + j);
+                    B[c][j] = r.x;
+                    B[c][j + 1] = r.y;
+                }
+                if (out_pre) st2(out_pre + c * pitch + s0 + j, v);
+            }
         }
     }
     // the snapshot of the first sweep (:555 at its start): the neighbours' boundary values in A, or this
