@@ -1882,6 +1882,60 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
             const int uk = idx / (9 * m), rem = idx - uk * 9 * m, mf = rem / (3 * m), off = rem - mf * 3 * m;
             so[it] = (int)(((u0 + uk) * slots * 3 + (int64_t)mf * slots + off) * 8);
         }
+    // Coalesced words (cw): a sweep's halo words leave as 16-byte sc1 buffer stores of whole t_overlap rows (Guideline
+    // 16 R1's payload form) instead of three 8-byte stores per face from each item-1 lane: the wave's rows (its
+    // un_eles' faces to neighbours on this rank, 3m words each) are cut into 16-byte chunks, a lane takes one or two
+    // and reads their two words from the tile in LDS, where the item-1 pass has just put them (this wave's own lanes).
+    // Word w of a row is component w % 3 of the sub-element at face position i (k = w / 3 + 1, i = k or m + 1 - k
+    // reversed: halo_words' placement inverted). Per lane, fixed for the call: the chunk's byte offset in a snapshot
+    // buffer and its two LDS indices. The boundary faces' constant words go out once, before the sweeps, into the
+    // buffer the first sweep writes (as halo_words with bc there).
+    const int rowc = 3 * m / 2, nch = (ub - ua) * 3 * rowc;
+    const bool cw = snap16 && nch <= 128 && 3 * m <= 9 * m * (ub - ua);
+    int co[2] = {-1, -1};
+    unsigned ci[2] = {0u, 0u};
+    if (cw) {
+        // face position -> tile-local sub-element (the same in every un_ele of the level), in this wave's slots of
+        // the snapshot image as scratch until the first snapshot load
+        for (int j = ln; j < nsub; j += 64) {
+            const int4 e = H.hsub[j];
+            if (e.x) LM[OHI + ha + e.x - 1] = (double)j;
+            if (e.y) LM[OHI + ha + m + e.y - 1] = (double)j;
+            if (e.z) LM[OHI + ha + 2 * m + e.z - 1] = (double)j;
+        }
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            const int ch = ln + 64 * it;
+            if (ch >= nch) continue;
+            const int uk = ua + ch / (3 * rowc), rem = ch % (3 * rowc), f = rem / rowc, cwi = rem % rowc;
+            const int4 rec = H.hface[3 * (u0 + uk) + f];
+            if ((rec.x & 3) != 1) continue;
+            const bool rev = (rec.x >> 2) != 0;
+            unsigned idx[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int w = 2 * cwi + h, k = w / 3 + 1, c = w % 3, i = rev ? m - k + 1 : k;
+                const int j = (int)LM[OHI + ha + f * m + i - 1];
+                idx[h] = (unsigned)(c * XP + (uk << nsub_log2) + j);
+            }
+            ci[it] = idx[0] | (idx[1] << 16);
+            co[it] = (rec.y + 2 * cwi) * 8;
+        }
+        // the boundary faces' words, constant in the call, into the buffer the first sweep publishes into
+        if (run >= 1 && 1 < total && I1.j[0] >= 0) {
+            double *tout0 = ((total - 2) & 1) ? buf1 : buf0;
+            const int pos[3] = {hq & 1023, (hq >> 10) & 1023, hq >> 20};
+#pragma unroll
+            for (int f = 0; f < 3; ++f) {
+                const int i = pos[f];
+                if (!i || (hr[f].x & 3) != 0) continue;
+                const int a = (i - 1) * 3 + (f == 2 ? 1 : 0), b = (i - 1) * 3 + (f == 1 ? 1 : 2);
+                const double2 v = H.bcv[hr[f].z + i - 1];
+                st_coh(tout0 + hr[f].y + a, v.x);
+                st_coh(tout0 + hr[f].y + b, v.y);
+            }
+        }
+    }
     // poll flags f[0 .. n) (lane i one) until each is >= want; bounded (the give-up word tmo)
     auto poll = [&](int n, auto &&flag_of, unsigned want) {
         for (int base = 0; base < n; base += 64) {
@@ -1986,10 +2040,23 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
             pw_face(I1.j[0], P1, I1.b[0], r);
 #pragma unroll
             for (int c = 0; c < 3; ++c) LM[c * XP + I1.j[0]] = r[c];
-            if (tout) {
+            if (tout && !cw) {
                 HaloArgs Hn = H;
                 Hn.tov = tout;
                 halo_words<true>(Hn, hr, hq, r, sw == 0);
+            }
+        }
+        if (tout && cw) {   // this wave's rows, 16 bytes a lane (the item-1 values just written to LM)
+            asm volatile("" : "+v"(co[0]), "+v"(co[1]), "+v"(ci[0]), "+v"(ci[1]));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(tout, (short)0, tin_bytes, 0x00020000);
+#pragma unroll
+            for (int it = 0; it < 2; ++it) {
+                if (co[it] < 0) continue;
+                const double v0 = LM[ci[it] & 65535], v1 = LM[ci[it] >> 16];
+                const unsigned long long b0 = (unsigned long long)__double_as_longlong(v0),
+                                         b1 = (unsigned long long)__double_as_longlong(v1);
+                const v4u val = {(unsigned)b0, (unsigned)(b0 >> 32), (unsigned)b1, (unsigned)(b1 >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(val, rs, co[it], 0, kAuxSc1);
             }
         }
         if (stamps) {
