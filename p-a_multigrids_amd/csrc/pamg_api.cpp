@@ -83,10 +83,13 @@ int dev_alloc(pamg_handle *h, T **p, size_t count) {
 // every setup transfer runs on the handle's stream: its streams are non-blocking, so work on
 // them is not ordered against the null stream a blocking hipMemcpy uses (a memset queued on
 // h->stream could land after such a copy)
+int face_gates_drain(pamg_handle *h);   // (a host wait on the handle's stream first reads its chain gates back)
+
 template <class T>
 int dev_upload(pamg_handle *h, T **p, const std::vector<T> &v) {
     CHK(dev_alloc(h, p, v.size()));
     if (!v.empty()) {
+        CHK(face_gates_drain(h));
         HIPCHK(h, hipMemcpyAsync(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));   // v may be freed on return
     }
@@ -157,6 +160,7 @@ struct Span {
 int drain_timing(pamg_handle *h) {
     auto &T = h->timing;
     if (T.pending.empty()) return PAMG_OK;
+    CHK(face_gates_drain(h));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     for (auto &r : T.pending) {
         float ms = 0.f;
@@ -174,6 +178,7 @@ int drain_timing(pamg_handle *h) {
 // ---- scratch ------------------------------------------------------------
 int ensure_scratch(pamg_handle *h, size_t bytes) {
     if (h->scratch_bytes >= bytes) return PAMG_OK;
+    CHK(face_gates_drain(h));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     dev_free(h->scratch);
     h->scratch = nullptr;
@@ -461,6 +466,7 @@ int comm_error(pamg_handle *h) {
 // N = 8 shape (1,024 un_eles, an RCCL self-peer exchange) took 233.7 us against 169.2 us without a
 // communicator, its exchange hidden behind the launch (profiles/r05_c_xe_probe.txt)
 int sync_stream(pamg_handle *h, hipStream_t s) {
+    CHK(face_gates_drain(h));
     if (!h->comm || (!h->comm->nccl && !h->comm->local)) {
         HIPCHK(h, hipStreamSynchronize(s));
         return PAMG_OK;
@@ -655,7 +661,10 @@ bool chain_guard_on() {
 // invalid after the error (set them again, or start a new time step from a known tnew). Checked only
 // when such a launch ran since the last check (the other op = 1 calls stay asynchronous); the word is
 // cleared once reported, so the next call on the handle runs again.
+int face_gates_drain(pamg_handle *h);
+
 int face_chain_check(pamg_handle *h) {
+    CHK(face_gates_drain(h));
     if (!h->chain_tmo || !h->chain_pending) return PAMG_OK;
     h->chain_pending = false;
     unsigned v = 0;
@@ -683,6 +692,101 @@ bool face_tiles_ok(pamg_handle *h, int l) {
 bool face_fusable(pamg_handle *h, int l) { return face_tiles_ok(h, l); }
 
 int face_residual(pamg_handle *h, int l, bool neg);
+
+// face_call's executed sweeps as one launch each (from the snapshot the call's halo refresh wrote)
+int face_call_sweeps(pamg_handle *h, int l, int sweeps, int run, bool dead_last, bool src_is_T, bool both, bool res_in_sweep) {
+    Level &L = h->lv[l];
+    const double rdt = 1 / h->p.dt;
+    const int kid = (l == 1) ? PAMG_K_SMOOTH_L1 : PAMG_K_SMOOTH;
+    double *buf[2] = {h->tov, h->tov_b};
+    for (int s = 0; s < run; ++s) {
+        const bool fin = s + 1 == run;
+        // read tnew_nonlin, RHS; write tnew_nonlin (+ tnew in the last sweep, + the next halo words)
+        const int store = fin ? (dead_last ? 2 : 1) : 0;
+        const bool r = s == 0 && res_in_sweep;
+        if (r) h->rhsn_valid = false;
+        Span sp(h, kid, (store == 1 ? 96.0 : 72.0) * (double)L.N + (r ? 24.0 * (double)L.N : 0.0) + 168.0 * h->U);
+        HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
+                                          s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
+                                          h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store, s == 0,
+                                          s == 0 && src_is_T, r ? L.RES : nullptr));
+        if (s + 1 < sweeps) CHK(halo(h, l, buf[(sweeps - 2 - s) & 1]));   // the next sweep's remote words
+    }
+    if (both) HIPCHK(h, launch_copy(h->stream, L.TNN, L.T, 3 * L.pitch));
+    return PAMG_OK;
+}
+
+// PAMG_CHAIN_GATE=0 (A/B): the host waits for each guarded chain launch (round 5's first form) instead of
+// gating the stream on the launch's own report
+bool chain_gate_on() {
+    const char *e = getenv("PAMG_CHAIN_GATE");   // read per call: tests switch it within a process
+    return !(e && atoi(e) == 0);
+}
+
+int face_gate_setup(pamg_handle *h) {
+    if (h->gate) return PAMG_OK;
+    // the stream waits on it (hipStreamWaitValue64): HIP's signal memory, as xc_sig
+    HIPCHK(h, hipExtMallocWithFlags((void **)&h->gate, sizeof(unsigned long long), hipMallocSignalMemory));
+    unsigned long long v = 0;
+    HIPCHK(h, hipMemcpy(&v, h->gate, sizeof v, hipMemcpyDeviceToHost));
+    h->gate_base = v;
+    HIPCHK(h, hipHostMalloc((void **)&h->gate_stat, kGateRing * sizeof(unsigned long long), hipHostMallocCoherent));
+    memset(h->gate_stat, 0, kGateRing * sizeof(unsigned long long));   // (tags start at 1)
+    HIPCHK(h, hipStreamCreateWithFlags(&h->stream_fb, hipStreamNonBlocking));
+    return PAMG_OK;
+}
+
+// read back the gated chain launches in stream order: each one's report arrives once it has run (its
+// workgroups all resident: it opened its gate itself) or given up (the stream waits at its gate: the call
+// runs here with one launch per sweep on stream_fb, from the input and snapshot the aborted launch left
+// untouched, and then opens the gate). Every host wait on the handle's stream drains them first.
+int face_gates_drain(pamg_handle *h) {
+    while (!h->gates.empty()) {
+        const pamg_handle::GatePending g = h->gates.front();
+        h->gates.erase(h->gates.begin());
+        volatile unsigned long long *st = h->gate_stat + (g.seq & (kGateRing - 1));
+        const auto t0 = std::chrono::steady_clock::now();
+        unsigned long long v = 0;
+        for (unsigned i = 0;; ++i) {
+            v = *st;
+            if ((v >> 1) == g.seq) break;
+            if ((i & 4095) != 4095) continue;
+            const hipError_t e = hipStreamQuery(h->stream);
+            if (e != hipSuccess && e != hipErrorNotReady) {
+                h->gates.clear();
+                HIPCHK(h, e);
+            }
+            if ((e == hipSuccess && (*st >> 1) != g.seq) ||
+                std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600)) {
+                h->gates.clear();
+                h->err = "face chain: a gated launch never reported (the state is invalid)";
+                return PAMG_ERR_HIP;
+            }
+        }
+        if (!(v & 1)) continue;
+        Level &L = h->lv[g.l];
+        double *const keep[3] = {L.T, L.TNN, L.RHS};
+        const hipStream_t main = h->stream;
+        L.T = g.T;
+        L.TNN = g.TNN;
+        L.RHS = g.RHS;
+        h->stream = h->stream_fb;
+        int rc = face_call_sweeps(h, g.l, g.sweeps, g.run, g.dead_last, g.src_is_T, g.both, false);
+        if (rc == PAMG_OK && hipMemsetAsync(h->chain_tmo + 3, 0, sizeof(unsigned), h->stream) != hipSuccess) rc = PAMG_ERR_HIP;
+        if (rc == PAMG_OK && hipStreamWriteValue64(h->stream, h->gate, g.want, 0) != hipSuccess) rc = PAMG_ERR_HIP;
+        h->stream = main;
+        L.T = keep[0];
+        L.TNN = keep[1];
+        L.RHS = keep[2];
+        if (rc != PAMG_OK) {
+            h->gates.clear();
+            if (h->err.empty()) h->err = "face chain: the gated fallback failed to launch";
+            return rc;
+        }
+        h->timing.seq[PAMG_K_FACE_FALLBACK] += 1;
+    }
+    return PAMG_OK;
+}
 
 // res: also get_residual of level l (A tnew - RHS with the halo refreshed from tnew, :725-873) before
 // the call changes tnew -- computed by the call's first tile sweep from the iterate and snapshot it
@@ -745,7 +849,15 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
         }
         const unsigned f0 = L.chain_epoch;
         L.chain_epoch += (unsigned)run + 1;
-        const bool guard = chain_guard_on();
+        const bool guard = chain_guard_on(), gated = guard && chain_gate_on();
+        ChainGate G;
+        if (gated) {
+            CHK(face_gate_setup(h));
+            if (h->gates.size() >= kGateRing / 2) CHK(face_gates_drain(h));   // (the status ring's reuse)
+            G.gate = h->gate;
+            G.stat = h->gate_stat;
+            G.seq = h->gate_seq;
+        }
         {
             // the state crosses HBM once per call: tnew_nonlin and RHS in, tnew (+ tnew_nonlin) out
             Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
@@ -753,12 +865,21 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
             HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags,
                                         L.chain_nb_off, L.chain_nb_list, h->chain_tmo, run, sweeps,
                                         dead_last ? 2 : both ? 3 : 1,
-                                        h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, src_is_T, f0, guard ? 1 : 0));
+                                        h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, src_is_T, f0, guard ? 1 : 0, G));
         }
         // fail safe: a launch whose workgroups were not all resident (a CU-masked stream, another stream's or
-        // process's kernels on the CUs) aborted before touching anything -- the call runs below, one launch
-        // per sweep, from the same input and halo snapshot (the host waits for the chain to know)
+        // process's kernels on the CUs) aborted before touching anything -- the call runs with one launch per
+        // sweep, from the same input and halo snapshot: gated, the stream waits for the launch's report and the
+        // host runs it when it reads the report back (face_gates_drain, at the latest when the API call ends);
+        // PAMG_CHAIN_GATE=0, the host waits for the chain and runs it below
         if (!guard) return PAMG_OK;
+        if (gated) {
+            h->gate_seq += 1;
+            h->gate_base += 1;
+            HIPCHK(h, hipStreamWaitValue64(h->stream, h->gate, h->gate_base, hipStreamWaitValueGte));
+            h->gates.push_back({G.seq, h->gate_base, l, sweeps, run, dead_last, src_is_T, both, L.T, L.TNN, L.RHS});
+            return PAMG_OK;
+        }
         if (!h->guard_host) HIPCHK(h, hipHostMalloc((void **)&h->guard_host, sizeof(unsigned)));
         HIPCHK(h, hipMemcpyAsync(h->guard_host, h->chain_tmo + 3, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
         CHK(sync_stream(h, h->stream));
@@ -777,21 +898,7 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
         if (both) HIPCHK(h, launch_copy(h->stream, L.TNN, L.T, 3 * L.pitch));
         return PAMG_OK;
     }
-    for (int s = 0; s < run; ++s) {
-        const bool fin = s + 1 == run;
-        // read tnew_nonlin, RHS; write tnew_nonlin (+ tnew in the last sweep, + the next halo words)
-        const int store = fin ? (dead_last ? 2 : 1) : 0;
-        const bool r = s == 0 && res_in_sweep;
-        if (r) h->rhsn_valid = false;
-        Span sp(h, kid, (store == 1 ? 96.0 : 72.0) * (double)L.N + (r ? 24.0 * (double)L.N : 0.0) + 168.0 * h->U);
-        HIPCHK(h, launch_face_sweep_fused(h->stream, L, buf[(sweeps - 1 - s) & 1],
-                                          s + 1 < sweeps ? buf[(sweeps - 2 - s) & 1] : nullptr, h->tovo,
-                                          h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, store, s == 0,
-                                          s == 0 && src_is_T, r ? L.RES : nullptr));
-        if (s + 1 < sweeps) CHK(halo(h, l, buf[(sweeps - 2 - s) & 1]));   // the next sweep's remote words
-    }
-    if (both) HIPCHK(h, launch_copy(h->stream, L.TNN, L.T, 3 * L.pitch));
-    return PAMG_OK;
+    return face_call_sweeps(h, l, sweeps, run, dead_last, src_is_T, both, res_in_sweep);
 }
 
 // `sweeps` sweeps on level l reading the iterate from T (src_is_T: the leg
@@ -1191,7 +1298,9 @@ int face_pp_level(pamg_handle *h, int l, bool last) {
         CHK(face_call(h, l, true, ns, true));   // :331 via :351
         Level &V = h->lv[l];
         h->rhsn_valid = false;
-        {
+        // the coarsest level's get_residual (:338): nothing restricts or reads it (restrictor(L) is empty,
+        // splitting.F90:18), and the next cycle rewrites it -- only the call's last cycle's is state
+        if (last) {
             Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)V.N + 168.0 * h->U);
             HIPCHK(h, launch_face_residual(h->stream, V, h->tov, false, l == 1, rdt, h->slots));
         }
@@ -1279,6 +1388,7 @@ int vcycle_face_fused(pamg_handle *h, int n) {
             CHK(face_call(h, l, true, ns, true));
             CHK(restrict_(h, l));
             if (l < L) continue;   // levels < L: get_residual rides on the prolongation-leg call below
+            if (!last) continue;   // the coarsest level's: read by nothing, rewritten next cycle (face_pp_level)
             Level &V = h->lv[l];
             h->rhsn_valid = false;
             Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)V.N + 168.0 * h->U);   // tnew, RHS in, residual out
@@ -2661,13 +2771,18 @@ int pamg_last_error(pamg_handle *h, char *buf, int len) {
 int pamg_destroy(pamg_handle *h) {
     if (!h) return PAMG_OK;
     (void)hipSetDevice(h->device);
+    (void)face_gates_drain(h);
     (void)hipStreamSynchronize(h->stream);
+    if (h->stream_fb) (void)hipStreamSynchronize(h->stream_fb);
     (void)hipStreamSynchronize(h->stream_comm);
     if (h->stream_c) (void)hipStreamSynchronize(h->stream_c);
     free_levels(h);
     dev_free(h->scratch);
     dev_free(h->chain_tmo);
     if (h->guard_host) (void)hipHostFree(h->guard_host);
+    if (h->gate) (void)hipFree(h->gate);
+    if (h->gate_stat) (void)hipHostFree(h->gate_stat);
+    if (h->stream_fb) (void)hipStreamDestroy(h->stream_fb);
     dev_free(h->xc_done);
     dev_free(h->xe_done);
     for (auto e : h->xe_ev)

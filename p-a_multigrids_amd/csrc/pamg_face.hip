@@ -1325,13 +1325,23 @@ __device__ __forceinline__ bool chain_enter(unsigned *g, unsigned *aborted) {
     __syncthreads();
     return go != 0;
 }
-__device__ __forceinline__ void chain_leave(unsigned *g) {
+// The launch's gate (ChainGate, pamg_internal.h; null gate: the host reads *aborted after the launch): the last
+// workgroup out reports the launch in the host's pinned status ring (seq << 1 | aborted) and, when it ran, adds 1 to
+// the gate signal the stream waits on before the call's next launch -- an aborted launch leaves the stream waiting
+// until the host has run the fallback (pamg_api.cpp face_gates_drain)
+__device__ __forceinline__ void chain_leave(unsigned *g, const ChainGate &G) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned e = __hip_atomic_fetch_add((g_u32 *)g + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (e + 1 == gridDim.x) {
+            const unsigned ab = __hip_atomic_load((g_u32 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kGuardAbort;
             __hip_atomic_store((g_u32 *)g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store((g_u32 *)g + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (G.gate) {
+                __hip_atomic_store(G.stat + (G.seq & (kGateRing - 1)), (G.seq << 1) | (ab ? 1ull : 0ull), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                if (!ab) __hip_atomic_fetch_add(G.gate, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
 }
@@ -1386,9 +1396,9 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                                                           int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                           double rdt, double omega, const int *__restrict__ cpos,
                                                           int nup, int nui, int early, unsigned f0, int snap_ok,
-                                                          long long *stamps, int guard) {
+                                                          long long *stamps, int guard, ChainGate G) {
     if (guard && !chain_enter(tmo + 1, tmo + 3)) {   // not co-resident: leave the state to the host's fallback
-        chain_leave(tmo + 1);
+        chain_leave(tmo + 1, G);
         return;
     }
     constexpr int NT = kChainNT, PER = kChainPer;
@@ -1698,7 +1708,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain(double *T, double *T
                 if (store >= 2) T[c * pitch + s0 + j] = X[c][j];
             }
     }
-    if (guard) chain_leave(tmo + 1);
+    if (guard) chain_leave(tmo + 1, G);
 }
 
 // ---- the chain with un_eles owned by waves (PAMG_CHAIN_PW, default where it applies): the red-black
@@ -1727,10 +1737,10 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
                                                                int64_t pitch, int64_t N, int nsub_log2, int slots, int level1,
                                                                double rdt, double omega, const int *__restrict__ cpos,
                                                                int nup, int nui, int early, unsigned f0, int snap_ok,
-                                                               long long *stamps, int guard) {
+                                                               long long *stamps, int guard, ChainGate G) {
     (void)omega;
     if (guard && !chain_enter(tmo + 1, tmo + 3)) {   // not co-resident: leave the state to the host's fallback
-        chain_leave(tmo + 1);
+        chain_leave(tmo + 1, G);
         return;
     }
     constexpr int NT = kChainNT;
@@ -2094,7 +2104,7 @@ __global__ __launch_bounds__(kChainNT, 1) void k_face_chain_pw(double *T, double
             if (store != 2) TNN[c * pitch + s0 + j] = LM[c * XP + j];
             if (store >= 2) T[c * pitch + s0 + j] = LM[c * XP + j];
         }
-    if (guard) chain_leave(tmo + 1);
+    if (guard) chain_leave(tmo + 1, G);
 }
 
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -2323,8 +2333,9 @@ bool face_chain_fits(int nsub, int U, int cus) {
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
                              int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T,
-                             unsigned f0, int guard) {
+                             unsigned f0, int guard, ChainGate G) {
     if (L.N == 0 || run <= 0) return hipSuccess;
+    if (G.gate && (!guard || !G.stat)) return hipErrorInvalidValue;   // the gate reports the guard's outcome
     // store 1: tnew := the iterate before the last sweep, tnew_nonlin := the last; 2: tnew := the last (a dead
     // last sweep); 3: both := the last (the corrected cycle's coarsest call, tnew := tnew_nonlin after it)
     if (!face_chain_fits(L.nsub, U, cus) || !L.fnb || store < 1 || store > 3) return hipErrorInvalidValue;
@@ -2368,7 +2379,7 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     int snap_ok = !(snap_env && atoi(snap_env) == 0);
     void *args[] = {&T, &TNN, &SRC, &RHS, &stc, &fnb, &fface, &fsx, &tov, &tov_b, &H, &flags, &nb_off, &nb_list, &tmo,
                     &run, &total, &store, (void *)&E, &pitch, &N, &lg, &slots, &l1, &rdt, &omega, &cpos, &nup, &nui, &early, &f0,
-                    &snap_ok, &stamps, &guard};
+                    &snap_ok, &stamps, &guard, &G};
     // the LDS records and item lists need the colour lists' sizes to fit the items (KU = 2, KD = 1)
     const bool uni = L.nsub >= 64,
                lrec = k <= kChainRec && L.cpos && (int64_t)k * L.nup <= 2 * kChainNT && (int64_t)k * L.ndn <= kChainNT;

@@ -220,6 +220,20 @@ struct pamg_handle {
                                      // ([1..2] the chain's co-residency guard, [3] its aborts)
     unsigned *guard_host = nullptr;  // pinned: the chain's abort count, read after each guarded launch
     bool chain_pending = false;      // a chain or wavefront launch ran since face_chain_check last read it
+    // the guarded chain launches' gates (face_call, PAMG_CHAIN_GATE): the stream waits on `gate` (signal
+    // memory) after each launch for the count the launch adds when it ran; an aborted one leaves the stream
+    // waiting until the host has run the call's fallback (face_gates_drain) -- the host no longer waits for
+    // each launch. gate_stat: pinned ring of the launches' reports (seq << 1 | aborted, kGateRing entries)
+    unsigned long long *gate = nullptr, *gate_stat = nullptr;
+    unsigned long long gate_seq = 1, gate_base = 0;   // next launch's tag; the gate's count so far
+    struct GatePending {
+        unsigned long long seq, want;
+        int l, sweeps, run;
+        bool dead_last, src_is_T, both;
+        double *T, *TNN, *RHS;   // the level's buffers at the launch (level 2's RHS is swapped within a call)
+    };
+    std::vector<GatePending> gates;   // in stream order, not yet read back
+    hipStream_t stream_fb = nullptr;  // the gated fallback's launches (the handle's stream waits at the gate)
     // the face operator's wavefront calls (k_face_wave; lazy, single domain): the ticket order (a
     // reverse Cuthill-McKee numbering of neig_local), its band, the neighbours on the device and the
     // per-un_ele flags + ticket counter
@@ -434,10 +448,16 @@ hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, doub
                             const int *order, unsigned *tmo, int run, int total, int store, bool rb, bool level1,
                             double rdt, int slots, bool from_T = false);
 int face_chain_per_wg(int nsub, int U, int cus);
+// a chain launch's gate report (pamg_face.hip chain_leave; gate null: none)
+constexpr unsigned long long kGateRing = 1024;
+struct ChainGate {
+    unsigned long long *gate = nullptr, *stat = nullptr;
+    unsigned long long seq = 0;
+};
 hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, double *tov, double *tov_b, double *tovo,
                              unsigned *flags, const int *nb_off, const int *nb_list, unsigned *tmo, int run, int total,
                              int store, bool rb, bool level1, double rdt, double omega, int slots, bool from_T = false,
-                             unsigned f0 = 0, int guard = 0);
+                             unsigned f0 = 0, int guard = 0, ChainGate G = ChainGate());
 hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, double rdt);
 hipError_t launch_sweep_stencil(hipStream_t s, const Level &L, double *out, double rdt);
 }  // namespace pamg
