@@ -602,6 +602,10 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_WAVES256
 #define PAMG_FACE_PP_WAVES256 4
 #endif
+// ... its instances without the folded interpolation (A/B)
+#ifndef PAMG_FACE_PP_WAVES256_PLAIN
+#define PAMG_FACE_PP_WAVES256_PLAIN 4
+#endif
 #ifndef PAMG_FACE_PP_BLDS
 #define PAMG_FACE_PP_BLDS 1
 #endif
@@ -634,7 +638,7 @@ __device__ __forceinline__ void pp_stamp(int i) {
 #define PAMG_FACE_PP_FOLD_WAVES PAMG_FACE_PP_WAVES
 #endif
 template <int TS, int NT, bool RB, int K, bool FOLD = false>
-__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? PAMG_FACE_PP_WAVES256 : FOLD ? PAMG_FACE_PP_FOLD_WAVES : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
+__global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256 : PAMG_FACE_PP_WAVES256_PLAIN) : FOLD ? PAMG_FACE_PP_FOLD_WAVES : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, double *out_end2,
     const double *__restrict__ RHS,
     const double *__restrict__ stc, const int4 *__restrict__ fnb, const double *__restrict__ fface,
