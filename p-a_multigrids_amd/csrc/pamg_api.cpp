@@ -1288,6 +1288,18 @@ int face_pp_emit(pamg_handle *h, int l, const PPPass &q) {
     return PAMG_OK;
 }
 
+// the coarsest level's two smoother calls of a cycle that is not the call's last as ONE call: the restriction
+// leg's (:331, ns sweeps, the last dead: tnew := sweep ns - 1) and the coarse solve's (:344-359, ns n_coarse
+// sweeps from tnew, the last dead). Between them the cycle computes only the coarsest residual (:338), which
+// such a cycle skips (face_pp_level), and the second call's leg copy tnew_nonlin := tnew (:348) continues from
+// the first call's tnew: one call of (ns - 1) + (ns n_coarse - 1) executed sweeps and a dead last one, whose
+// halo words at the seam are the ones the first call's last executed sweep published -- the words of that tnew,
+// as the second call's refresh would write them. PAMG_FACE_COARSE_MERGE=0: the two calls (A/B).
+bool face_coarse_merged(pamg_handle *h, bool last) {
+    const char *e = getenv("PAMG_FACE_COARSE_MERGE");   // read per call: tests switch it within a process
+    return !last && h->p.n_smooth >= 1 && h->p.n_coarse >= 1 && !(e && atoi(e) == 0);
+}
+
 // level l's part of cycle c of the fused face cycle (levels l .. L): the coarsest level's calls; a level
 // below it as a two-sweep stream (its restrictor before the launch that writes its new residual, then the
 // next level), or as its two calls around the next level (vcycle_face_fused's order)
@@ -1295,6 +1307,7 @@ int face_pp_level(pamg_handle *h, int l, bool last) {
     const int L = h->p.multi_levels, ns = h->p.n_smooth;
     const double rdt = 1 / h->p.dt;
     if (l == L) {
+        if (face_coarse_merged(h, last)) return face_call(h, L, true, ns + ns * h->p.n_coarse - 1, true);
         CHK(face_call(h, l, true, ns, true));   // :331 via :351
         Level &V = h->lv[l];
         h->rhsn_valid = false;
@@ -1385,6 +1398,7 @@ int vcycle_face_fused(pamg_handle *h, int n) {
     for (int c = 0; c < n; ++c) {
         const bool last = c + 1 == n;
         for (int l = 1; l <= L; ++l) {   // :323-340
+            if (l == L && face_coarse_merged(h, last)) break;   // (the call below runs both)
             CHK(face_call(h, l, true, ns, true));
             CHK(restrict_(h, l));
             if (l < L) continue;   // levels < L: get_residual rides on the prolongation-leg call below
@@ -1394,7 +1408,8 @@ int vcycle_face_fused(pamg_handle *h, int n) {
             Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)V.N + 168.0 * h->U);   // tnew, RHS in, residual out
             HIPCHK(h, launch_face_residual(h->stream, V, h->tov, false, l == 1, rdt, h->slots));
         }
-        CHK(face_call(h, L, true, ns * h->p.n_coarse, !last));   // :344-359
+        if (face_coarse_merged(h, last)) CHK(face_call(h, L, true, ns + ns * h->p.n_coarse - 1, true));
+        else CHK(face_call(h, L, true, ns * h->p.n_coarse, !last));   // :344-359
         // :363-378; the residual of the restriction leg (:336) is due after the level's call there, and
         // nothing changes level l's tnew, RHS or halo words until this call starts: it computes it
         for (int l = L - 1; l >= 1; --l) CHK(face_call(h, l, true, ns, !last, true));
