@@ -44,6 +44,11 @@ CASES = {
     "irregular_s3_l3":     ("irregular.msh", 3, 3, 4, 3, 2, 2, 0, "fp64", None),
     "e900_s2_l2_jacobi":   ("900_ele.msh", 2, 2, 4, 1, 1, 2, 0, "fp64", None),
     "u8192_s3_l3_1cycle":  ("untitled8192.msh", 3, 3, 4, 3, 1, 1, 0, "fp64", 16384),
+    # the benchmarked instances: the bench workload's own shape (S = 5, the resident
+    # k_vc_resb tiles), config 5's mesh at S = 6 (sub-un_ele tiles) and config 2's exact shape
+    "u8192_s5_l3":         ("untitled8192.msh", 5, 3, 4, 3, 1, 2, 0, "fp64", 32768),
+    "irregular_s6_l3":     ("irregular.msh", 6, 3, 4, 3, 1, 2, 0, "fp64", None),
+    "e900_s3_l3_jacobi":   ("900_ele.msh", 3, 3, 4, 1, 1, 2, 0, "fp64", None),
 }
 
 
