@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # lanes x 2 flops x 2.4 GHz)
 FP64_PEAK_TFLOPS = 78.6
 EVENT_STRIDE = 10
-ALL_CLASSES = 0xFF7F   # every timing class (PAMG_K_*) but sweep_bench
+ALL_CLASSES = 0x2FF7F   # every timing class (PAMG_K_*) but sweep_bench (bit 16 face_fallback counts regardless)
 SWEEP_LAUNCHES = 60    # launches of each level-1 HBM sweep roofline measurement
 
 
@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     # 200 warm-up cycles (~30 ms): after 5 (~1 ms) the GPU's clocks have not settled and the
     # timed region reads 6,550 instead of 7,460 V-cycles/s on the same box
-    # (scripts/event_probe.py, profiles/r01_v15_warmup.txt)
+    # (scripts/event_probe.py, archive/profiles/r01_v15_warmup.txt)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--nsplit", type=int, default=5)
@@ -147,15 +147,30 @@ CPU_STRIP = (32, 8)   # 512 un_eles: 1/16 of untitled8192's, the same 4**5 sub-e
 CPU_SHARE = 16        # host cores of a one-GPU share of the box (OMP_NUM_THREADS there)
 
 
+CPU_PAIRS = 3        # independent (1-cycle, 3-cycle) run pairs of the 1-core baseline; the median is reported
+
+
+def spaced_cores(n):
+    """n cores of this process's affinity set, spread out (distinct core complexes where there are many)"""
+    cores = sorted(os.sched_getaffinity(0))
+    if len(cores) <= n:
+        return cores[:n]
+    step = len(cores) // n
+    return [cores[i * step] for i in range(n)]
+
+
 def cpu_baseline():
     """Reference CPU path on this host, measured at the benchmarked n_split = 5 and L = 3: the
     reference Fortran itself (fp64 build, oracle/_ref, 1 core, its own `cpu_time for time_loop`
-    window) on a bounded sample -- one time step of 1 and of 2 V-cycles on a 512-element
-    synthetic strip; the difference is the steady-state cost of one V-cycle (the first cycle of
-    a run carries a one-off cost the second does not). The reference's work is per un_ele
-    (stencils re-derived per un_ele visit, then its 4**n_split sub-elements; nothing couples
-    un_eles in mode 9), so untitled8192's 8192 un_eles take 16x as long; the 16x is checked
-    against the full-size run by scripts/cpu_baseline_probe.py (profiles/r02_cpu_baseline_probe*.txt)."""
+    window) on a bounded sample -- one time step of 1 and of 3 V-cycles on a 512-element
+    synthetic strip; half the difference is the steady-state cost of one V-cycle (the first cycle
+    of a run carries a one-off cost the others do not, and it varies from run to run: round 5's
+    single 2-minus-1 difference read 5.5 s on one box and 9.1 s on another). CPU_PAIRS pairs run at
+    once, each process pinned to its own core (spread over the core complexes); the median pair is
+    the value and the spread is reported. The reference's work is per un_ele (stencils re-derived per
+    un_ele visit, then its 4**n_split sub-elements; nothing couples un_eles in mode 9), so
+    untitled8192's 8192 un_eles take 16x as long; the 16x is checked against the full-size run by
+    scripts/cpu_baseline_probe.py (profiles/r05_final_cpu_baseline_probe.txt: 150.05 s per V-cycle)."""
     import pamg
     tmp = tempfile.mkdtemp(prefix="pamg_cpu_msh_")
     try:
@@ -163,8 +178,13 @@ def cpu_baseline():
         strip = pamg.Mesh.strip(*CPU_STRIP)
         strip.write_msh(path)
         U = strip.U
-        t1 = run_reference(path, 5, 1, 1)
-        t2 = run_reference(path, 5, 1, 2)
+        cores1 = spaced_cores(2 * CPU_PAIRS)
+        procs = [reference_proc(path, 5, 1, nmg, cores1[2 * i + (nmg == 3)]) for i in range(CPU_PAIRS) for nmg in (1, 3)]
+        ts = [reference_wait(p) for p in procs]
+        pairs = [(ts[2 * i], ts[2 * i + 1]) for i in range(CPU_PAIRS)]
+        diffs = sorted((b - a) / 2 for a, b in pairs if a is not None and b is not None and b > a)
+        t1 = sorted(a for a, _ in pairs if a is not None)
+        t1 = t1[len(t1) // 2] if t1 else None
         # the same sample on every core of the GPU's host share at once: the reference is serial and its mode-9
         # un_eles are uncoupled, so CPU_SHARE strips (1/16 of the mesh each) run as independent processes, one
         # per core -- the all-cores figure beside the 1-core baseline
@@ -176,10 +196,10 @@ def cpu_baseline():
             tall[nmg] = [reference_wait(p) for p in procs]
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    if t1 is None or t2 is None or t2 <= t1:
+    if not diffs:
         return None
     scale = 8192 / U
-    tc = t2 - t1
+    tc = diffs[len(diffs) // 2]
     allc = None
     if all(v is not None for v in tall[1] + tall[2]):
         steady = sorted(b - a for a, b in zip(tall[1], tall[2]))
@@ -191,11 +211,16 @@ def cpu_baseline():
                            f"({scale:g} x {tcn:.2f} s)")
     return dict(value=1.0 / (scale * tc), unit="V-cycles/s", cores=1, kind="reference", all_cores=allc,
                 sample=f"reference fp64 build (flang -O2) on 1 core of '{host_cpu()}' at n_split=5, multi_levels=3, "
-                       f"n_smooth=4 on a {U}-element synthetic strip ({CPU_STRIP[0]}x{CPU_STRIP[1]}x2): one time step "
-                       f"of 1 V-cycle took {t1:.2f} s and of 2 V-cycles {t2:.2f} s in its time_loop window; value = "
-                       f"1 / ({scale:g} x {tc:.2f} s), the steady-state V-cycle scaled to untitled8192's 8192 "
-                       f"elements (the reference's work is linear in the element count)",
-                seconds_1cycle=t1, seconds_2cycles=t2, host_cpu=host_cpu())
+                       f"n_smooth=4 on a {U}-element synthetic strip ({CPU_STRIP[0]}x{CPU_STRIP[1]}x2): {CPU_PAIRS} pairs of "
+                       f"one time step of 1 and of 3 V-cycles (each process on its own core), steady-state V-cycle = "
+                       f"(t3 - t1) / 2 per pair = {', '.join(f'{d:.2f}' for d in diffs)} s, median {tc:.2f} s; value = "
+                       f"1 / ({scale:g} x {tc:.2f} s), scaled to untitled8192's 8192 elements (the reference's work is "
+                       f"linear in the element count; full-size check 150.05 s per V-cycle, "
+                       f"profiles/r05_final_cpu_baseline_probe.txt)",
+                pair_seconds=[[round(a, 2) if a else None, round(b, 2) if b else None] for a, b in pairs],
+                steady_cycle_s=[round(d, 3) for d in diffs],
+                spread=round(diffs[-1] / diffs[0], 3) if diffs[0] > 0 else None,
+                seconds_1cycle=t1, host_cpu=host_cpu())
 
 
 SKIP_DIGEST = ("pamg_face.hip", "pamg_mesh.cpp", "pamg_vtu.cpp")

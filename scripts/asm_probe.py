@@ -1,7 +1,7 @@
 """The north star's HBM roofline kernel (k_sweep_assembled, 168 B per sub-element) and the matrix-free sweep
 beside it, on bench.py's level 1 (untitled8192, n_split 5): average of `--launches` evented launches after a
 warm-up, repeated `--reps` times (GPU box only). The block layout comes from PAMG_ASM_LAYOUT, the plane gap
-from PAMG_PITCH_PAD (scripts/r5_e.sh runs the variants in separate processes)."""
+from PAMG_PITCH_PAD (archive/scripts/r5_e.sh runs the variants in separate processes)."""
 import argparse
 import os
 import sys

@@ -4,7 +4,7 @@
 of its arithmetic, tests/test_contracted_oracle.py; arith = 0 is the reference's order). Per
 level: the cancellation factor kappa_l = max|RHS_l| / max|res_l| and the max abs difference of
 every field, relative to the field's own scale and to the scale of the terms it was computed
-from. GPU box; the committed output is profiles/r02_conditioning.txt."""
+from. GPU box; the committed output is archive/profiles/r02_conditioning.txt."""
 import os
 import sys
 

@@ -2,7 +2,7 @@
 n_split = 5 on the 512-element strip bench.py samples and on the full untitled8192.msh, plus
 untitled8192 at n_split = 3 and 4 (the per-sub-element cost across sizes). Every number is the
 reference's own `cpu_time for time_loop` window. ~5 min of CPU on the GPU box's host; writes a table to stdout
-(committed as profiles/r02_cpu_baseline_probe.txt)."""
+(committed as archive/profiles/r02_cpu_baseline_probe.txt)."""
 import os
 import sys
 import tempfile

@@ -2,7 +2,7 @@
 against the reference's ReadMSH + O(U^2) CheckNeig (the oracle's literal restatement,
 oracle/pamg_oracle.c, pinned to the reference; Msh2Tri.F90:323-330, 776-963 -- 99 % of a large
 run in grofiling.txt:6-8). Synthetic strips written as gmsh 2.2 (pamg_msh_write).
-Writes a table to stdout; the committed copy is profiles/r02_ingest_timing.txt."""
+Writes a table to stdout; the committed copy is archive/profiles/r02_ingest_timing.txt."""
 import os
 import sys
 import tempfile

@@ -1,5 +1,5 @@
 """Wall time of the driver's 20-cycle call (vcycle(20) + synchronize) per rank partition of
-untitled8192 S=5, simulated on one GPU (detached, rank 0); GPU box only. profiles/r03_m_sync_probe.txt is its
+untitled8192 S=5, simulated on one GPU (detached, rank 0); GPU box only. archive/profiles/r03_m_sync_probe.txt is its
 A/B of the host wait (mode 0 spin, 1 hipStreamSynchronize, 2 sleeping poll) under a switch
 since removed (the waits measured within noise)."""
 import os

@@ -356,7 +356,7 @@ def test_fused_vcycle_interleaved_with_call_sites_bitwise(mesh, S, L, fused):
 # ones (tnew) -- a bound that does not depend on how far the levels have converged (observed
 # <= 2e-15 of it; on bench.py's workload every level is well conditioned, kappa_l =
 # max|RHS_l| / max|res_l| <= 8, and the same numbers are <= 4e-13 of each level's own RHS scale:
-# profiles/r02_conditioning.txt). With arith = 0 every field is bitwise.
+# archive/profiles/r02_conditioning.txt). With arith = 0 every field is bitwise.
 TOL_CONTRACTED = 1e-12
 SOLUTION = ("tnew_L1", "told_L1", "RHS_L1", "tnew_nonlin", "t_overlap", "t_overlap_old")
 
