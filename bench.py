@@ -44,6 +44,7 @@ import subprocess
 import sys
 import tempfile
 import time
+from datetime import timedelta
 
 import numpy as np
 
@@ -56,6 +57,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # lanes x 2 flops x 2.4 GHz)
 FP64_PEAK_TFLOPS = 78.6
 EVENT_STRIDE = 10
+# the bound of every host collective of a multi-rank run (PAMG_BENCH_RENDEZVOUS_S overrides; tests use a short one)
+RENDEZVOUS_S = int(os.environ.get("PAMG_BENCH_RENDEZVOUS_S", "300"))
 ALL_CLASSES = 0x2FF7F   # every timing class (PAMG_K_*) but sweep_bench (bit 16 face_fallback counts regardless)
 SWEEP_LAUNCHES = 60    # launches of each level-1 HBM sweep roofline measurement
 
@@ -449,7 +452,10 @@ def main():
     import pamg
 
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # every host collective is bounded (RENDEZVOUS_S): a rank that never joins, or never reaches the
+        # communicator's creation, ends the run with an error line instead of a hang -- RCCL's own initialisation
+        # cannot be bounded (pamg_comm_init, profiles/r06_rccl_init_probe.txt), so every rank meets here first
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=RENDEZVOUS_S))
     mesh = pamg.Mesh.read(a.mesh)
 
     def comm_for(_mode=None):
@@ -459,6 +465,7 @@ def main():
             return (world, rank, None, mesh.x_strip_owner(world))
         obj = [pamg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
+        dist.barrier()   # all ranks hold the id and enter pamg_comm_init together
         return (world, rank, obj[0], mesh.x_strip_owner(world))
 
     comm = comm_for()
@@ -773,5 +780,18 @@ def main():
         dist.destroy_process_group()
 
 
+def error_line(e):
+    """one JSON line naming the failing rank and the error (the run exits non-zero)"""
+    return json.dumps({"metric": "multigrid V-cycles/sec + smoother HBM GB/s vs roofline, 8192-ele tri mesh",
+                       "value": None, "error": f"{type(e).__name__}: {e}", "rank": int(os.environ.get("RANK", "0")),
+                       "world_size": int(os.environ.get("WORLD_SIZE", "1"))})
+
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 -- reported as the run's JSON line, then a non-zero exit
+        print(error_line(e), flush=True)
+        sys.exit(1)

@@ -69,7 +69,10 @@ extern "C" {
 #define PAMG_K_FACE_FALLBACK 16  /* face-operator smoother calls whose persistent chain launch found its workgroups not
                                     all resident and left the state untouched: run with one launch per sweep instead
                                     (counted in pamg_timing_issued whatever the timing mask) */
-#define PAMG_K_COUNT 17
+#define PAMG_K_COARSE_GATHER 17  /* op = 1 on a partition: the ranks' coarsest-level blocks (RHS each cycle, tnew once
+                                    per call) gathered into every rank's replica of that level (the agglomerated
+                                    coarsest level: the single-domain chain runs on each rank) */
+#define PAMG_K_COUNT 18
 
 typedef struct pamg_handle pamg_handle;
 typedef struct pamg_mesh pamg_mesh;
@@ -262,8 +265,13 @@ int pamg_comm_unique_id(char out[128]);
  * other ranks is exchanged with grouped ncclSend/ncclRecv after every halo write.
  * RCCL's asynchronous error state is polled at the end of pamg_vcycle / pamg_run and
  * while pamg_synchronize and the getters wait: a failed peer returns PAMG_ERR_COMM (the
- * communicator is aborted) instead of a hang; PAMG_COMM_TIMEOUT_S (seconds), when set, also
- * bounds how long pamg_synchronize waits for the stream to drain. */
+ * communicator is aborted) instead of a hang. Every wait for a stream that carries
+ * exchanges (pamg_synchronize, the getters, the calls that read state back) is bounded by
+ * PAMG_COMM_TIMEOUT_S (seconds, default 120): a rank whose peer stops exchanging returns
+ * PAMG_ERR_COMM within that bound. pamg_comm_init itself blocks until every rank has joined
+ * (RCCL's bootstrap has no bound, profiles/r06_rccl_init_probe.txt): the launcher bounds it
+ * (bench.py: a gloo barrier with a timeout right before it). A failed pamg_comm_init leaves
+ * the handle as it was (no communicator, rank or owner map bound). */
 int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int U, const int *owner);
 int pamg_owned_count(pamg_handle *h);
 /* one-rank RCCL communicator with a self-peer halo plan: the handle owns the whole mesh, but

@@ -31,7 +31,7 @@ namespace pamg {
 // reads of its words (the send completion of ncclSend). Posts carry a per-pair sequence
 // number, so ranks meet exchange by exchange as grouped send/recv calls do.
 struct LocalGroup {
-    struct Post { long seq = 0; const double *ptr = nullptr; hipEvent_t ev = nullptr; };
+    struct Post { long seq = 0; const double *ptr = nullptr; hipEvent_t ev = nullptr; int64_t pitch = 0; };
     int n = 0;
     std::mutex mu;
     std::condition_variable cv;
@@ -115,53 +115,36 @@ hipEvent_t take_event(pamg_handle *h) {
     return e;
 }
 
-// in_packet (the resident launches, one kernel per call) with PAMG_EVENTS_IN_PACKET=1: the pair goes to the
-// launch itself (launch_events, hipExtLaunchKernel), which records it in its dispatch packet around the
-// kernel, instead of two marker packets (a marker pair costs ~26 us per 20-cycle call in the driver's shape,
-// profiles/r05_a_shape_probe.txt; A/B runs)
-bool events_in_packet() {
-    static const bool on = getenv("PAMG_EVENTS_IN_PACKET") && atoi(getenv("PAMG_EVENTS_IN_PACKET")) == 1;
-    return on;
-}
+// an event pair around the work issued in a scope, on stream s, when its timing class is enabled (one in
+// `stride` of its spans). (Events recorded in the resident launch's own dispatch packet, hipExtLaunchKernel,
+// measured no cheaper than the marker pair: profiles/r05_a_shape_probe.txt, r05_c_events_ab.txt; removed.)
 struct Span {
-    pamg_handle *h; int kid; double bytes; hipStream_t s; hipEvent_t a = nullptr, b = nullptr; bool pk = false;
-    Span(pamg_handle *h_, int kid_, double bytes_, hipStream_t s_ = nullptr, bool in_packet = false)
-        : h(h_), kid(kid_), bytes(bytes_), s(s_ ? s_ : h_->stream) {
+    pamg_handle *h; int kid; double bytes; hipStream_t s; hipEvent_t a = nullptr, b = nullptr;
+    Span(pamg_handle *h_, int kid_, double bytes_, hipStream_t s_ = nullptr)
+        : h(h_->tparent ? h_->tparent : h_), kid(kid_), bytes(bytes_), s(s_ ? s_ : h_->stream) {
         if ((h->timing.mask & (1u << kid)) && h->timing.seq[kid]++ % h->timing.stride == 0) {
             a = take_event(h);
-            if (in_packet && events_in_packet()) {
-                pk = true;
-                b = take_event(h);
-                launch_events() = LaunchEvents{a, b, false};
-            } else {
-                (void)hipEventRecord(a, s);
-            }
+            (void)hipEventRecord(a, s);
         }
     }
     ~Span() {
         if (!a) return;
-        if (pk) {
-            LaunchEvents &E = launch_events();
-            const bool used = E.used;
-            E = LaunchEvents{};
-            if (!used) {   // the launch did not take them (an error path): nothing was recorded
-                h->timing.pool.push_back(a);
-                h->timing.pool.push_back(b);
-                return;
-            }
-        } else {
-            b = take_event(h);
-            (void)hipEventRecord(b, s);
-        }
+        b = take_event(h);
+        (void)hipEventRecord(b, s);
         h->timing.pending.push_back(Timing::Rec{kid, a, b, bytes});
     }
 };
 
+int settle(pamg_handle *h);
+int sync_stream(pamg_handle *h, hipStream_t s);
 int drain_timing(pamg_handle *h) {
     auto &T = h->timing;
     if (T.pending.empty()) return PAMG_OK;
-    CHK(face_gates_drain(h));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    // spans may sit on the comm stream (the exchange spans, the early exchange's): the stream joins every
+    // exchange in flight first, and the comm stream is drained too, so no event pair is read before it ran
+    CHK(settle(h));
+    CHK(sync_stream(h, h->stream));
+    CHK(sync_stream(h, h->stream_comm));
     for (auto &r : T.pending) {
         float ms = 0.f;
         HIPCHK(h, hipEventElapsedTime(&ms, r.a, r.b));
@@ -212,6 +195,55 @@ int local_timeout_s() {
     const int t = e ? atoi(e) : 120;
     return t > 0 ? t : 120;
 }
+
+// Bounded RCCL waits. A grouped send/recv that answers ncclInProgress is polled here for at
+// most PAMG_COMM_TIMEOUT_S (default 120 s, the local group's exchange bound), and every host wait for a stream
+// that carries exchanges is bounded the same way (sync_stream); on the bound or an error the communicator is
+// aborted, so a rank that stops issuing exchanges ends its peers' calls with PAMG_ERR_COMM instead of hanging
+// them. The communicator's initialisation cannot be bounded from here: RCCL 2.27's bootstrap waits for every
+// rank, and a non-blocking communicator (ncclConfig_t::blocking = 0) blocked inside ncclCommInitRankConfig
+// itself, while a blocking init left on a helper thread faults the process at exit
+// (profiles/r06_rccl_init_probe.txt). The caller's launcher bounds it (bench.py: a gloo barrier with a timeout
+// right before pamg_comm_init), and the communicator stays blocking.
+int nccl_settle(ncclComm_t c, ncclResult_t r, int limit_s, std::string &err, const char *what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(limit_s)) {
+            err = std::string(what) + ": not complete within " + std::to_string(limit_s) +
+                  " s (PAMG_COMM_TIMEOUT_S); a peer rank did not join or stopped";
+            return PAMG_ERR_COMM;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (ncclCommGetAsyncError(c, &r) != ncclSuccess) r = ncclSystemError;
+    }
+    if (r != ncclSuccess) {
+        err = std::string(what) + ": " + ncclGetErrorString(r);
+        return PAMG_ERR_COMM;
+    }
+    return PAMG_OK;
+}
+
+// a grouped send/recv's end: polled to completion of its enqueueing; the communicator aborted on failure
+int nccl_group_end(pamg_handle *h) {
+    const ncclResult_t r = ncclGroupEnd();
+    const int rc = nccl_settle(h->comm->nccl, r, local_timeout_s(), h->err, "ncclGroupEnd (halo exchange)");
+    if (rc != PAMG_OK) {
+        (void)ncclCommAbort(h->comm->nccl);
+        h->comm->nccl = nullptr;
+    }
+    return rc;
+}
+
+// ncclSend / ncclRecv inside a group only enqueue (a non-blocking communicator may answer ncclInProgress)
+#define NCCLQ(h, expr)                                                                    \
+    do {                                                                                  \
+        ncclResult_t r_ = (expr);                                                         \
+        if (r_ != ncclSuccess && r_ != ncclInProgress) {                                  \
+            (void)ncclGroupEnd();                                                         \
+            (h)->err = std::string(#expr) + ": " + ncclGetErrorString(r_);                \
+            return PAMG_ERR_COMM;                                                         \
+        }                                                                                 \
+    } while (0)
 
 // w words per entry (6: tnew and told; 3: the tnew words of the resident call's ring), into recv
 int exchange_local(pamg_handle *h, int l, const double *send, hipStream_t st, int w, double *recv) {
@@ -289,11 +321,11 @@ int exchange(pamg_handle *h, int l, int buf, hipStream_t st, double *dst = nullp
         const int peer = P.peers[q];
         const size_t ns = (size_t)(P.send_peer_off[q + 1] - P.send_peer_off[q]);
         const size_t nr = (size_t)(P.recv_peer_off[q + 1] - P.recv_peer_off[q]);
-        if (ns) NCCLCHK(h, ncclSend(send + 6 * (size_t)P.send_peer_off[q], 6 * ns, ncclDouble, peer, h->comm->nccl, st));
-        if (nr) NCCLCHK(h, ncclRecv(P.d_recv + 6 * (size_t)P.recv_peer_off[q], 6 * nr, ncclDouble, peer,
-                                    h->comm->nccl, st));
+        if (ns) NCCLQ(h, ncclSend(send + 6 * (size_t)P.send_peer_off[q], 6 * ns, ncclDouble, peer, h->comm->nccl, st));
+        if (nr) NCCLQ(h, ncclRecv(P.d_recv + 6 * (size_t)P.recv_peer_off[q], 6 * nr, ncclDouble, peer,
+                                  h->comm->nccl, st));
     }
-    NCCLCHK(h, ncclGroupEnd());
+    CHK(nccl_group_end(h));
     HIPCHK(h, launch_halo_unpack(st, L, dst, h->tovo));
     return PAMG_OK;
 }
@@ -315,11 +347,11 @@ int exchange_ring(pamg_handle *h, int c, hipStream_t st) {
         const int peer = P.peers[q];
         const size_t ns = (size_t)(P.send_peer_off[q + 1] - P.send_peer_off[q]);
         const size_t nr = (size_t)(P.recv_peer_off[q + 1] - P.recv_peer_off[q]);
-        if (ns) NCCLCHK(h, ncclSend(send + 3 * (size_t)P.send_peer_off[q], 3 * ns, ncclDouble, peer, h->comm->nccl, st));
-        if (nr) NCCLCHK(h, ncclRecv(P.d_recv3 + 3 * (size_t)P.recv_peer_off[q], 3 * nr, ncclDouble, peer,
-                                    h->comm->nccl, st));
+        if (ns) NCCLQ(h, ncclSend(send + 3 * (size_t)P.send_peer_off[q], 3 * ns, ncclDouble, peer, h->comm->nccl, st));
+        if (nr) NCCLQ(h, ncclRecv(P.d_recv3 + 3 * (size_t)P.recv_peer_off[q], 3 * nr, ncclDouble, peer,
+                                  h->comm->nccl, st));
     }
-    NCCLCHK(h, ncclGroupEnd());
+    CHK(nccl_group_end(h));
     HIPCHK(h, launch_halo_unpack3(st, L, h->tov));
     return PAMG_OK;
 }
@@ -389,17 +421,6 @@ int xe_setup(pamg_handle *h) {
     return PAMG_OK;
 }
 
-// PAMG_PITCH_PAD=<doubles> (A/B runs, rounded to 64): a gap between the state planes of a level, so that
-// the planes of one sub-element are not a power-of-two distance apart (64 MiB at n_split = 5)
-int64_t plane_pad() {
-    static const int64_t pad = getenv("PAMG_PITCH_PAD") ? (std::max(0L, atol(getenv("PAMG_PITCH_PAD"))) + 63) / 64 * 64 : 0;
-    return pad;
-}
-
-bool early_xc_enabled() {
-    static const bool on = !(getenv("PAMG_EARLY_XC") && atoi(getenv("PAMG_EARLY_XC")) == 0);
-    return on;
-}
 
 int halo(pamg_handle *h, int l, double *dst = nullptr) {
     const HaloPlan &P = h->lv[l].halo;
@@ -436,8 +457,13 @@ int join_comm(pamg_handle *h) {
 
 // the entry of a call that may read or write what an exchange still in flight touches (the send and receive
 // buffers, t_overlap, t_overlap_old): its work waits for the exchange (the resident call's early exchange is
-// not joined when the call returns, vcycle_fused)
-int settle(pamg_handle *h) { return h->comm ? join_comm(h) : PAMG_OK; }
+// not joined when the call returns, vcycle_fused). A gated chain launch still unread also blocks the stream
+// until the host reads its report (face_gates_drain): every entry reads them first, so no later host wait or
+// implicit device synchronisation (hipFree) can wait on a gate that only this thread would open
+int settle(pamg_handle *h) {
+    CHK(face_gates_drain(h));
+    return h->comm ? join_comm(h) : PAMG_OK;
+}
 
 // RCCL's asynchronous error state (polled at the ends of the hot-path calls): a
 // failed peer or link is reported as PAMG_ERR_COMM instead of a hang in the next exchange
@@ -471,10 +497,10 @@ int sync_stream(pamg_handle *h, hipStream_t s) {
         HIPCHK(h, hipStreamSynchronize(s));
         return PAMG_OK;
     }
-    const char *env = getenv("PAMG_COMM_TIMEOUT_S");
-    // unset: no limit on an RCCL rank (only the error polling), the exchange bound on a local group
-    const int limit = env ? atoi(env) : h->comm->local ? local_timeout_s() : 0;
-    static const int spin_ms = getenv("PAMG_SYNC_SPIN_MS") ? std::max(0, atoi(getenv("PAMG_SYNC_SPIN_MS"))) : 5;
+    // PAMG_COMM_TIMEOUT_S (default 120 s) on both transports: a peer that never issues its side of an exchange
+    // ends this rank's wait with PAMG_ERR_COMM (RCCL's error state does not report a missing peer)
+    const int limit = local_timeout_s();
+    constexpr int spin_ms = 5;
     const auto t0 = std::chrono::steady_clock::now();
     const auto spin_end = t0 + std::chrono::milliseconds(spin_ms);
     for (unsigned i = 0;; ++i) {
@@ -511,6 +537,11 @@ int sync_stream(pamg_handle *h, hipStream_t s) {
 bool face_chain_ok(pamg_handle *h, int l) {
     const char *ev = getenv("PAMG_FACE_CHAIN");   // read per call: tests switch it within a process
     if ((ev && atoi(ev) == 0) || h->nranks != 1 || h->comm || h->neig_local.empty()) return false;
+    // the coarsest-level replica of a partition in a local group (pamg_comm_local_group: every rank's handle in
+    // one process, on one GPU): the ranks' chains would compete for the same CUs, and an aborted one's fallback
+    // (the host's launches on stream_fb) can sit behind another rank's gate in a shared hardware queue -- such a
+    // replica runs its calls one launch per sweep (bitwise the chain). One process per GPU keeps the chain.
+    if (h->tparent && h->tparent->comm && h->tparent->comm->local) return false;
     if (!h->cus) {
         int n = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || n <= 0) n = 1;
@@ -648,14 +679,6 @@ int face_wave_grid_for(pamg_handle *h, int l, int run) {
     return g;
 }
 
-// PAMG_CHAIN_GUARD=0 (A/B): the chain's workgroups start without the co-residency guard and the host does
-// not wait for each chain launch (a launch that is not co-resident then gives up on its bounded spins and the
-// call fails, face_chain_check)
-bool chain_guard_on() {
-    const char *e = getenv("PAMG_CHAIN_GUARD");   // read per call: tests switch it within a process
-    return !(e && atoi(e) == 0);
-}
-
 // the give-up word of the chain's and the wavefront's bounded spins: a call that hit it failed, and
 // the state it left was computed from halo words that had not all arrived -- the handle's fields are
 // invalid after the error (set them again, or start a new time step from a known tnew). Checked only
@@ -665,6 +688,10 @@ int face_gates_drain(pamg_handle *h);
 
 int face_chain_check(pamg_handle *h) {
     CHK(face_gates_drain(h));
+    if (h->agg) {
+        const int rc = face_chain_check(h->agg);
+        if (rc != PAMG_OK) { h->err = h->agg->err; return rc; }
+    }
     if (!h->chain_tmo || !h->chain_pending) return PAMG_OK;
     h->chain_pending = false;
     unsigned v = 0;
@@ -679,11 +706,8 @@ int face_chain_check(pamg_handle *h) {
 }
 
 // a sweep as one launch on LDS tiles (k_face_tile / k_face_sweep) instead of the two colour
-// launches (PAMG_FACE_FUSED=0: the per-colour kernels)
-bool face_tiles_ok(pamg_handle *h, int l) {
-    static const bool fuse_env = !getenv("PAMG_FACE_FUSED") || atoi(getenv("PAMG_FACE_FUSED")) != 0;
-    return fuse_env && h->p.op == 1 && face_sweep_fusable(h->lv[l]);
-}
+// launches (the per-colour kernels remain for the level shapes the tiles do not cover)
+bool face_tiles_ok(pamg_handle *h, int l) { return h->p.op == 1 && face_sweep_fusable(h->lv[l]); }
 
 // ... and the whole smoother call with the halo words handed from sweep to sweep on the device
 // (face_call): a single domain (a partition exchanges them between sweeps)
@@ -716,13 +740,6 @@ int face_call_sweeps(pamg_handle *h, int l, int sweeps, int run, bool dead_last,
     return PAMG_OK;
 }
 
-// PAMG_CHAIN_GATE=0 (A/B): the host waits for each guarded chain launch (round 5's first form) instead of
-// gating the stream on the launch's own report
-bool chain_gate_on() {
-    const char *e = getenv("PAMG_CHAIN_GATE");   // read per call: tests switch it within a process
-    return !(e && atoi(e) == 0);
-}
-
 int face_gate_setup(pamg_handle *h) {
     if (h->gate) return PAMG_OK;
     // the stream waits on it (hipStreamWaitValue64): HIP's signal memory, as xc_sig
@@ -741,6 +758,10 @@ int face_gate_setup(pamg_handle *h) {
 // runs here with one launch per sweep on stream_fb, from the input and snapshot the aborted launch left
 // untouched, and then opens the gate). Every host wait on the handle's stream drains them first.
 int face_gates_drain(pamg_handle *h) {
+    if (h->agg) {   // the coarsest level's replica runs its chains on this handle's stream
+        const int rc = face_gates_drain(h->agg);
+        if (rc != PAMG_OK) { h->err = h->agg->err; return rc; }
+    }
     while (!h->gates.empty()) {
         const pamg_handle::GatePending g = h->gates.front();
         h->gates.erase(h->gates.begin());
@@ -783,7 +804,7 @@ int face_gates_drain(pamg_handle *h) {
             if (h->err.empty()) h->err = "face chain: the gated fallback failed to launch";
             return rc;
         }
-        h->timing.seq[PAMG_K_FACE_FALLBACK] += 1;
+        (h->tparent ? h->tparent : h)->timing.seq[PAMG_K_FACE_FALLBACK] += 1;
     }
     return PAMG_OK;
 }
@@ -849,15 +870,12 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
         }
         const unsigned f0 = L.chain_epoch;
         L.chain_epoch += (unsigned)run + 1;
-        const bool guard = chain_guard_on(), gated = guard && chain_gate_on();
         ChainGate G;
-        if (gated) {
-            CHK(face_gate_setup(h));
-            if (h->gates.size() >= kGateRing / 2) CHK(face_gates_drain(h));   // (the status ring's reuse)
-            G.gate = h->gate;
-            G.stat = h->gate_stat;
-            G.seq = h->gate_seq;
-        }
+        CHK(face_gate_setup(h));
+        if (h->gates.size() >= kGateRing / 2) CHK(face_gates_drain(h));   // (the status ring's reuse)
+        G.gate = h->gate;
+        G.stat = h->gate_stat;
+        G.seq = h->gate_seq;
         {
             // the state crosses HBM once per call: tnew_nonlin and RHS in, tnew (+ tnew_nonlin) out
             Span sp(h, kid, (dead_last ? 72.0 : 96.0) * (double)L.N + 168.0 * h->U);
@@ -865,27 +883,18 @@ int face_call(pamg_handle *h, int l, bool src_is_T, int sweeps, bool dead_last, 
             HIPCHK(h, launch_face_chain(h->stream, L, h->U, h->cus, h->tov, h->tov_b, h->tovo, L.chain_flags,
                                         L.chain_nb_off, L.chain_nb_list, h->chain_tmo, run, sweeps,
                                         dead_last ? 2 : both ? 3 : 1,
-                                        h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, src_is_T, f0, guard ? 1 : 0, G));
+                                        h->p.solver == 3, l == 1, rdt, h->p.omega, h->slots, src_is_T, f0, 1, G));
         }
         // fail safe: a launch whose workgroups were not all resident (a CU-masked stream, another stream's or
         // process's kernels on the CUs) aborted before touching anything -- the call runs with one launch per
-        // sweep, from the same input and halo snapshot: gated, the stream waits for the launch's report and the
-        // host runs it when it reads the report back (face_gates_drain, at the latest when the API call ends);
-        // PAMG_CHAIN_GATE=0, the host waits for the chain and runs it below
-        if (!guard) return PAMG_OK;
-        if (gated) {
-            h->gate_seq += 1;
-            h->gate_base += 1;
-            HIPCHK(h, hipStreamWaitValue64(h->stream, h->gate, h->gate_base, hipStreamWaitValueGte));
-            h->gates.push_back({G.seq, h->gate_base, l, sweeps, run, dead_last, src_is_T, both, L.T, L.TNN, L.RHS});
-            return PAMG_OK;
-        }
-        if (!h->guard_host) HIPCHK(h, hipHostMalloc((void **)&h->guard_host, sizeof(unsigned)));
-        HIPCHK(h, hipMemcpyAsync(h->guard_host, h->chain_tmo + 3, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
-        CHK(sync_stream(h, h->stream));
-        if (*h->guard_host == 0) return PAMG_OK;
-        HIPCHK(h, hipMemsetAsync(h->chain_tmo + 3, 0, sizeof(unsigned), h->stream));
-        h->timing.seq[PAMG_K_FACE_FALLBACK] += 1;
+        // sweep, from the same input and halo snapshot: the stream waits for the launch's report at its gate and
+        // the host runs the fallback when it reads the report back (face_gates_drain, at the latest when the API
+        // call ends). (Round 5's first form, the host waiting for every launch, cost 2.3 % more; removed.)
+        h->gate_seq += 1;
+        h->gate_base += 1;
+        HIPCHK(h, hipStreamWaitValue64(h->stream, h->gate, h->gate_base, hipStreamWaitValueGte));
+        h->gates.push_back({G.seq, h->gate_base, l, sweeps, run, dead_last, src_is_T, both, L.T, L.TNN, L.RHS});
+        return PAMG_OK;
     }
     if (const int g = face_wave_grid_for(h, l, run)) {   // the call in one wavefront launch
         CHK(tags(&g0, &g1, &tag0));
@@ -1118,11 +1127,9 @@ double vcycle_flops(pamg_handle *h) {
     }
     return fl;
 }
-// PAMG_PIPE_KEEP=<mask> forces stores into every pipelined launch (A/B runs; 7 = all)
-int pipe_keep_env() {
-    static const int k = getenv("PAMG_PIPE_KEEP") ? atoi(getenv("PAMG_PIPE_KEEP")) & PAMG_KEEP_ALL : 0;
-    return k;
-}
+// the stores a pipelined launch makes beyond what the call needs: none (forcing them, the round-2 A/B, moved
+// 120 instead of 72 B per level-1 sub-element)
+constexpr int kPipeKeep = 0;
 
 // the exact local solve of level l (coarse_solver = 1): tnew = tnew_nonlin = A_e^-1 RHS, with
 // A_e^-1 from FINDInv, formed on first use
@@ -1135,7 +1142,7 @@ int direct_solve(pamg_handle *h, int l) {
         HIPCHK(h, launch_block_ops(h->stream, L, h->U, 1 / h->p.dt, L.Ainv, d_err));
         std::vector<int> err(std::max(h->U, 1));
         HIPCHK(h, hipMemcpyAsync(err.data(), d_err, sizeof(int) * h->U, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
+        CHK(sync_stream(h, h->stream));   // (the gates first: hipFree waits for the whole device)
         (void)hipFree(d_err);
         for (int q = 0; q < h->U; ++q)
             if (err[q]) {
@@ -1294,10 +1301,10 @@ int face_pp_emit(pamg_handle *h, int l, const PPPass &q) {
 // such a cycle skips (face_pp_level), and the second call's leg copy tnew_nonlin := tnew (:348) continues from
 // the first call's tnew: one call of (ns - 1) + (ns n_coarse - 1) executed sweeps and a dead last one, whose
 // halo words at the seam are the ones the first call's last executed sweep published -- the words of that tnew,
-// as the second call's refresh would write them. PAMG_FACE_COARSE_MERGE=0: the two calls (A/B).
+// as the second call's refresh would write them. (The two calls run in a call's last cycle, whose residual is
+// state; the merged form is bitwise them: tests/test_face_operator.py, oracle parity.)
 bool face_coarse_merged(pamg_handle *h, bool last) {
-    const char *e = getenv("PAMG_FACE_COARSE_MERGE");   // read per call: tests switch it within a process
-    return !last && h->p.n_smooth >= 1 && h->p.n_coarse >= 1 && !(e && atoi(e) == 0);
+    return !last && h->p.n_smooth >= 1 && h->p.n_coarse >= 1;
 }
 
 // level l's part of cycle c of the fused face cycle (levels l .. L): the coarsest level's calls; a level
@@ -1362,6 +1369,12 @@ int vcycle_face_pp(pamg_handle *h, int n) {
     Level &L2 = h->lv[2];
     const bool rf = !(rr_env && atoi(rr_env) == 0) && h->p.multi_levels >= 2 && L2.RHSN_alt;
     double *const rhs2_home = L2.RHS;
+    // an error return inside the loop leaves level 2's buffers as it found them (the state is invalid after an
+    // error, but RHS and RHSN_alt stay the handle's own two buffers in their roles)
+    struct Home {
+        Level &V; double *home;
+        ~Home() { if (V.RHS != home) std::swap(V.RHS, V.RHSN_alt); }
+    } home_guard{L2, rhs2_home};
     size_t p = 0;
     for (int c = 0; c < n; ++c) {
         h->tnn_level = 1;
@@ -1389,6 +1402,155 @@ int vcycle_face_pp(pamg_handle *h, int n) {
     return face_chain_check(h);
 }
 
+// ---- op = 1 on a partition: the coarsest level agglomerated ----------------------------
+// On a partition the coarsest level's smoother calls -- 62 of the cycle's 74 sweeps at the bench shape, each
+// reading the halo words the neighbours' previous sweep wrote -- would be one launch and one exchange per sweep.
+// The level is small (12.6 MB per field for all of untitled8192 at n_split 5) and, in the reference's cycle,
+// nothing finer reads it back within a call (the prolongator's output is overwritten, SURVEY.md A3 iv); in the
+// corrected cycle only its result is read. So every rank gathers the ranks' blocks of the level's RHS (the
+// restriction of their own level-2 residuals, splitting.F90:10-32) into a replica of the WHOLE level (h->agg,
+// single domain, renumbered rank block by rank block) and runs there the single-domain coarsest calls
+// (transport_tri_semi.F90:331 via :351, :338, :344-359): the persistent chain, its halo words handed over inside
+// the launch. The replicas stay identical on every rank (the same inputs through the same kernels), and a rank
+// copies its own block of the result back into its level L. The replica's tnew carries over from call to call as
+// the level's tnew does (it is never reset, A3 v); it is gathered from the ranks once at the start of each call,
+// so a partition's level L written between calls by anything else (pamg_set_state, per-step calls) is picked up.
+// Bitwise the single domain (tests/test_face_operator.py). PAMG_FACE_AGG=0 at upload keeps the per-sweep form.
+
+// the local-group transport: every peer's block of a 3-plane field pulled from its handle, behind its event
+int gather_local(pamg_handle *h, const double *local, int64_t lpitch, double *rep, int64_t rpitch, int nsub,
+                 hipStream_t st) {
+    Comm &C = *h->comm;
+    LocalGroup &G = *C.local;
+    const int me = h->rank, n = G.n;
+    std::vector<LocalGroup::Post> got(n);
+    auto wait_posts = [&](std::vector<LocalGroup::Post> &box, const char *what) -> int {
+        std::unique_lock<std::mutex> lk(G.mu);
+        for (int peer = 0; peer < n; ++peer) {
+            if (peer == me) continue;
+            const long want = C.seq[peer] + 1;
+            LocalGroup::Post &b = box[(size_t)peer * n + me];
+            if (!G.cv.wait_for(lk, std::chrono::seconds(local_timeout_s()), [&] { return b.seq >= want; })) {
+                h->err = "local coarse gather: rank " + std::to_string(me) + " timed out waiting for rank " +
+                         std::to_string(peer) + "'s " + what;
+                return PAMG_ERR_COMM;
+            }
+            if (b.seq != want) { h->err = "local coarse gather: sequence mismatch"; return PAMG_ERR_COMM; }
+            got[peer] = b;
+        }
+        return PAMG_OK;
+    };
+    HIPCHK(h, hipEventRecord(C.ev_ready, st));
+    {
+        std::lock_guard<std::mutex> lk(G.mu);
+        for (int peer = 0; peer < n; ++peer)
+            if (peer != me) G.ready[(size_t)me * n + peer] = {C.seq[peer] + 1, local, C.ev_ready, lpitch};
+    }
+    G.cv.notify_all();
+    CHK(wait_posts(G.ready, "coarse block"));
+    for (int peer = 0; peer < n; ++peer) {
+        if (peer == me) continue;
+        const size_t cnt = (size_t)(h->agg_off[peer + 1] - h->agg_off[peer]) * nsub;
+        HIPCHK(h, hipStreamWaitEvent(st, got[peer].ev, 0));
+        if (cnt)
+            HIPCHK(h, hipMemcpy2DAsync(rep + (size_t)h->agg_off[peer] * nsub, rpitch * sizeof(double), got[peer].ptr,
+                                       got[peer].pitch * sizeof(double), cnt * sizeof(double), 3,
+                                       hipMemcpyDeviceToDevice, st));
+    }
+    // this rank's reads are issued; its own block may change once every peer's are
+    HIPCHK(h, hipEventRecord(C.ev_done, st));
+    {
+        std::lock_guard<std::mutex> lk(G.mu);
+        for (int peer = 0; peer < n; ++peer)
+            if (peer != me) G.done[(size_t)me * n + peer] = {C.seq[peer] + 1, nullptr, C.ev_done, 0};
+    }
+    G.cv.notify_all();
+    CHK(wait_posts(G.done, "read completion"));
+    for (int peer = 0; peer < n; ++peer) {
+        if (peer == me) continue;
+        HIPCHK(h, hipStreamWaitEvent(st, got[peer].ev, 0));
+        C.seq[peer] += 1;
+    }
+    return PAMG_OK;
+}
+
+// RCCL: one grouped send / recv per peer and plane (an allgatherv of the blocks); a self-peer communicator
+// (pamg_comm_init_self) sends its whole level to itself through RCCL, so the transport runs on one GPU
+int gather_rccl(pamg_handle *h, const double *local, int64_t lpitch, double *rep, int64_t rpitch, int nsub,
+                hipStream_t st) {
+    const bool self_peer = !h->vpart.empty();
+    const size_t mine = (size_t)h->U * nsub;
+    NCCLCHK(h, ncclGroupStart());
+    for (int r = 0; r < h->nranks; ++r) {
+        if (r == h->rank && !self_peer) continue;   // (copied on the device)
+        const size_t cnt = (size_t)(h->agg_off[r + 1] - h->agg_off[r]) * nsub;
+        for (int c = 0; c < 3; ++c) {
+            if (mine) NCCLQ(h, ncclSend(local + c * lpitch, mine, ncclDouble, r, h->comm->nccl, st));
+            if (cnt)
+                NCCLQ(h, ncclRecv(rep + c * rpitch + (size_t)h->agg_off[r] * nsub, cnt, ncclDouble, r, h->comm->nccl, st));
+        }
+    }
+    return nccl_group_end(h);
+}
+
+// level L's field `local` of every rank into the replica's `rep`
+int agg_gather(pamg_handle *h, const double *local, double *rep) {
+    const int L = h->p.multi_levels;
+    const Level &V = h->lv[L], &R = h->agg->lv[L];
+    Span sp(h, PAMG_K_COARSE_GATHER, 24.0 * (double)R.N);   // the whole level arrives (this rank's block by copy)
+    const bool self_peer = !h->vpart.empty();
+    if (!self_peer && h->U)
+        HIPCHK(h, hipMemcpy2DAsync(rep + (size_t)h->agg_off[h->rank] * V.nsub, R.pitch * sizeof(double), local,
+                                   V.pitch * sizeof(double), (size_t)h->U * V.nsub * sizeof(double), 3,
+                                   hipMemcpyDeviceToDevice, h->stream));
+    if (h->comm && h->comm->nccl) return gather_rccl(h, local, V.pitch, rep, R.pitch, V.nsub, h->stream);
+    if (h->comm && h->comm->local) return gather_local(h, local, V.pitch, rep, R.pitch, V.nsub, h->stream);
+    return PAMG_OK;   // a detached partition (timing probes): its own block only
+}
+
+// this rank's block of the replica's level-L fields back into its own level L
+int agg_copy_back(pamg_handle *h, bool res) {
+    const int L = h->p.multi_levels;
+    Level &V = h->lv[L];
+    const Level &R = h->agg->lv[L];
+    if (!h->U) return PAMG_OK;
+    const size_t off = (size_t)h->agg_off[h->vpart.empty() ? h->rank : 0] * V.nsub;
+    for (int f = 0; f < 3; ++f) {
+        if (f == 2 && !res) continue;
+        double *dst = f == 0 ? V.T : f == 1 ? V.TNN : V.RES;
+        const double *src = f == 0 ? R.T : f == 1 ? R.TNN : R.RES;
+        HIPCHK(h, hipMemcpy2DAsync(dst, V.pitch * sizeof(double), src + off, R.pitch * sizeof(double),
+                                   (size_t)h->U * V.nsub * sizeof(double), 3, hipMemcpyDeviceToDevice, h->stream));
+    }
+    return PAMG_OK;
+}
+
+// the reference cycle's coarsest-level work of cycle c (vcycle_face_fused: the restriction-leg call, the
+// residual in the call's last cycle, the coarse solve -- or their merged call) on the replica
+int agg_coarse_cycle(pamg_handle *h, bool first, bool last) {
+    const int L = h->p.multi_levels;
+    pamg_handle *r = h->agg;
+    if (first) CHK(agg_gather(h, h->lv[L].T, r->lv[L].T));
+    CHK(agg_gather(h, h->lv[L].RHS, r->lv[L].RHS));
+    CHK(face_pp_level(r, L, last));
+    return last ? agg_copy_back(h, true) : PAMG_OK;
+}
+
+int smooth_to_tnew(pamg_handle *h, int l, int sweeps);
+
+// the corrected cycle's coarse solve (vcycle_corrected: tnew := 0, n_smooth n_coarse sweeps, tnew := the
+// result) on the replica; its result is read by the interpolation into level L - 1
+int agg_coarse_corrected(pamg_handle *h) {
+    const int L = h->p.multi_levels, ns = h->p.n_smooth;
+    pamg_handle *r = h->agg;
+    Level &C = r->lv[L];
+    CHK(agg_gather(h, h->lv[L].RHS, C.RHS));
+    HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));   // from zero
+    if (ns * h->p.n_coarse > 0 && face_fusable(r, L)) CHK(face_call(r, L, true, ns * h->p.n_coarse, false, false, true));
+    else CHK(smooth_to_tnew(r, L, ns * h->p.n_coarse));
+    return agg_copy_back(h, false);
+}
+
 int vcycle_face_fused(pamg_handle *h, int n) {
     if (h->p.multi_levels >= 2 && h->p.n_smooth >= 2)
         for (int l = 1; l < h->p.multi_levels; ++l)
@@ -1398,6 +1560,7 @@ int vcycle_face_fused(pamg_handle *h, int n) {
     for (int c = 0; c < n; ++c) {
         const bool last = c + 1 == n;
         for (int l = 1; l <= L; ++l) {   // :323-340
+            if (l == L && h->agg) break;   // (the replica runs the coarsest level, below)
             if (l == L && face_coarse_merged(h, last)) break;   // (the call below runs both)
             CHK(face_call(h, l, true, ns, true));
             CHK(restrict_(h, l));
@@ -1408,7 +1571,8 @@ int vcycle_face_fused(pamg_handle *h, int n) {
             Span sp(h, PAMG_K_RESIDUAL, 72.0 * (double)V.N + 168.0 * h->U);   // tnew, RHS in, residual out
             HIPCHK(h, launch_face_residual(h->stream, V, h->tov, false, l == 1, rdt, h->slots));
         }
-        if (face_coarse_merged(h, last)) CHK(face_call(h, L, true, ns + ns * h->p.n_coarse - 1, true));
+        if (h->agg) CHK(agg_coarse_cycle(h, c == 0, last));   // a partition: the agglomerated coarsest level
+        else if (face_coarse_merged(h, last)) CHK(face_call(h, L, true, ns + ns * h->p.n_coarse - 1, true));
         else CHK(face_call(h, L, true, ns * h->p.n_coarse, !last));   // :344-359
         // :363-378; the residual of the restriction leg (:336) is due after the level's call there, and
         // nothing changes level l's tnew, RHS or halo words until this call starts: it computes it
@@ -1448,8 +1612,10 @@ int vcycle_corrected(pamg_handle *h) {
         CHK(restrict_(h, l));
     }
     Level &C = h->lv[L];
-    if (L > 1) HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));   // a coarse level starts from zero
-    if (L == 1) {
+    if (L > 1 && !h->agg) HIPCHK(h, hipMemsetAsync(C.T, 0, 3 * (size_t)C.pitch * sizeof(double), h->stream));   // a coarse level starts from zero
+    if (h->agg) {
+        CHK(agg_coarse_corrected(h));   // a partition: the agglomerated coarsest level
+    } else if (L == 1) {
         CHK(smooth_to_tnew(h, 1, ns));
         CHK(residual_corrected(h, 1));
     } else if (h->p.coarse_solver == 1) {
@@ -1582,12 +1748,11 @@ int vcycle_corrected_face_pp(pamg_handle *h, int n) {
 // per-step sequence above (tests/test_corrected.py). The halo words of the state are the last smoother
 // call's, level 1's post-smoothing call of the last cycle (every coarser level writes a subset of its
 // slots before it): its tnew words are written by the launch, the words constant within a time step by
-// k_overlap_static, the remote ones exchanged after the call (halo_exchange = 0). PAMG_NO_CORR_RESIDENT
-// (A/B) keeps the per-step sequence.
+// k_overlap_static, the remote ones exchanged after the call (halo_exchange = 0). fused = 0 keeps the per-step
+// sequence.
 int call_schedule(pamg_handle *h);
 bool corrected_resident_ok(pamg_handle *h) {
-    static const bool off = getenv("PAMG_NO_CORR_RESIDENT") != nullptr;
-    return !off && h->p.cycle == 1 && h->p.fused != 0 && h->p.op == 0 && h->p.coarse_solver == 0 && h->p.solver != 2 &&
+    return h->p.cycle == 1 && h->p.fused != 0 && h->p.op == 0 && h->p.coarse_solver == 0 && h->p.solver != 2 &&
            h->p.halo_exchange == 0 && h->p.n_smooth > 0 && call_schedule(h) == 3 &&
            vcycle_corrected_supported(h->p.n_split, h->p.multi_levels);
 }
@@ -1615,7 +1780,7 @@ int vcycle_corrected_resident(pamg_handle *h, int n) {
     }
     h->rhsn_valid = false;   // residuals and coarse RHS rewritten (RHSN does not follow them)
     {
-        Span sp(h, PAMG_K_VCYCLE_CORR, vcycle_corr_bytes(h), nullptr, true);
+        Span sp(h, PAMG_K_VCYCLE_CORR, vcycle_corr_bytes(h));
         HIPCHK(h, launch_vcycle_corrected(h->stream, h->lv, L, h->U, h->p.n_split, h->p.n_smooth, h->p.n_coarse,
                                           1 / h->p.dt, h->tov, h->tovo, P1.send_buf(buf), h->lv[2].RHSN, PAMG_KEEP_ALL, n));
     }
@@ -1625,12 +1790,11 @@ int vcycle_corrected_resident(pamg_handle *h, int n) {
 }
 
 // n V-cycles as two fused launches each (pamg_vcycle.hip)
-// pipelined-call schedule (pamg_set_call_schedule; PAMG_CALL_SCHEDULE=<s> overrides for A/B runs)
+// pipelined-call schedule (pamg_set_call_schedule)
 // 0 automatic: the resident form where it applies (two levels or more, the halo words exchanged
 // once per call), else one launch per cycle (one GPU) or two tile streams (a partition)
 int call_schedule(pamg_handle *h) {
-    static const int cs_env = getenv("PAMG_CALL_SCHEDULE") ? atoi(getenv("PAMG_CALL_SCHEDULE")) : -1;
-    const int s = cs_env >= 0 ? cs_env : h->call_schedule;
+    const int s = h->call_schedule;
     if (s) return s;
     if (vcycle_resident_supported(h->p.n_split, h->p.multi_levels)) return 3;
     return h->nranks > 1 ? 2 : 1;
@@ -1708,7 +1872,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
     //
     // pamg_set_call_schedule(h, s): 0 automatic (3 where it applies, else 2 on a partition of
     // a multi-rank run, 1 on one GPU), 1 one launch per cycle, 2 two tile streams, 3 resident
-    // (below); PAMG_CALL_SCHEDULE=<s> overrides for A/B runs. (Round 1 tried a persistent
+    // (below). (Round 1 tried a persistent
     // form of the pipelined launch and dropped it at 128 VGPRs with spills; the resident form
     // fits -- its final-cycle stores are peeled out of the cycle loop and its loop is
     // unswitched by wave role, pamg_vcycle.hip k_vc_res / k_vc_resb.)
@@ -1738,7 +1902,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
         const int kt = rhsf && !dead_after ? PAMG_KEEP_TOLD : 0;
         // inside pamg_run (dead_after) the halo words die unread too -- unless every cycle's are exchanged
         const bool hx = h->p.halo_exchange == 1;
-        const int keep = (dead_after ? pipe_keep_env() | (hx ? PAMG_KEEP_HALO : 0) : PAMG_KEEP_ALL) | kt;
+        const int keep = (dead_after ? kPipeKeep | (hx ? PAMG_KEEP_HALO : 0) : PAMG_KEEP_ALL) | kt;
         if (kt) CHK(join_comm(h));   // the send buffers' told halves are rewritten
         // halo_exchange = 1: every cycle's words are exchanged. Cycles 0 .. n-2 pack the tnew words
         // of their remote entries into level 1's ring (k_vc_res / k_vc_resb with XC) and publish
@@ -1754,8 +1918,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
             CHK(xc_setup(h, n));
             HIPCHK(h, hipMemsetAsync(h->xc_done, 0, (size_t)(n - 1) * sizeof(unsigned), h->stream));
             {
-                Span sp(h, PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, false) + 24.0 * (n - 1) * P1.remote.size(),
-                        nullptr, true);
+                Span sp(h, PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, false) + 24.0 * (n - 1) * P1.remote.size());
                 HIPCHK(h, launch_vcycle_resident_xc(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt,
                                                     h->tov, h->tovo, P1.send_buf(buf), L2.RHSN, keep, n, P1.d_ring,
                                                     3 * (int64_t)P1.remote.size(), h->xc_done, h->xc_sig));
@@ -1774,7 +1937,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
             // rounds run (the exchange reads only their send words and writes only the remote slots of
             // t_overlap / t_overlap_old, which no tile of the launch writes). A call that starts a time step
             // (RHSF) writes the send buffers' told halves itself and exchanges after the launch.
-            const bool xe = !rhsf && !dead_after && steps == 1 && h->comm && !P1.peers.empty() && early_xc_enabled();
+            const bool xe = !rhsf && !dead_after && steps == 1 && h->comm && !P1.peers.empty();
             EarlyXc X{};
             if (xe) {
                 // the counter is never reset (a memset before the launch delays it by a few us): this call's
@@ -1790,8 +1953,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
                 HIPCHK(h, hipEventRecord(h->xe_ev[0], h->stream));
             }
             {
-                Span sp(h, rhsf ? PAMG_K_VCYCLE_RES_RHSF : PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, rhsf), nullptr,
-                        true);
+                Span sp(h, rhsf ? PAMG_K_VCYCLE_RES_RHSF : PAMG_K_VCYCLE_RES, vcycle_res_bytes(h, keep, rhsf));
                 HIPCHK(h, launch_vcycle_resident(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
                                                  h->tovo, P1.send_buf(buf), L2.RHSN, keep, rhsf,
                                                  two ? P1.send_buf(1 - buf) : nullptr, n, steps, xe ? &X : nullptr));
@@ -1845,9 +2007,9 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
         // launches alternate between the halves so that each stream always has the next one queued
         const hipStream_t st[2] = {h->stream, h->stream_c};
         // the first coarse launch's RHS and residual are rewritten by the first pipelined one
-        const int ck = pipe_keep_env() & PAMG_KEEP_COARSE;
+        const int ck = kPipeKeep & PAMG_KEEP_COARSE;
         const int ua[2] = {0, mid}, ub[2] = {mid, h->U};
-        const int kf = dead_after ? pipe_keep_env() : PAMG_KEEP_ALL;   // the call's last level-1 launch
+        const int kf = dead_after ? kPipeKeep : PAMG_KEEP_ALL;   // the call's last level-1 launch
         for (int q = 0; q < 2; ++q) {
             Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h, ck) * (ub[q] - ua[q]) / h->U, st[q]);
             HIPCHK(h, launch_vcycle_coarse(st[q], h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
@@ -1855,7 +2017,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
         }
         for (int c = 0; c < n; ++c) {
             const bool pc = c + 1 < n;
-            const int keep = pc ? pipe_keep_env() | (c + 2 == n && !dead_after ? PAMG_KEEP_COARSE : 0) : kf;
+            const int keep = pc ? kPipeKeep | (c + 2 == n && !dead_after ? PAMG_KEEP_COARSE : 0) : kf;
             for (int q = 0; q < 2; ++q) {
                 const double f = (double)(ub[q] - ua[q]) / h->U;
                 Span sp(h, pc ? PAMG_K_VCYCLE_PIPE : PAMG_K_VCYCLE,
@@ -1881,7 +2043,7 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
     // (into_next below); else its RHS and residual stores are rewritten by the first
     // pipelined launch if n > 1
     if (pipe && n > 0 && !h->coarse_ahead) {
-        const int ck = (n > 1 || dead_after) ? pipe_keep_env() & PAMG_KEEP_COARSE : PAMG_KEEP_ALL;
+        const int ck = (n > 1 || dead_after) ? kPipeKeep & PAMG_KEEP_COARSE : PAMG_KEEP_ALL;
         Span sp(h, PAMG_K_VCYCLE_COARSE, vcycle_coarse_bytes(h, ck));
         HIPCHK(h, launch_vcycle_coarse(h->stream, h->lv, L, h->U, h->p.n_split, ns, h->p.n_coarse, rdt, h->tov,
                                        h->tovo, L2.RHSN, 0, -1, ck));
@@ -1917,10 +2079,10 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
             // them), the coarse levels' RHS and residual unless they reach their final cycle
             // here, the halo words unless every cycle's are exchanged
             const bool dead = pipe && dead_after && h->p.halo_exchange == 0;
-            const int keep = c + 1 == n && into_next ? pipe_keep_env() | (n == 1 ? PAMG_KEEP_COARSE : 0)
-                             : pc ? pipe_keep_env() | (c + 2 == n && !dead ? PAMG_KEEP_COARSE : 0) |
+            const int keep = c + 1 == n && into_next ? kPipeKeep | (n == 1 ? PAMG_KEEP_COARSE : 0)
+                             : pc ? kPipeKeep | (c + 2 == n && !dead ? PAMG_KEEP_COARSE : 0) |
                                         (h->p.halo_exchange == 1 ? PAMG_KEEP_HALO : 0)
-                                  : (dead && c + 1 == n ? pipe_keep_env() : PAMG_KEEP_ALL);
+                                  : (dead && c + 1 == n ? kPipeKeep : PAMG_KEEP_ALL);
             // rhs_first: this launch also starts the time step -- told := tnew and level 1's RHS
             // (k_rhs's work: +48 B stored, 24 B of RHS not read per level-1 sub-element)
             // (+24 B of s' read and 24 B of RHS stored per level-1 sub-element, the RHS read
@@ -1957,6 +2119,85 @@ int vcycle_fused(pamg_handle *h, int n, bool dead_after, int steps = 1) {
     if (conc && n > 0) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_coarse, 0));   // join
     return join_comm(h);
 }
+
+// the replica of the coarsest level for op = 1 on a partition (agg_coarse_cycle); PAMG_FACE_AGG=0 (read here, at
+// upload): none -- the partition then runs its coarsest calls one launch per sweep, exchanging between sweeps
+int agg_create(pamg_handle *h, int U, const double *X, const int *region, const int *neig, const int *fneig,
+               const int *dir) {
+    const char *e = getenv("PAMG_FACE_AGG");
+    const int L = h->p.multi_levels;
+    if (h->coarse_only || h->p.op != 1 || L < 2 || (h->nranks == 1 && h->vpart.empty()) || (e && atoi(e) == 0))
+        return PAMG_OK;
+    // the replica's numbering: rank 0's un_eles (ascending global id), then rank 1's, ... (a self-peer
+    // communicator: one block, the global order)
+    std::vector<int> order;
+    order.reserve(U);
+    h->agg_off.assign(1, 0);
+    if (h->nranks == 1) {
+        for (int g = 0; g < U; ++g) order.push_back(g);
+        h->agg_off.push_back(U);
+    } else {
+        for (int r = 0; r < h->nranks; ++r) {
+            for (int g = 0; g < U; ++g)
+                if (h->owner[g] == r) order.push_back(g);
+            h->agg_off.push_back((int)order.size());
+        }
+    }
+    std::vector<int> pnew(U);
+    for (int i = 0; i < U; ++i) pnew[order[i]] = i;
+    std::vector<double> Xp(6 * (size_t)U);
+    std::vector<int> regp(U), neigp(3 * (size_t)U), fneigp(3 * (size_t)U), dirp(3 * (size_t)U);
+    for (int i = 0; i < U; ++i) {
+        const int g = order[i];
+        for (int c = 0; c < 6; ++c) Xp[6 * (size_t)i + c] = X[6 * (size_t)g + c];
+        regp[i] = region[g];
+        for (int f = 0; f < 3; ++f) {
+            const int nb = neig[3 * (size_t)g + f];
+            neigp[3 * (size_t)i + f] = nb >= 1 ? pnew[nb - 1] + 1 : nb;
+            fneigp[3 * (size_t)i + f] = fneig[3 * (size_t)g + f];
+            dirp[3 * (size_t)i + f] = dir[3 * (size_t)g + f];
+        }
+    }
+    // the replica works on this handle's streams (its chains are ordered with the cycle) and creates none of its
+    // own but the chain gates' fallback stream, on first use: a process then holds the four streams of a
+    // single-domain handle, one per hardware queue (GPU_MAX_HW_QUEUES = 4), so the fallback never waits behind
+    // the gate it opens
+    auto *r = new pamg_handle;
+    r->p = h->p;
+    r->device = h->device;
+    r->stream = h->stream;
+    r->stream_comm = h->stream_comm;
+    r->stream_c = h->stream_c;
+    r->borrowed_stream = true;
+    r->coarse_only = true;
+    r->tparent = h;
+    r->cus = h->cus;
+    const int rc = pamg_upload_mesh(r, U, Xp.data(), regp.data(), neigp.data(), fneigp.data(), dirp.data());
+    if (rc != PAMG_OK) {
+        h->err = "coarse replica: " + r->err;
+        (void)pamg_destroy(r);
+        return rc;
+    }
+    h->agg = r;
+    return PAMG_OK;
+}
+
+// the communicator (blocking: see nccl_settle); a failure binds nothing to the handle
+int nccl_init(pamg_handle *h, ncclComm_t *out, int nranks, ncclUniqueId uid, int rank) {
+    *out = nullptr;
+    ncclComm_t nc = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&nc, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        h->err = "ncclCommInitRank (rank " + std::to_string(rank) + " of " + std::to_string(nranks) + "): " +
+                 ncclGetErrorString(r);
+        if (nc) (void)ncclCommAbort(nc);
+        return PAMG_ERR_COMM;
+    }
+    *out = nc;
+    return PAMG_OK;
+}
+
+void nccl_release(ncclComm_t c) { (void)ncclCommDestroy(c); }
 
 void free_levels(pamg_handle *h) {
     for (int l = 1; l <= kMaxLevels; ++l) {
@@ -2064,18 +2305,21 @@ int pamg_comm_unique_id(char out[128]) {
 int pamg_comm_init(pamg_handle *h, int nranks, int rank, const char id[128], int U, const int *owner) {
     if (!h || nranks < 1 || rank < 0 || rank >= nranks || !owner || U < 1) return PAMG_ERR_ARG;
     if (h->mesh_ready) { h->err = "pamg_comm_init must precede pamg_upload_mesh"; return PAMG_ERR_STATE; }
-    h->nranks = nranks;
-    h->rank = rank;
-    h->owner.assign(owner, owner + U);
+    ncclComm_t nc = nullptr;
     if (nranks > 1 && id) {   // id == NULL: detached partition (pamg_halo_loopback exchanges)
         if (h->comm) { h->err = "communicator already bound"; return PAMG_ERR_STATE; }
         HIPCHK(h, hipSetDevice(h->device));
         ncclUniqueId uid;
         std::memcpy(&uid, id, 128);
-        // bound to the handle only once RCCL has initialised it (a failure leaves no half-bound
-        // communicator behind, so a retry can bind again)
-        ncclComm_t nc = nullptr;
-        NCCLCHK(h, ncclCommInitRank(&nc, nranks, uid, rank));
+        // the communicator, the rank and the owner map are bound to the handle only once RCCL has initialised
+        // it (a failure -- a peer that never joins, nccl_init's bound -- leaves the handle as it was, so a retry
+        // can bind again)
+        CHK(nccl_init(h, &nc, nranks, uid, rank));
+    }
+    h->nranks = nranks;
+    h->rank = rank;
+    h->owner.assign(owner, owner + U);
+    if (nc) {
         h->comm = new Comm;
         h->comm->nccl = nc;
     }
@@ -2092,7 +2336,7 @@ int pamg_comm_init_self(pamg_handle *h, const char id[128], int U, const int *pa
     // the plan and the communicator are bound only once RCCL has initialised it: a failure leaves
     // the handle as it was (no half-bound communicator, no self-peer parts), so a retry can bind
     ncclComm_t nc = nullptr;
-    NCCLCHK(h, ncclCommInitRank(&nc, 1, uid, 0));
+    CHK(nccl_init(h, &nc, 1, uid, 0));
     h->nranks = 1;
     h->rank = 0;
     h->owner.assign(U, 0);
@@ -2161,6 +2405,10 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
     if (!h || U < 1 || !X || !region || !neig || !fneig || !dir) return PAMG_ERR_ARG;
     CHK(settle(h));
     HIPCHK(h, hipSetDevice(h->device));
+    if (h->agg) {
+        (void)pamg_destroy(h->agg);
+        h->agg = nullptr;
+    }
     free_levels(h);
     h->U_global = U;
     h->owned.clear();
@@ -2226,6 +2474,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
             if (v < 0 || v >= (int)pos[l].size() || seen[v]++) { h->err = "storage order is not a permutation"; return PAMG_ERR_STATE; }
     }
     for (int l = 1; l <= Lc; ++l) {
+        if (h->coarse_only && l < Lc) continue;   // a replica of the coarsest level (agg_create)
         Level &L = h->lv[l];
         L.pos = pos[l];
         L.isplit = S - l + 1;
@@ -2235,7 +2484,9 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         L.richardson = h->p.solver == 2;
         L.nsub = 1 << (2 * L.isplit);
         L.N = (int64_t)L.nsub * Ul;
-        L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64) + plane_pad();
+        // (a gap between the planes, so that a sub-element's three are not a power-of-two distance apart, measured
+        // within noise: profiles/r05_e_asm_layouts.txt)
+        L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64);
         double *base = nullptr;
         // level 1: the source term s' (SRC); level 2: RHSN_alt for the concurrent fused cycle
         const size_t planes = (l <= 2) ? 21 : 18;
@@ -2389,7 +2640,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         CHK(dev_alloc(h, &P.d_recv, 6 * P.recv_dst.size()));
     }
     // initial condition (:237-252): tnew = 0, region 4 => 1 on level 1
-    {
+    if (!h->coarse_only) {
         Level &L1 = h->lv[1];
         bool any = false;
         for (int q = 0; q < Ul; ++q) any |= region[h->owned[q]] == 4;
@@ -2408,7 +2659,7 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->mesh_ready = true;
-    return PAMG_OK;
+    return agg_create(h, U, X, region, neig, fneig, dir);
 }
 
 int pamg_owned_count(pamg_handle *h) { return h ? h->U : PAMG_ERR_ARG; }
@@ -2564,7 +2815,7 @@ int vcycle(pamg_handle *h, int n, bool dead_after) {
         if (corrected_resident_ok(h)) return vcycle_corrected_resident(h, n);
         if (face_corrected_pp_ok(h)) return vcycle_corrected_face_pp(h, n);
         for (int c = 0; c < n; ++c) CHK(vcycle_corrected(h));
-        return PAMG_OK;
+        return h->p.op == 1 ? face_chain_check(h) : PAMG_OK;
     }
     if (fused_ok(h)) return vcycle_fused(h, n, dead_after);
     if (face_cycle_fusable(h)) return vcycle_face_fused(h, n);
@@ -2621,7 +2872,7 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
         if (ntime >= 2 && n_multigrid >= 1 && h->p.cycle == 0 && h->p.fused == 3 && h->p.coarse_solver == 0 &&
             h->p.op == 0 && h->p.halo_exchange == 0 && !h->coarse_ahead && call_schedule(h) == 3 && fused_ok(h) &&
             vcycle_resident_run_supported(h->p.n_split, L) && vcycle_rhsf_supported(h->p.n_split) &&
-            !PAMG_RHS_TOLD_HALO && getenv("PAMG_NO_RHS_FUSION") == nullptr && getenv("PAMG_NO_RESIDENT_RUN") == nullptr) {
+            !PAMG_RHS_TOLD_HALO) {
             int rc = begin_timestep(h, true, true, true);
             if (rc == PAMG_OK) rc = vcycle_fused(h, n_multigrid, false, ntime);
             if (rc != PAMG_OK) {
@@ -2643,7 +2894,7 @@ int pamg_run(pamg_handle *h, int ntime, int n_multigrid) {
                                vcycle_rhsf_supported(h->p.n_split) &&
                                (cs == 3 ? vcycle_resident_supported(h->p.n_split, L)
                                         : cs == 1 && (n_multigrid > 1 || t + 1 < ntime)) &&
-                               !PAMG_RHS_TOLD_HALO && getenv("PAMG_NO_RHS_FUSION") == nullptr;
+                               !PAMG_RHS_TOLD_HALO;
         int rc = begin_timestep(h, n_multigrid > 0 && h->p.cycle == 0, fused_next, defer_rhs);
         if (rc == PAMG_OK) rc = vcycle(h, n_multigrid, t + 1 < ntime);   // a step's leftovers die in the next one
         if (rc != PAMG_OK) {
@@ -2787,6 +3038,10 @@ int pamg_destroy(pamg_handle *h) {
     if (!h) return PAMG_OK;
     (void)hipSetDevice(h->device);
     (void)face_gates_drain(h);
+    if (h->agg) {
+        (void)pamg_destroy(h->agg);
+        h->agg = nullptr;
+    }
     (void)hipStreamSynchronize(h->stream);
     if (h->stream_fb) (void)hipStreamSynchronize(h->stream_fb);
     (void)hipStreamSynchronize(h->stream_comm);
@@ -2794,7 +3049,6 @@ int pamg_destroy(pamg_handle *h) {
     free_levels(h);
     dev_free(h->scratch);
     dev_free(h->chain_tmo);
-    if (h->guard_host) (void)hipHostFree(h->guard_host);
     if (h->gate) (void)hipFree(h->gate);
     if (h->gate_stat) (void)hipHostFree(h->gate_stat);
     if (h->stream_fb) (void)hipStreamDestroy(h->stream_fb);
@@ -2805,8 +3059,12 @@ int pamg_destroy(pamg_handle *h) {
     if (h->xc_sig) (void)hipFree(h->xc_sig);
     for (auto e : h->timing.pool) (void)hipEventDestroy(e);
     for (auto &r : h->timing.pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    if (h->borrowed_stream) {   // a coarsest-level replica: the streams are its parent's
+        delete h;
+        return PAMG_OK;
+    }
     if (h->comm) {
-        if (h->comm->nccl) ncclCommDestroy(h->comm->nccl);
+        if (h->comm->nccl) nccl_release(h->comm->nccl);
         if (h->comm->ev_ready) (void)hipEventDestroy(h->comm->ev_ready);
         if (h->comm->ev_done) (void)hipEventDestroy(h->comm->ev_done);
         if (LocalGroup *G = h->comm->local) {
@@ -2825,7 +3083,7 @@ int pamg_destroy(pamg_handle *h) {
         if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(h->stream_comm);
     if (h->stream_c) (void)hipStreamDestroy(h->stream_c);
-    (void)hipStreamDestroy(h->stream);
+    if (!h->borrowed_stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return PAMG_OK;
 }

@@ -606,18 +606,6 @@ __global__ __launch_bounds__(NT, (RB && TS <= 1024) ? PAMG_FACE_WAVES : 1) void 
 #ifndef PAMG_FACE_PP_WAVES256_PLAIN
 #define PAMG_FACE_PP_WAVES256_PLAIN 4
 #endif
-#ifndef PAMG_FACE_PP_BLDS
-#define PAMG_FACE_PP_BLDS 1
-#endif
-#ifndef PAMG_FACE_PP_SNAP1
-#define PAMG_FACE_PP_SNAP1 1
-#endif
-#ifndef PAMG_FACE_PP_GHOST_EARLY
-#define PAMG_FACE_PP_GHOST_EARLY 1
-#endif
-#ifndef PAMG_FACE_PP_GLDS
-#define PAMG_FACE_PP_GLDS 1
-#endif
 // NT: red-black passes with fewer threads than up sub-elements run a second up item on some threads. For
 // the 256-sub-element un_ele 192 threads (136 ups, one each) measured faster than 128 (0.71 vs 0.73 ms of
 // coarse launches per cycle); for the 1,024 one 576 threads (528 ups) measured slower than 512 (level-1
@@ -651,25 +639,18 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
     constexpr int NUP = M * (M + 1) / 2, KU = RB ? (NUP + NT - 1) / NT : PER, KD = RB ? (TS - NUP + NT - 1) / NT : 0;
     static_assert((RB || (TS % NT == 0 && PER % 2 == 0)) && M * M == TS && 3 * M <= NT && TS <= 1024,
                   "whole un_ele tiles of <= 1,024; Jacobi: adjacent pairs per thread");
-    // one LDS array: the iterate, the RHS, the halo snapshot of each sweep, omega / D
-    // PAMG_FACE_PP_BLDS (A/B): 1 the RHS staged in LDS beside the iterate; 0 each item's RHS in registers,
-    // loaded from memory at its position (less LDS: more workgroups per CU)
-    constexpr bool BL = PAMG_FACE_PP_BLDS != 0;
-    // ONE snapshot image (PAMG_FACE_PP_SNAP1, default): the second sweep's snapshot -- the ghost updates -- stays in the
-    // registers of the threads that compute it and replaces the first sweep's once that sweep's last reader has
-    // passed: the up pass (a down sub-element never reads the snapshot, words_up) or Jacobi's read phase. 53,952 ->
-    // 51,648 B of LDS: three workgroups per CU instead of two (phase stamps, profiles/r05_n_pp_stamps.txt: 512 of
-    // the 768 slots were ever resident)
-    constexpr bool SNAP1 = PAMG_FACE_PP_SNAP1 != 0 && K == 2;
-    // PAMG_FACE_PP_GHOST_EARLY (a build macro, A/B): the ghost update's operands in this tile gathered from memory
-    // like the others, and the update run before the tile's barrier (see ghost below)
-    constexpr bool GEARLY = PAMG_FACE_PP_GHOST_EARLY != 0 && K == 2;
-    constexpr int OX = 0, OB = 3 * TS, OH = (BL ? 6 : 3) * TS, OW = OH + (SNAP1 ? 1 : K) * NH;
+    // one LDS array: the iterate, the RHS, ONE halo snapshot image, omega / D. The second sweep's snapshot -- the
+    // ghost updates -- stays in the registers of the threads that compute it and replaces the first sweep's once
+    // that sweep's last reader has passed: the up pass (a down sub-element never reads the snapshot, words_up) or
+    // Jacobi's read phase. 53,952 -> 51,648 B of LDS: three workgroups per CU instead of two (phase stamps,
+    // profiles/r05_n_pp_stamps.txt: 512 of the 768 slots were ever resident). (Measured, not kept: the RHS in
+    // registers instead of LDS; the ghost update's operands from LDS after the tile's barrier.)
+    constexpr int OX = 0, OB = 3 * TS, OH = 6 * TS, OW = OH + NH;
     __shared__ double LDSM[OW + 24];
     double (*X)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OX);
     double (*B)[TS] = reinterpret_cast<double (*)[TS]>(LDSM + OB);
     double *WD = LDSM + OW;
-    auto HI = [&](int snap) { return LDSM + OH + (SNAP1 ? 0 : snap) * NH; };
+    double *const HS = LDSM + OH;   // the snapshot image
     const int t = threadIdx.x;
     // (Measured, not kept: starting the first round's k-th workgroup of a CU k x 4 / 8 / 12 us late, so that the
     // co-resident workgroups' load, sweep and store phases fall apart -- the level-1 passes 0.74 -> 0.75 / 0.76 /
@@ -734,7 +715,7 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
             for (int fi = 0; fi < 3; ++fi) {
                 if (yy[fi] >= 0) {
                     ldv(yy[fi], yv[fi]);
-                } else if (GEARLY && yy[fi] > -(1 + TS)) {
+                } else if (yy[fi] > -(1 + TS)) {
                     ldv(s0 - 1 - yy[fi], yv[fi]);   // this tile's own start value, as its bulk load forms it
                 } else {
 #pragma unroll
@@ -761,19 +742,13 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
             inb[k] = fnb[ij[k]];
         }
     }
-    double ib[KU + KD][3];   // the items' RHS (BL = 0)
-    if constexpr (!BL)
-#pragma unroll
-        for (int k = 0; k < KU + KD; ++k)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) ib[k][c] = RHS[c * pitch + s0 + (ij[k] < 0 ? 0 : ij[k])];
     (void)nup;
-    // PAMG_FACE_PP_GLDS: unless the start iterate is stored (out_pre), the RHS -- and the start iterate when it is read
+    // unless the start iterate is stored (out_pre), the RHS -- and the start iterate when it is read
     // (not a start from zero) -- go to LDS by LDS-DMA: a wave's 64 pairs of a plane are one 1 KiB global_load_lds_dwordx4
     // into X / B (lane-linear), no VGPR round trip; in the folded instance an interpolation is then added to X in place
     // by the pair's own thread (after its wave's wait: its lane wrote that pair), v + a as in the register path; the
     // __syncthreads below waits for the rest
-    const bool gr = PAMG_FACE_PP_GLDS && BL && !out_pre, ga = gr && (!FOLD || A);
+    const bool gr = !out_pre, ga = gr && (!FOLD || A);
     if (gr) {
         constexpr int aux = (PAMG_NT & 1) ? 2 : 0;
         const int lane = t & 63;
@@ -797,13 +772,11 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const double2 v = ld2(A + c * pitch + s0 + j);
-                const double2 r = BL ? ld2(RHS + c * pitch + s0 + j) : make_double2(0.0, 0.0);
+                const double2 r = ld2(RHS + c * pitch + s0 + j);
                 X[c][j] = v.x;
                 X[c][j + 1] = v.y;
-                if (BL) {
-                    B[c][j] = r.x;
-                    B[c][j + 1] = r.y;
-                }
+                B[c][j] = r.x;
+                B[c][j + 1] = r.y;
                 if (out_pre) st2(out_pre + c * pitch + s0 + j, v);
             }
         }
@@ -826,7 +799,7 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
                 if (Tc) v = make_double2(v.x + a0[c], v.y + a1[c]);
                 X[c][j] = v.x;
                 X[c][j + 1] = v.y;
-                if (BL && !gr) {
+                if (!gr) {
                     const double2 r = ld2(RHS + c * pitch + s0 + j);
                     B[c][j] = r.x;
                     B[c][j + 1] = r.y;
@@ -840,7 +813,7 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
     if (gon)
 #pragma unroll
         for (int kk = 0; kk < 3; ++kk)
-            HI(0)[hq + kk] = ge.x >= 0 ? xe[kk] : ge.x == -1 ? bcpair(hface[3 * u + fu - 1].z + spu - 1, fu, kk) : 0.0;
+            HS[hq + kk] = ge.x >= 0 ? xe[kk] : ge.x == -1 ? bcpair(hface[3 * u + fu - 1].z + spu - 1, fu, kk) : 0.0;
     // the neighbour's operator record for the ghost update (scalar loads, in flight across the barrier)
     FaceRec Rv;
     const double *wdv = nullptr;
@@ -849,21 +822,14 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
         load_face_rec(stc, fface, fsx, v, Rv);
         wdv = fface + v * kFaceStride + kFaceWD + 3 * face_pattern(nbe);
     }
-    double hn[3] = {0.0, 0.0, 0.0};   // SNAP1: this thread's slot of the second sweep's snapshot
+    double hn[3] = {0.0, 0.0, 0.0};   // this thread's slot of the second sweep's snapshot
     // the neighbour's boundary sub-element e after the first sweep (an up one: its sweep reads its down
     // neighbours, unchanged since the previous sweep, and the snapshot across its faces): the second
-    // sweep's snapshot -- face_core on v's record and the values gathered above. GEARLY: every operand came from
+    // sweep's snapshot -- face_core on v's record and the values gathered above. Every operand came from
     // memory, so the update runs as soon as they arrive, before the tile's barrier (no LDS read, no second barrier)
     auto ghost = [&]() {
         if (gon) {
             if (ge.x >= 0) {
-                const int yy[3] = {ge.y, ge.z, ge.w};
-                if (!GEARLY)
-#pragma unroll
-                    for (int fi = 0; fi < 3; ++fi)
-                        if (yy[fi] < 0 && yy[fi] > -(1 + TS))
-#pragma unroll
-                            for (int c = 0; c < 3; ++c) yv[fi][c] = X[c][-1 - yy[fi]];
                 double r[3];
                 // (the component of a halo word is a run-time selector: picked by selects, so that yv stays in
                 // registers)
@@ -871,42 +837,33 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
                                       [&](int fi, int c) { return c == 0 ? yv[fi][0] : c == 1 ? yv[fi][1] : yv[fi][2]; },
                                       [&](int q) { return wdv[q]; }, level1, rdt, r);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    if (SNAP1) hn[c] = r[c];
-                    else HI(1)[hq + c] = r[c];
-                }
-            } else if (!SNAP1) {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) HI(1)[hq + c] = HI(0)[hq + c];   // boundary words: constant
+                for (int c = 0; c < 3; ++c) hn[c] = r[c];
             }
         }
     };
-    if constexpr (K == 2 && GEARLY) ghost();
+    if constexpr (K == 2) ghost();
     __syncthreads();
     pp_stamp(1);
-    if constexpr (K == 2 && !GEARLY) {
-        ghost();
-        __syncthreads();   // the ghost updates read the start iterate (X) before the sweeps rewrite it
-    }
     if constexpr (K == 2) pp_stamp(2);
-    // SNAP1: the second sweep's snapshot into the image, after the first sweep's last read of it (boundary words: constant)
+    // the second sweep's snapshot into the image, after the first sweep's last read of it (boundary words: constant)
     auto snap_next = [&]() {
-        if (SNAP1 && gon && ge.x >= 0)
+        if (K == 2 && gon && ge.x >= 0)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) HI(0)[hq + c] = hn[c];
+            for (int c = 0; c < 3; ++c) HS[hq + c] = hn[c];
     };
     auto xin = [&](int c, int q) { return X[c][q]; };
     // one item k: face_apply<MODE> of position ij[k] from the tile, the RHS and snapshot snap
     auto item = [&](auto mc, int k, int snap, double r[3]) {
         constexpr int MODE = decltype(mc)::value;
         const int j = ij[k];
-        const double *H = HI(snap);
+        const double *H = HS;
+        (void)snap;
         auto hv = [&](int64_t, int mf, int sp, int kk) { return H[((mf - 1) * M + sp - 1) * 3 + kk]; };
         double x[3], bb[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             x[c] = X[c][j];
-            bb[c] = BL ? B[c][j] : ib[k][c];
+            bb[c] = B[c][j];
         }
         const int wb = 3 * face_pattern(inb[k]);
         face_apply<MODE>(R, xin, x, bb, inb[k], u, hv, [&](int i) { return MODE == 3 ? 0.0 : WD[wb + i]; }, level1, rdt, r);
@@ -2219,11 +2176,9 @@ hipError_t launch_face_sweep_fused(hipStream_t s, const Level &L, const double *
 // chain exits cleanly). So the grid is checked against the same occupancy bound the cooperative launch
 // checks (workgroups per CU x CUs) and launched as a plain kernel: on the stream's turn every workgroup
 // of such a grid is dispatched at once, and every in-kernel wait is bounded (the give-up word tmo), so a
-// grid that did not become resident ends in PAMG_ERR_HIP, never in a hang. PAMG_CHAIN_COOP=1 restores
-// the cooperative launch (A/B).
+// grid that did not become resident ends in PAMG_ERR_HIP, never in a hang (round 5: the arrival guard
+// makes such a grid leave without touching anything, and the host runs the call's fallback).
 static hipError_t launch_coresident(const void *f, int grid, int nt, void **args, hipStream_t s) {
-    static const bool coop = getenv("PAMG_CHAIN_COOP") && atoi(getenv("PAMG_CHAIN_COOP")) != 0;
-    if (coop) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(nt), args, 0, s);
     static std::mutex mu;
     static std::map<std::pair<const void *, int>, int> cap;   // co-resident workgroups per (kernel, block)
     int n = 0;
@@ -2293,9 +2248,7 @@ hipError_t launch_face_pp(hipStream_t s, const Level &L, int K, const double *in
 #define PAMG_FPPK(TS, NT)                                          \
     if (rb) { if (K == 2) PAMG_FPP(TS, NT, true, 2); else PAMG_FPP(TS, NT, true, 1); } \
     else { if (K == 2) PAMG_FPP(TS, NT, false, 2); else PAMG_FPP(TS, NT, false, 1); }
-    // PAMG_FACE_PP_NT=512 (A/B): the red-black 256 instance at 128 threads (k_face_pp's NT note)
-    static const bool nt512 = getenv("PAMG_FACE_PP_NT") && atoi(getenv("PAMG_FACE_PP_NT")) == 512;
-    if (L.nsub == 256 && rb && !nt512) {   // 136 ups: 192 threads, one each
+    if (L.nsub == 256 && rb) {   // 136 ups: 192 threads, one each
         if (K == 2) PAMG_FPP(256, 192, true, 2); else PAMG_FPP(256, 192, true, 1);
     } else if (L.nsub == 1024) { PAMG_FPPK(1024, 512) }
     else if (L.nsub == 256) { PAMG_FPPK(256, 128) }
@@ -2355,8 +2308,9 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     const int4 *fnb = L.fnb;
     const int *fsx = L.fsx;
     int64_t pitch = L.pitch, N = L.N;
-    // PAMG_CHAIN_STAMPS=<file>: append every launch's per-sweep phase stamps of workgroups 0..7
-    static const char *stamp_path = getenv("PAMG_CHAIN_STAMPS");
+    // PAMG_CHAIN_STAMPS=<file> (a PAMG_STAMPS=1 diagnostics build): append every launch's per-sweep phase stamps
+    // of workgroups 0..7
+    static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_CHAIN_STAMPS") : nullptr;
     long long *stamps = nullptr;
     // the per-wave chain stamps every wave of workgroups 0..7 (kPWStamps a sweep), the workgroup chain
     // thread 0 of each (4 a sweep); the header's sign tells them apart
@@ -2371,10 +2325,10 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     const int *cpos = L.cpos;
     int nup = L.nup;
     const double *SRC = from_T ? L.T : L.TNN;
-    // PAMG_CHAIN_EARLY (A/B): 0 publish after the down pass, 1 the words after the up pass, 2 words and
-    // flag, 3 (default) as 2 with the up pass split around the wait (k_face_chain)
-    static const int early_env = [] { const char *e = getenv("PAMG_CHAIN_EARLY"); return e ? atoi(e) : 3; }();
-    int nui = L.nui, early = L.words_up ? early_env : 0;
+    // the publish point (k_face_chain): 3 the words and the flag right after the up pass, which is split around
+    // the wait; 2 the same without the split; 0 after the down pass (a level whose words are not all on up
+    // sub-elements). Measured: 0 -> 2 -> 3, 10.4 -> 9.1 -> 8.7 us per sweep (profiles/r03_n_face_chain_early.txt)
+    int nui = L.nui, early = L.words_up ? 3 : 0;
     // the split up pass needs each half's items in one item per thread
     if (early == 3 && !(nui > 0 && (int64_t)k * nui <= kChainNT && (int64_t)k * (L.nup - nui) <= kChainNT)) early = 2;
     // PAMG_CHAIN_SNAP16=0: the snapshot's 8-byte loads, the form a snapshot buffer beyond a buffer
@@ -2400,13 +2354,10 @@ hipError_t launch_face_chain(hipStream_t s, const Level &L, int U, int cus, doub
     if (!(pw_env && atoi(pw_env) == 0) && rb && lrec && early == 3 && uni && L.nsub <= 64 &&
         qpw * std::max(nui, std::max(L.nup - nui, L.ndn)) <= 64)
         f = (const void *)k_face_chain_pw;
-    // PAMG_CHAIN_WGFLAG (the per-wave chain's flags, read per launch): 0 one flag per wave, 1 one per workgroup
-    // stored by its last wave to publish, 2 (default) as 1 with one polling wave per workgroup
-    // (profiles/r05_y_chain_wgflag.txt, r05_z_chain_leader_poll.txt)
-    const char *wgf_env = getenv("PAMG_CHAIN_WGFLAG");
-    const int wgf = wgf_env ? atoi(wgf_env) : 2;
-    if (f == (const void *)k_face_chain_pw && wgf >= 1) early |= 32;
-    if (f == (const void *)k_face_chain_pw && wgf >= 2) early |= 64;
+    // the per-wave chain's flags: one per workgroup, stored by its last wave to publish, and one polling wave per
+    // workgroup (bits 32 and 64; one flag per wave measured slower: profiles/r05_y_chain_wgflag.txt,
+    // r05_z_chain_leader_poll.txt)
+    if (f == (const void *)k_face_chain_pw) early |= 32 | 64;
     hipError_t e = launch_coresident(f, grid, kChainNT, args, s);
     if (stamp_path) {
         std::vector<long long> h(nst);
@@ -2469,7 +2420,7 @@ hipError_t launch_face_wave(hipStream_t s, const Level &L, int U, int grid, doub
     hipError_t e = hipMemsetAsync(flags, 0, sizeof(unsigned) * ((size_t)U + 1), s);
     if (e != hipSuccess) return e;
     // PAMG_WAVE_STAMPS=<file>: append every launch's per-ticket phase stamps of workgroups 0..7
-    static const char *stamp_path = getenv("PAMG_WAVE_STAMPS");
+    static const char *stamp_path = PAMG_STAMPS ? getenv("PAMG_WAVE_STAMPS") : nullptr;   // (diagnostics build)
     long long *stamps = nullptr;
     const size_t nst = (size_t)8 * kWaveStampT * kWaveStampW;
     if (stamp_path) {

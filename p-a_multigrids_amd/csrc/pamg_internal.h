@@ -218,7 +218,6 @@ struct pamg_handle {
     std::vector<int> neig_local;
     unsigned *chain_tmo = nullptr;   // give-up word of the face chain's / wavefront's bounded spins
                                      // ([1..2] the chain's co-residency guard, [3] its aborts)
-    unsigned *guard_host = nullptr;  // pinned: the chain's abort count, read after each guarded launch
     bool chain_pending = false;      // a chain or wavefront launch ran since face_chain_check last read it
     // the guarded chain launches' gates (face_call, PAMG_CHAIN_GATE): the stream waits on `gate` (signal
     // memory) after each launch for the count the launch adds when it ran; an aborted one leaves the stream
@@ -259,6 +258,15 @@ struct pamg_handle {
     hipEvent_t xe_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool xe_ev_valid = false;
     int cus = 0;                     // compute units of the device
+    // op = 1 on a partition: the coarsest level agglomerated (pamg_api.cpp agg_*). `agg` is a
+    // replica handle holding only level L of the WHOLE mesh, un_eles renumbered so that every rank's are one
+    // block (agg_off[r] .. agg_off[r + 1]); it shares this handle's stream. Each cycle gathers the ranks' level-L
+    // RHS into it and every rank runs the single-domain coarsest calls (the persistent chain) on its own copy.
+    pamg_handle *agg = nullptr;
+    std::vector<int> agg_off;
+    bool coarse_only = false;        // this handle is such a replica: levels below L are not allocated
+    bool borrowed_stream = false;    // `stream` belongs to another handle (the replica's parent)
+    pamg_handle *tparent = nullptr;  // the replica's timing spans and fallback counts go to its parent's Timing
 };
 
 // ---- setup (pamg_setup.cpp) ----
@@ -285,14 +293,6 @@ int build_face(pamg_handle *h, int l, const double *Xg, const int *neig, const i
 
 // ---- kernels (pamg_kernels.hip) ----
 namespace pamg {
-// the timing events of the next resident launch on this host thread (pamg_api.cpp Span, in-packet form): a
-// launch that finds them set launches with hipExtLaunchKernel, whose dispatch packet records them around the
-// kernel itself -- no marker packets between back-to-back work (pamg_vcycle.hip)
-struct LaunchEvents {
-    hipEvent_t a = nullptr, b = nullptr;
-    bool used = false;
-};
-LaunchEvents &launch_events();
 hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int sweeps, int solver,
                          double rdt, double omega, double *tov, double *tovo);
 hipError_t launch_residual(hipStream_t s, const Level &L, double rdt, bool neg = false);

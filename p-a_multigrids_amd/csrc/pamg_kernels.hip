@@ -456,7 +456,7 @@ __global__ __launch_bounds__(kBlock) void k_to_aos(const double *__restrict__ so
 // (3 planes). Traffic per sub-element: x 24 + b 24 + out 24 + A 72 + w 24 = 168 B
 // (SURVEY.md 8d). The sweep is the contracted arithmetic of arith = 1 (one fma chain
 // per row, pamg_device.h StcF): bitwise the oracle's orc_sweep_once(arith = 1).
-// Layout of the assembled blocks (PAMG_ASM_LAYOUT, A/B runs; asm_layout below):
+// Layout of the assembled blocks (round 5's A/B, kAsmLayout below):
 //   0  twelve SoA planes (blk[q pitch + s]): 18 load streams + 3 store streams a launch, the planes N
 //      doubles (64 MiB at n_split = 5) apart -- 0.63-0.69 of 8 TB/s across boxes (round 4);
 //   1  tiled: per tile of kAsmTile = 128 sub-elements the twelve planes of the tile, one after the other
@@ -773,8 +773,10 @@ hipError_t launch_smooth(hipStream_t s, const Level &L, const double *src, int s
     if (npairs == 0 || sweeps <= 0) return hipSuccess;
     const HaloPlan &P = L.halo;
     HaloArgs H{P.d_hsub, P.d_hface, P.d_bcv, P.d_told_halo, tov, tovo, P.d_send, 1 << L.isplit};
-    static const bool diag_nohalo = getenv("PAMG_DIAG_NOHALO") != nullptr;       // diagnostics only:
-    static const bool diag_nouniform = getenv("PAMG_DIAG_NOUNIFORM") != nullptr;  // A/B of the fused forms
+    // diagnostics build only (make PAMG_STAMPS=1): the halo words not written (wrong results) or the non-uniform
+    // instance, for A/B timing of the fused forms
+    static const bool diag_nohalo = PAMG_STAMPS && getenv("PAMG_DIAG_NOHALO") != nullptr;
+    static const bool diag_nouniform = PAMG_STAMPS && getenv("PAMG_DIAG_NOUNIFORM") != nullptr;
     if (diag_nohalo) H.hsub = nullptr;
     const int lg = log2i(L.nsub);
     const dim3 g(grid_for(npairs)), b(kBlock);
@@ -956,12 +958,8 @@ hipError_t launch_to_aos(hipStream_t s, const Level &L, const double *soa, doubl
     return hipGetLastError();
 }
 
-// PAMG_ASM_LAYOUT=<layout><K> (A/B runs; read once): the layout of the assembled blocks and, tiled, the
-// tiles per wave
-int asm_layout() {
-    static const int v = getenv("PAMG_ASM_LAYOUT") ? atoi(getenv("PAMG_ASM_LAYOUT")) : 41;
-    return v;
-}
+// the assembled blocks are tiled (layout 1 of the note above k_build_blocks), swept by k_sweep_assembled<4, 1>
+constexpr int kAsmLayout = 1;
 
 size_t asm_blocks_doubles(const Level &L) {
     return 12 * (size_t)((L.pitch + kAsmTile - 1) / kAsmTile * kAsmTile);
@@ -970,7 +968,7 @@ size_t asm_blocks_doubles(const Level &L) {
 hipError_t launch_build_blocks(hipStream_t s, const Level &L, double rdt) {
     (void)rdt;   // the blocks are the records' kStcA words, assembled with rdt on the host
     hipLaunchKernelGGL(k_build_blocks, dim3(grid_for(L.N)), dim3(kBlock), 0, s, L.stc, L.blocks, L.pitch, L.N,
-                       log2i(L.nsub), asm_layout() / 10);
+                       log2i(L.nsub), kAsmLayout);
     return hipGetLastError();
 }
 
@@ -978,36 +976,11 @@ hipError_t launch_sweep_assembled(hipStream_t s, const Level &L, double *out, do
     (void)rdt;
     if (L.N % 2) return hipErrorInvalidValue;
     const int64_t npairs = L.N / 2;
-    const int v = asm_layout();
-    if (v / 10 == 0) {
-        hipLaunchKernelGGL((k_sweep_assembled<0, 1>), dim3(grid_for(npairs)), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks,
-                           out, L.pitch, npairs);
-        return hipGetLastError();
-    }
-    // tiled: a wave per K tiles of 128 sub-elements
-    const int K = v % 10;
-    const int64_t ntiles = (L.N + kAsmTile - 1) / kAsmTile, waves = (ntiles + K - 1) / K;
-    const unsigned grid = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
-    if (v / 10 == 4) {   // tiled, every stream through LDS-DMA (A/B: PAMG_ASM_LAYOUT=41)
-        const unsigned g4 = (unsigned)((ntiles + kBlock / 64 - 1) / (kBlock / 64));
-        hipLaunchKernelGGL((k_sweep_assembled<4, 1>), dim3(g4), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out, L.pitch, npairs);
-        return hipGetLastError();
-    }
-    if (v / 10 == 3) {   // tiled, the blocks through LDS-DMA (A/B: PAMG_ASM_LAYOUT=31 / 32)
-        if (K == 1) hipLaunchKernelGGL((k_sweep_assembled<3, 1>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out, L.pitch, npairs);
-        else if (K == 2) hipLaunchKernelGGL((k_sweep_assembled<3, 2>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out, L.pitch, npairs);
-        else return hipErrorInvalidValue;
-        return hipGetLastError();
-    }
-    switch (K) {
-        case 1: hipLaunchKernelGGL((k_sweep_assembled<1, 1>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
-                                   L.pitch, npairs); break;
-        case 2: hipLaunchKernelGGL((k_sweep_assembled<1, 2>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
-                                   L.pitch, npairs); break;
-        case 4: hipLaunchKernelGGL((k_sweep_assembled<1, 4>), dim3(grid), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out,
-                                   L.pitch, npairs); break;
-        default: return hipErrorInvalidValue;
-    }
+    // tiled, every stream of a wave's tile of 128 sub-elements through LDS-DMA (the other layouts and tilings of
+    // the note above k_build_blocks measured slower and are removed)
+    const int64_t ntiles = (L.N + kAsmTile - 1) / kAsmTile;
+    const unsigned g4 = (unsigned)((ntiles + kBlock / 64 - 1) / (kBlock / 64));
+    hipLaunchKernelGGL((k_sweep_assembled<4, 1>), dim3(g4), dim3(kBlock), 0, s, L.TNN, L.RHS, L.blocks, out, L.pitch, npairs);
     return hipGetLastError();
 }
 

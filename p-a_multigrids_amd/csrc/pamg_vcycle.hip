@@ -47,11 +47,6 @@ PAMG_VC_DECL(1) PAMG_VC_DECL(2) PAMG_VC_DECL(3) PAMG_VC_DECL(4) PAMG_VC_DECL(5) 
 PAMG_VC_DECL(8)
 #undef PAMG_VC_DECL
 
-LaunchEvents &launch_events() {
-    thread_local LaunchEvents e;
-    return e;
-}
-
 namespace {
 
 hipError_t launch_part(hipStream_t s, const Level *lv, int L, int U, int n_split, int n_smooth, int n_coarse,

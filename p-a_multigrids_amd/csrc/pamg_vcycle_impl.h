@@ -1926,20 +1926,11 @@ __global__ __launch_bounds__(512, PAMG_CORR_WAVES) void k_vc_corr(VArgs A, const
     else role(std::integral_constant<int, 0>{});
 }
 
-// a resident launch (one kernel per pamg_vcycle call): with the caller's timing events set (launch_events),
-// through hipExtLaunchKernel -- the dispatch packet records them around the kernel
+// a resident launch (one kernel per pamg_vcycle call)
 template <class K>
 void launch_resident_kernel(K k, unsigned grid, unsigned block, hipStream_t s, const VArgs &A) {
-    LaunchEvents &E = launch_events();
-    if (E.a && E.b) {
-        hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, E.a, E.b, 0u, A, A.lv[0].stc, A.lv[1].stc,
-                              A.lv[2].stc, A.lv[3].stc, A.lv[4].stc);
-        E.used = true;
-        E.a = E.b = nullptr;
-    } else {
-        hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, A, A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc,
-                           A.lv[4].stc);
-    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, A, A.lv[0].stc, A.lv[1].stc, A.lv[2].stc, A.lv[3].stc,
+                       A.lv[4].stc);
 }
 
 // part: 0 level 1 (k_vc_fine), 1 coarse levels (k_vc_coarse), 2 level 1 + next cycle's coarse levels
@@ -2013,7 +2004,7 @@ inline bool no_scratch(const void *kernel) {
 
 // the 64-VGPR instance only where it saves a round: more workgroups than 3 per CU, at most 4
 // (at n_split = 3 the launch fits one round either way and the bounded instance is 50 %
-// slower; PAMG_W8_MAX_GRID=<n> overrides the upper bound for A/B runs)
+// slower)
 template <int S, int L, class ST>
 hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     static const long n_cu = [] {
@@ -2026,9 +2017,8 @@ hipError_t launch_slt(hipStream_t s, const VArgs &A, unsigned grid, int part) {
     // wave at any size: 0.2678 -> 0.2560 ms per full-mesh cycle)
     // (the pipelined launch without its dead-until-final stores, kKeep*, moves 72 instead of
     // 120 B per level-1 sub-element and gains from it too: 0.1377 -> 0.1328 ms per full-mesh
-    // cycle, scripts/ab_probe.py with PAMG_W8_MAX_GRID)
-    static const long w8_env = getenv("PAMG_W8_MAX_GRID") ? atol(getenv("PAMG_W8_MAX_GRID")) : -1;
-    const long w8_max = w8_env >= 0 ? w8_env : ((std::is_same<ST, Stc>::value || part >= 2) ? (1l << 40) : 4 * n_cu);
+    // cycle, scripts/ab_probe.py)
+    const long w8_max = (std::is_same<ST, Stc>::value || part >= 2) ? (1l << 40) : 4 * n_cu;
     // (and only instances that fit 64 VGPRs without scratch: several L >= 4 and n_split = 3
     // instances spill there and stay at their natural register count)
     if (part >= 4 || std::is_same<ST, StcR>::value) return launch_sltw<S, L, ST, false>(s, A, grid, part);

@@ -22,7 +22,7 @@ TNEW, TOLD, RHS, RESIDUAL, TNEW_NONLIN, SOURCE = 0, 1, 2, 3, 4, 5
  K_VCYCLE_COARSE) = range(10)
 K_NAMES = ["smooth_L1", "smooth", "residual", "restrict", "prolong", "rhs", "halo", "sweep_bench", "vcycle",
            "vcycle_coarse", "vcycle_pipe", "vcycle_rhsf", "vcycle_res", "vcycle_res_rhsf", "vcycle_corr",
-           "halo_early", "face_fallback"]
+           "halo_early", "face_fallback", "coarse_gather"]
 
 
 class PamgParams(C.Structure):

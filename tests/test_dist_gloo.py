@@ -23,6 +23,8 @@ import oracle_lib as O
 import pamg
 from pamg.solver import HaloPlan
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 S, LEVELS = 3, 3
 
 
@@ -107,3 +109,30 @@ def test_single_rank_plan_has_no_remote_entries():
     p = HaloPlan(mesh, 3, 1, 1, 0, None)
     assert len(p.remote_src) == 0 and len(p.recv_dst) == 0 and len(p.peers) == 0
     assert len(p.owned) == mesh.U
+
+
+def test_bench_rank_that_never_joins_ends_the_run_with_an_error_line():
+    """`bench.py --gpus 2` whose rank 1 never starts. RCCL's initialisation cannot be bounded
+    (profiles/r06_rccl_init_probe.txt), so bench.py meets every rank in a gloo rendezvous with a timeout before
+    pamg_comm_init: rank 0 must exit non-zero within the bound, with one JSON line naming its rank and the error,
+    instead of hanging. (Runs on the CPU: the rendezvous fails before any GPU work.)"""
+    import json
+    import socket
+    import subprocess
+    import sys
+    import time
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               PAMG_BENCH_RENDEZVOUS_S="10")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    dt = time.time() - t0
+    assert r.returncode != 0, r.stdout
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["rank"] == 0 and d["world_size"] == 2 and d["error"], d
+    assert dt < 200, dt

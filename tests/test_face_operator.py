@@ -133,18 +133,27 @@ def test_face_chain_8byte_snapshot_is_bitwise_the_oracle(solver, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mesh,S,L,parts,kind,solver,cycle", [
-    ("untitled8192.msh", 3, 3, 4, "strip", 3, 0), ("untitled8192.msh", 3, 2, 8, "strip", 3, 1),
-    ("irregular.msh", 4, 2, 8, "strip", 1, 1), ("900_ele.msh", 2, 2, 3, "block", 3, 0),
-    # bench.py's op=1 mesh on 4 x-strips: levels of 1,024 / 256 / 64 sub-elements per un_ele as one tile
-    # launch per sweep, each launch's next-sweep words exchanged into the snapshot buffer that sweep reads
-    ("untitled8192.msh", 5, 3, 4, "strip", 3, 0), ("untitled8192.msh", 4, 3, 8, "block", 1, 0)])
-def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, solver, cycle):
+@pytest.mark.parametrize("mesh,S,L,parts,kind,solver,cycle,agg", [
+    ("untitled8192.msh", 3, 3, 4, "strip", 3, 0, "1"), ("untitled8192.msh", 3, 2, 8, "strip", 3, 1, "1"),
+    ("irregular.msh", 4, 2, 8, "strip", 1, 1, "1"), ("900_ele.msh", 2, 2, 3, "block", 3, 0, "1"),
+    ("untitled8192.msh", 4, 3, 8, "block", 1, 0, "1"),
+    # bench.py's op=1 configuration (n_split 5, L 3, GS) on 8 x-strips and 4 blocks, both cycles: levels of
+    # 1,024 / 256 sub-elements per un_ele as one tile launch per sweep, each launch's next-sweep words exchanged
+    # into the snapshot buffer that sweep reads; level 3 agglomerated (the ranks' RHS gathered each cycle into a
+    # replica of the whole level, the single-domain chain on every rank)
+    ("untitled8192.msh", 5, 3, 8, "strip", 3, 0, "1"), ("untitled8192.msh", 5, 3, 8, "strip", 3, 1, "1"),
+    ("untitled8192.msh", 5, 3, 4, "block", 3, 0, "1"), ("untitled8192.msh", 5, 3, 4, "block", 3, 1, "1"),
+    # PAMG_FACE_AGG=0: the coarsest level partitioned too, one launch and one exchange per sweep
+    ("untitled8192.msh", 5, 3, 4, "strip", 3, 0, "0"), ("irregular.msh", 4, 2, 8, "strip", 1, 1, "0")])
+def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, solver, cycle, agg, monkeypatch):
     """The halo is consumed every sweep: the partitions' exchanges (the multi-rank path with the
     device-copy transport, tests/test_multirank.py) carry the values the sweeps read -- after every
-    launch that writes a sweep's words, into the snapshot buffer the next sweep reads."""
+    launch that writes a sweep's words, into the snapshot buffer the next sweep reads. The coarsest level is
+    agglomerated: per cycle one gather of its RHS and at most two coarsest-level launches
+    (the chain), instead of a launch and an exchange per sweep."""
     import pamg
     from pamg.solver import local_group, run_ranks
+    monkeypatch.setenv("PAMG_FACE_AGG", agg)
     m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
     full = pamg.SemiImplicitIterative(m, S, L, solver=solver, cycle=cycle, op=1)
     drive(full, False, cycle)
@@ -152,7 +161,11 @@ def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, s
     ps = [pamg.SemiImplicitIterative(m, S, L, solver=solver, cycle=cycle, op=1, comm=(parts, r, None, owner))
           for r in range(parts)]
     local_group(ps)
-    run_ranks(ps, lambda p: drive(p, False, cycle))
+    for p in ps:
+        p.timing_enable(1 << 6 | 1 << 17)   # PAMG_K_HALO, PAMG_K_COARSE_GATHER
+        p.timing_reset()
+    steps, cycles, ns = 2, 2, 4
+    run_ranks(ps, lambda p: drive(p, False, cycle, steps, cycles))
     ref, ref_ov = full.state(), full.overlap()
     for r, p in enumerate(ps):
         own = np.flatnonzero(owner == r)
@@ -160,6 +173,18 @@ def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, s
             np.testing.assert_array_equal(v, ref[k][:, :, own], err_msg=f"rank {r} {k}")
         for x, y in zip(p.overlap(), ref_ov):
             np.testing.assert_array_equal(x, y[:, :, own])
+        tm = p.timing()
+        n_cycles = steps * cycles
+        if agg == "1":
+            # the RHS every cycle, tnew once per call (the reference cycle) -- the corrected one starts from zero
+            assert tm["coarse_gather"]["issued"] == n_cycles + (0 if cycle else steps), tm["coarse_gather"]
+            # exchanges only around the sweeps of levels 1 and 2 (their two calls' sweeps and the residuals' refreshes):
+            # the coarsest level's 62 sweeps exchange nothing (in a local group its replica runs them one launch per
+            # sweep, the ranks sharing one GPU; one process per GPU runs them as the chain: test_rccl_self.py)
+            assert tm["halo"]["issued"] <= (4 * ns + 4) * n_cycles, tm["halo"]
+        else:
+            assert tm["coarse_gather"]["issued"] == 0
+        p.close()
 
 
 @pytest.mark.gpu
@@ -361,4 +386,30 @@ def test_face_chain_not_coresident_falls_back_bitwise(cycle, monkeypatch):
     so["t_overlap"], so["t_overlap_old"] = o.overlap()
     assert_identical(sg, so)
     assert g.timing()["face_fallback"]["issued"] >= 2, g.timing()["face_fallback"]
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ns,corr_pp", [(4, "0"), (2, "1")])
+def test_face_chain_fallback_on_the_per_step_corrected_path(ns, corr_pp, monkeypatch):
+    """the corrected cycle's per-step sequence (PAMG_FACE_CORR_PP=0, or n_smooth = 2, where the
+    passes do not apply) runs the coarsest call through the gated chain too. With the stream CU-masked every such
+    launch gives up and the host runs its fallback: the call must read the gates back before it returns (a
+    later host wait, or a hipFree's implicit device synchronisation, would otherwise wait on a gate only the host
+    opens), and a mesh re-upload right after the call must not hang. The state equals the oracle's."""
+    monkeypatch.setenv("PAMG_STREAM_CU_MASK", "half")
+    monkeypatch.setenv("PAMG_FACE_CORR_PP", corr_pp)
+    g, o = gpu_pair("untitled8192.msh", 5, 3, 3, 1, ns)
+    g.timing_reset()
+    drive(g, False, 1, steps=1, cycles=2)
+    drive(o, True, 1, steps=1, cycles=2)
+    sg, so = g.state(), o.state()
+    sg["t_overlap"], sg["t_overlap_old"] = g.overlap()
+    so["t_overlap"], so["t_overlap_old"] = o.overlap()
+    assert_identical(sg, so)
+    assert g.timing()["face_fallback"]["issued"] >= 2, g.timing()["face_fallback"]
+    # a call that leaves gates behind would deadlock here: the re-upload frees the levels (hipFree)
+    g.vcycle(1)
+    m = g.mesh
+    g._call("pamg_upload_mesh", m.U, m.X, m.region, m.neig, m.fneig, m.dir)
     g.close()

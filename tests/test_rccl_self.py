@@ -60,10 +60,33 @@ def test_rccl_self_peer_face_operator():
     """op = 1 reads the halo every sweep: the words exchanged through RCCL are load-bearing"""
     mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "irregular.msh"))
     full, s = _pair(mesh, 3, 3, 3, op=1, cycle=1, n_smooth=2)
+    s.timing_enable(1 << 17)   # PAMG_K_COARSE_GATHER
+    s.timing_reset()
     for x in (full, s):
         x.begin_timestep()
         x.vcycle(2)
     _same(full, s)
+    # the coarsest level agglomerated: its RHS crosses RCCL (to this rank itself) once per cycle
+    assert s.timing()["coarse_gather"]["issued"] == 2, s.timing()["coarse_gather"]
+
+
+def test_rccl_self_peer_face_operator_reference_cycle():
+    """the reference cycle on the face operator through RCCL: the coarsest level's tnew gathered once per call,
+    its RHS once per cycle (the bench's op = 1 configuration, n_split 5)"""
+    mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
+    full, s = _pair(mesh, 5, 3, 4, op=1, cycle=0, n_smooth=4)
+    s.timing_enable(1 << 1 | 1 << 17)   # PAMG_K_SMOOTH (levels >= 2), PAMG_K_COARSE_GATHER
+    s.timing_reset()
+    for x in (full, s):
+        x.begin_timestep()
+        x.vcycle(3)
+        x.vcycle(2)
+    _same(full, s)
+    tm = s.timing()
+    assert tm["coarse_gather"]["issued"] == 5 + 2, tm["coarse_gather"]
+    # level 2 one launch per executed sweep (2 (n_smooth - 1) a cycle, + 1 in a call's last), the coarsest level as
+    # the replica's chain: one launch a cycle, two in a call's last -- not 62 launches and exchanges a cycle
+    assert tm["smooth"]["issued"] <= 5 * (2 * 3 + 1) + 2 * 2, tm["smooth"]
 
 
 def test_rccl_self_peer_early_exchange_is_hidden():
@@ -90,3 +113,23 @@ def test_rccl_self_peer_early_exchange_is_hidden():
     assert 0 <= t0 <= t1 < t2, (t0, t1, t2)
     s.close()
     full.close()
+
+
+def test_timing_read_right_after_an_early_exchange():
+    """the early exchange's spans sit on the comm stream and the call returns without joining it.
+    On the full bench mesh the exchange can outlast the launch (it only finds free CUs in the launch's tail), so
+    timing() read straight after the call -- no state() or overlap() first, which would settle -- must still
+    wait for those spans instead of failing on an event that has not completed."""
+    mesh = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
+    part = mesh.x_strip_owner(8)
+    s = pamg.SemiImplicitIterative(mesh, 5, 3, n_smooth=4, solver=3, arith=1, self_peer=(pamg.unique_id(), part))
+    s.begin_timestep()
+    s.timing_enable(0xFFFF)
+    s.timing_reset()
+    for _ in range(3):
+        s.vcycle(1)
+        tm = s.timing()
+    assert tm["halo_early"]["issued"] == 3 and tm["halo_early"]["launches"] == 3, tm["halo_early"]
+    assert tm["halo_early"]["ms"] > 0
+    s.close()
+
