@@ -89,3 +89,22 @@ def test_c_host_example_runs_the_time_loop():
     ref = float(np.sum(o.get(O.TNEW, 1) ** 2))
     assert abs(got - ref) <= 1e-12 * ref
     assert "destroyed" in r.stdout
+
+
+def test_every_runtime_switch_is_tested_or_diagnostics_only():
+    """every PAMG_* environment switch compiled into the default libpamg is exercised by
+    a test (tests/*.py names it); the diagnostics (stamps, halo-dropping A/B) are compiled in only with the
+    PAMG_STAMPS build (`PAMG_STAMPS ? getenv(..) : nullptr`, `PAMG_STAMPS && getenv(..)`)."""
+    import glob
+    import re
+    csrc = os.path.join(ROOT, "p-a_multigrids_amd", "csrc")
+    tests = "".join(open(f).read() for f in glob.glob(os.path.join(ROOT, "tests", "*.py"))
+                    if not f.endswith("test_abi.py"))
+    untested = []
+    for f in sorted(glob.glob(os.path.join(csrc, "*"))):
+        for ln in open(f):
+            for m in re.finditer(r'getenv\("(PAMG_[A-Z0-9_]+)"\)', ln):
+                diag = re.search(r"PAMG_STAMPS\s*(\?|&&)\s*getenv", ln)
+                if not diag and m.group(1) not in tests:
+                    untested.append((os.path.basename(f), m.group(1)))
+    assert not untested, untested
