@@ -492,6 +492,11 @@ int comm_error(pamg_handle *h) {
 // N = 8 shape (1,024 un_eles, an RCCL self-peer exchange) took 233.7 us against 169.2 us without a
 // communicator, its exchange hidden behind the launch (profiles/r05_c_xe_probe.txt)
 int sync_stream(pamg_handle *h, hipStream_t s) {
+    if (h->tparent) {   // a coarsest-level replica waits as its partition does (the same stream, its exchanges)
+        const int rc = sync_stream(h->tparent, s);
+        if (rc != PAMG_OK) h->err = h->tparent->err;
+        return rc;
+    }
     CHK(face_gates_drain(h));
     if (!h->comm || (!h->comm->nccl && !h->comm->local)) {
         HIPCHK(h, hipStreamSynchronize(s));

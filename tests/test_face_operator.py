@@ -413,3 +413,37 @@ def test_face_chain_fallback_on_the_per_step_corrected_path(ns, corr_pp, monkeyp
     m = g.mesh
     g._call("pamg_upload_mesh", m.U, m.X, m.region, m.neig, m.fneig, m.dir)
     g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cycle", [0, 1])
+def test_agglomerated_coarsest_level_follows_state_set_between_calls(cycle):
+    """The agglomerated coarsest level (VERDICT r05 item 1) keeps a replica of the whole level's tnew across calls;
+    it is gathered from the ranks at the start of every call, so a partition's coarsest tnew written between calls
+    (pamg_set_state) is what the next call starts from -- as on the single domain. Driven through pamg_run too
+    (ntime 2, n_multigrid 2). 4 x-strips of untitled8192 at n_split 4, bitwise the single domain."""
+    import pamg
+    from pamg.solver import local_group, run_ranks
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, "untitled8192.msh"))
+    S, L, parts = 4, 3, 4
+    owner = m.x_strip_owner(parts)
+    full = pamg.SemiImplicitIterative(m, S, L, solver=3, cycle=cycle, op=1)
+    ps = [pamg.SemiImplicitIterative(m, S, L, solver=3, cycle=cycle, op=1, comm=(parts, r, None, owner))
+          for r in range(parts)]
+    local_group(ps)
+    rng = np.random.default_rng(6)
+    x = rng.uniform(-1, 1, (3, full.nsub(L), m.U))
+
+    def seq(s, own):
+        s.run(2, 2)
+        s.set(pamg.TNEW, L, x[:, :, own])
+        s.begin_timestep()
+        s.vcycle(3)
+    seq(full, np.arange(m.U))
+    run_ranks(ps, lambda p: seq(p, np.flatnonzero(owner == ps.index(p))))
+    ref = full.state()
+    for r, p in enumerate(ps):
+        own = np.flatnonzero(owner == r)
+        for k, v in p.state().items():
+            np.testing.assert_array_equal(v, ref[k][:, :, own], err_msg=f"rank {r} {k}")
+        p.close()
