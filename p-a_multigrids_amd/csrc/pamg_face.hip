@@ -625,6 +625,20 @@ __device__ __forceinline__ void pp_stamp(int i) {
 #ifndef PAMG_FACE_PP_FOLD_WAVES
 #define PAMG_FACE_PP_FOLD_WAVES PAMG_FACE_PP_WAVES
 #endif
+// XCD-grouped tiles: blocks b and b + 8 are dealt to one XCD (round-robin, MI355X_MICROARCH.md "Workgroup
+// dispatch"; speed only, never correctness), so the tiles are renumbered for the passes to give each XCD a
+// contiguous range of un_eles: XCD class x = b % 8 takes [x q + min(x, r), ...) of the G = 8 q + r tiles, in order.
+// A tile gathers its neighbours' boundary values (the ghost update's operands, scattered 8-byte loads); with
+// neighbours in one contiguous range they are mostly tiles of the same XCD, loaded at about the same time, so the
+// gathers hit that XCD's L2 instead of the fabric. A bijection on [0, G).
+#ifndef PAMG_FACE_PP_XCD
+#define PAMG_FACE_PP_XCD 1
+#endif
+__device__ __forceinline__ int64_t xcd_tile(unsigned b, unsigned G) {
+    const unsigned q = G >> 3, r = G & 7, x = b & 7, i = b >> 3;
+    return (int64_t)x * q + (x < r ? x : r) + i;
+}
+
 template <int TS, int NT, bool RB, int K, bool FOLD = false>
 __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256 : PAMG_FACE_PP_WAVES256_PLAIN) : FOLD ? PAMG_FACE_PP_FOLD_WAVES : PAMG_FACE_PP_WAVES) : 1) void k_face_pp(
     const double *__restrict__ A, double *out_pre, double *out_mid, double *out_end, double *out_end2,
@@ -954,7 +968,7 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
     if (PAMG_STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_stamp(5);
     };
-    tile((int64_t)blockIdx.x);
+    tile(PAMG_FACE_PP_XCD ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
 }
 
 // ---- the wavefront call: every sweep of one smoother call on a level too large to stay on-chip
