@@ -16,6 +16,12 @@ if [ "$2" = "A" ]; then
   for f in bench bench_driver; do grep '^{' $O/$f.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); e=d.get('extra',{}); print('$f', d['value'], d['ms_per_step'], d['roofline']['frac'], (d.get('roofline_hbm_smoother') or {}).get('frac'), (e.get('op1') or {}).get('vcycles_per_s'), (e.get('op1_cycle1') or {}).get('vcycles_per_s'), (e.get('cycle1') or {}).get('vcycles_per_s'), (d.get('cpu_baseline') or {}).get('value'), ((d.get('cpu_baseline') or {}).get('all_cores') or {}).get('value'))"; done
   timeout -k 10 400 python scripts/strong_probe.py > $O/strong.txt 2>&1 || exit 1
   timeout -k 10 300 python -u scripts/face_strong_probe.py 5 10 1 > $O/face_partitions.txt 2>&1 || exit 1
+  # the multi-rank orchestration of bench.py (rendezvous, barrier before the communicator, MAX over ranks) on one
+  # GPU: two detached ranks (RCCL refuses two ranks on one GPU; the exchange itself is tests/test_rccl_self.py's)
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 5 --comm detached > $O/bench_2ranks_detached.log 2>&1 || \
+      { tail -20 $O/bench_2ranks_detached.log; exit 1; }
+  grep '^{' $O/bench_2ranks_detached.log | cut -c1-300
 fi
 if [ "$2" = "B" ]; then
   cd /tmp && export TMPDIR=/tmp
