@@ -2133,6 +2133,14 @@ int agg_create(pamg_handle *h, int U, const double *X, const int *region, const 
     const int L = h->p.multi_levels;
     if (h->coarse_only || h->p.op != 1 || L < 2 || (h->nranks == 1 && h->vpart.empty()) || (e && atoi(e) == 0))
         return PAMG_OK;
+    // only a level the persistent chain holds: that is what makes the whole level cost every rank no more than its
+    // own part did (latency-bound sweeps); a larger coarsest level stays partitioned, one launch per sweep
+    if (!h->cus) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || n <= 0) n = 1;
+        h->cus = n;
+    }
+    if (!face_chain_fits(1 << (2 * (h->p.n_split - L + 1)), U, h->cus)) return PAMG_OK;
     // the replica's numbering: rank 0's un_eles (ascending global id), then rank 1's, ... (a self-peer
     // communicator: one block, the global order)
     std::vector<int> order;
