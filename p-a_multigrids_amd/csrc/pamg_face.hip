@@ -696,8 +696,12 @@ __global__ __launch_bounds__(NT, RB ? (TS <= 256 ? (FOLD ? PAMG_FACE_PP_WAVES256
     int4 ge = make_int4(-1, -1, -1, -1);
     int gp = 0;   // e's face pattern (Level::gpat), loaded beside the entry
     if (gon) {
+#if PAMG_DIAG_NOGATHER   // timing diagnostic only (wrong results): no gather entry, no neighbour values, no ghost update
+        ge = make_int4(-3, 0, 0, 0);
+#else
         ge = gtab[(u * 3 + fu - 1) * M + spu - 1];
         gp = gpat[(u * 3 + fu - 1) * M + spu - 1];
+#endif
     }
     // the start iterate at global position g: A's value, plus the prolonged coarse correction where Tc is given (the
     // corrected cycle's interp_add, k_interp_add's arithmetic, folded into the first pass of the smoother call that
