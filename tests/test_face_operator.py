@@ -144,7 +144,10 @@ def test_face_chain_8byte_snapshot_is_bitwise_the_oracle(solver, monkeypatch):
     ("untitled8192.msh", 5, 3, 8, "strip", 3, 0, "1"), ("untitled8192.msh", 5, 3, 8, "strip", 3, 1, "1"),
     ("untitled8192.msh", 5, 3, 4, "block", 3, 0, "1"), ("untitled8192.msh", 5, 3, 4, "block", 3, 1, "1"),
     # PAMG_FACE_AGG=0: the coarsest level partitioned too, one launch and one exchange per sweep
-    ("untitled8192.msh", 5, 3, 4, "strip", 3, 0, "0"), ("irregular.msh", 4, 2, 8, "strip", 1, 1, "0")])
+    ("untitled8192.msh", 5, 3, 4, "strip", 3, 0, "0"), ("irregular.msh", 4, 2, 8, "strip", 1, 1, "0"),
+    # four levels: two partitioned levels below the agglomerated one
+    ("900_ele.msh", 4, 4, 4, "strip", 3, 0, "1"), ("untitled8192.msh", 4, 4, 8, "block", 1, 1, "1"),
+    ("test_sn2.msh", 4, 4, 3, "strip", 3, 1, "1")])
 def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, solver, cycle, agg, monkeypatch):
     """The halo is consumed every sweep: the partitions' exchanges (the multi-rank path with the
     device-copy transport, tests/test_multirank.py) carry the values the sweeps read -- after every
@@ -178,10 +181,10 @@ def test_face_operator_partitions_match_single_domain(mesh, S, L, parts, kind, s
         if agg == "1":
             # the RHS every cycle, tnew once per call (the reference cycle) -- the corrected one starts from zero
             assert tm["coarse_gather"]["issued"] == n_cycles + (0 if cycle else steps), tm["coarse_gather"]
-            # exchanges only around the sweeps of levels 1 and 2 (their two calls' sweeps and the residuals' refreshes):
+            # exchanges only around the sweeps of levels 1 .. L-1 (their two calls' sweeps and the residuals' refreshes):
             # the coarsest level's 62 sweeps exchange nothing (in a local group its replica runs them one launch per
             # sweep, the ranks sharing one GPU; one process per GPU runs them as the chain: test_rccl_self.py)
-            assert tm["halo"]["issued"] <= (4 * ns + 4) * n_cycles, tm["halo"]
+            assert tm["halo"]["issued"] <= (L - 1) * (2 * ns + 2) * n_cycles, tm["halo"]
         else:
             assert tm["coarse_gather"]["issued"] == 0
         p.close()
