@@ -107,3 +107,31 @@ def test_zero_cycles_and_zero_steps_change_nothing(op):
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,own,n", [("one_tri.msh", [0], 2), ("untitled8.msh", [0, 0, 0, 0, 2, 2, 2, 2], 3)])
+@pytest.mark.parametrize("op,cycle,fused", [(0, 0, 3), (0, 0, 0), (1, 0, 3), (1, 1, 3)])
+def test_rank_owning_no_un_ele(mesh, own, n, op, cycle, fused):
+    """A partition with a rank that owns nothing (more ranks than un_eles, or an owner map that skips a rank):
+    that rank still takes part in every exchange and coarsest-level gather, with nothing to send, and the
+    owning ranks' state equals the single domain's bit for bit (local-group transport)."""
+    import pamg
+    from pamg.solver import local_group, run_ranks
+    m = pamg.Mesh.read(os.path.join(goldens.MESHES, mesh))
+    owner = np.array(own, np.int32)
+    full = pamg.SemiImplicitIterative(m, 3, 3, op=op, cycle=cycle, fused=fused)
+    full.run(2, 2)
+    ps = [pamg.SemiImplicitIterative(m, 3, 3, op=op, cycle=cycle, fused=fused, comm=(n, r, None, owner))
+          for r in range(n)]
+    local_group(ps)
+    run_ranks(ps, lambda p: p.run(2, 2))
+    ref, ref_ov = full.state(), full.overlap()
+    for r, p in enumerate(ps):
+        o = np.flatnonzero(owner == r)
+        for k, v in p.state().items():
+            np.testing.assert_array_equal(v, ref[k][:, :, o], err_msg=f"rank {r} {k}")
+        for x, y in zip(p.overlap(), ref_ov):
+            np.testing.assert_array_equal(x, y[:, :, o])
+        p.close()
+    full.close()
