@@ -1312,6 +1312,17 @@ bool face_coarse_merged(pamg_handle *h, bool last) {
     return !last && h->p.n_smooth >= 1 && h->p.n_coarse >= 1;
 }
 
+// :336 for level l >= 2 of the face cycle: the restriction of level l's previous residual into level l+1's RHS -- the
+// buffer a fold made in the previous cycle's pass (swapped in), else the restrictor
+int face_restrict_prev(pamg_handle *h, int l) {
+    if (h->pp_folded[l]) {
+        std::swap(h->lv[l + 1].RHS, h->lv[l + 1].RHSN_alt);
+        h->pp_folded[l] = false;
+        return PAMG_OK;
+    }
+    return restrict_(h, l);
+}
+
 // level l's part of cycle c of the fused face cycle (levels l .. L): the coarsest level's calls; a level
 // below it as a two-sweep stream (its restrictor before the launch that writes its new residual, then the
 // next level), or as its two calls around the next level (vcycle_face_fused's order)
@@ -1333,7 +1344,7 @@ int face_pp_level(pamg_handle *h, int l, bool last) {
     }
     if (!face_pp_ok(h, l) || 2 * (ns - 1) + (last ? 1 : 0) < 3) {   // (one pass could not rotate its buffers)
         CHK(face_call(h, l, true, ns, true));
-        CHK(restrict_(h, l));
+        CHK(face_restrict_prev(h, l));
         CHK(face_pp_level(h, l + 1, last));
         return face_call(h, l, true, ns, !last, true);
     }
@@ -1341,12 +1352,22 @@ int face_pp_level(pamg_handle *h, int l, bool last) {
     h->overlap_static_l1 = false;
     std::vector<PPPass> plan;
     CHK(face_pp_plan(h, l, 2 * (ns - 1) + (last ? 1 : 0), h->lv[l].T, {ns - 1}, last ? 1 : 2, plan));
+    // the restrictor folded (vcycle_face_pp's level-1 fold, one level down): the pass that computes this cycle's
+    // residual restricts it into level l+1's RHSN_alt and, but in the call's last cycle, does not store it (only
+    // the restrictor reads it); the next cycle swaps that buffer in where it would restrict
+    const bool fold = h->pp_fold && h->lv[l + 1].RHSN_alt;
     bool restricted = false;
     for (const PPPass &q : plan) {
-        if (q.res && !restricted) { CHK(restrict_(h, l)); restricted = true; }   // :336, the previous residual
-        CHK(face_pp_emit(h, l, q));
+        if (q.res && !restricted) { CHK(face_restrict_prev(h, l)); restricted = true; }   // :336, the previous residual
+        PPPass qf = q;
+        if (q.res && fold && !last) {
+            qf.rhsc = h->lv[l + 1].RHSN_alt;
+            qf.res_drop = true;
+        }
+        CHK(face_pp_emit(h, l, qf));
+        if (qf.rhsc) h->pp_folded[l] = true;
     }
-    if (!restricted) CHK(restrict_(h, l));
+    if (!restricted) CHK(face_restrict_prev(h, l));
     return face_pp_level(h, l + 1, last);
 }
 
@@ -1373,13 +1394,22 @@ int vcycle_face_pp(pamg_handle *h, int n) {
     const char *rr_env = getenv("PAMG_FACE_RR");
     Level &L2 = h->lv[2];
     const bool rf = !(rr_env && atoi(rr_env) == 0) && h->p.multi_levels >= 2 && L2.RHSN_alt;
-    double *const rhs2_home = L2.RHS;
-    // an error return inside the loop leaves level 2's buffers as it found them (the state is invalid after an
-    // error, but RHS and RHSN_alt stay the handle's own two buffers in their roles)
+    // levels 2 .. L: each RHS's own buffer (the folds swap RHS and RHSN_alt). An error return inside the loop leaves
+    // the buffers as it found them (the state is invalid after an error, but RHS and RHSN_alt stay the handle's own
+    // two buffers in their roles); the coarse levels' folds are off outside this call
+    const int Lc = h->p.multi_levels;
+    double *rhs_home[kMaxLevels + 1] = {};
+    for (int l = 2; l <= Lc; ++l) rhs_home[l] = h->lv[l].RHS;
     struct Home {
-        Level &V; double *home;
-        ~Home() { if (V.RHS != home) std::swap(V.RHS, V.RHSN_alt); }
-    } home_guard{L2, rhs2_home};
+        pamg_handle *h; int Lc; double *const *home;
+        ~Home() {
+            for (int l = 2; l <= Lc; ++l)
+                if (h->lv[l].RHS != home[l]) std::swap(h->lv[l].RHS, h->lv[l].RHSN_alt);
+            h->pp_fold = false;
+            for (bool &f : h->pp_folded) f = false;
+        }
+    } home_guard{h, Lc, rhs_home};
+    h->pp_fold = rf;
     size_t p = 0;
     for (int c = 0; c < n; ++c) {
         h->tnn_level = 1;
@@ -1397,9 +1427,11 @@ int vcycle_face_pp(pamg_handle *h, int n) {
         CHK(face_pp_level(h, 2, c + 1 == n));
     }
     for (; p < plan.size(); ++p) CHK(face_pp_emit(h, 1, plan[p]));
-    if (L2.RHS != rhs2_home) {   // level 2's RHS back in its own buffer
-        HIPCHK(h, hipMemcpyAsync(L2.RHSN_alt, L2.RHS, 3 * (size_t)L2.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
-        std::swap(L2.RHS, L2.RHSN_alt);
+    for (int l = 2; l <= Lc; ++l) {   // each RHS back in its own buffer
+        Level &V = h->lv[l];
+        if (V.RHS == rhs_home[l]) continue;
+        HIPCHK(h, hipMemcpyAsync(V.RHSN_alt, V.RHS, 3 * (size_t)V.pitch * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+        std::swap(V.RHS, V.RHSN_alt);
     }
     // the halo the per-step sequence leaves: level 1's last smoother call's words, from its tnew (:555)
     HIPCHK(h, launch_face_words(h->stream, h->lv[1], h->U, h->tov, h->tovo));
@@ -2501,14 +2533,15 @@ int pamg_upload_mesh(pamg_handle *h, int U, const double *X, const int *region, 
         // within noise: profiles/r05_e_asm_layouts.txt)
         L.pitch = std::max<int64_t>(64, (L.N + 63) / 64 * 64);
         double *base = nullptr;
-        // level 1: the source term s' (SRC); level 2: RHSN_alt for the concurrent fused cycle
-        const size_t planes = (l <= 2) ? 21 : 18;
+        // level 1: the source term s' (SRC); level 2: RHSN_alt for the concurrent fused cycle and the face cycle's
+        // level-1 restrictor fold, levels 3 .. L: RHSN_alt for the face cycle's folds of the coarser levels
+        const size_t planes = 21;
         CHK(dev_alloc(h, &base, planes * (size_t)L.pitch));
         HIPCHK(h, hipMemsetAsync(base, 0, planes * (size_t)L.pitch * sizeof(double), h->stream));
         L.T = base; L.TNN = base + 3 * L.pitch; L.RHS = base + 6 * L.pitch; L.RES = base + 9 * L.pitch;
         L.TOLD = base + 12 * L.pitch;
         L.RHSN = base + 15 * L.pitch;   // restriction of the zero residual: valid
-        L.RHSN_alt = (l == 2) ? base + 18 * L.pitch : nullptr;
+        L.RHSN_alt = (l >= 2) ? base + 18 * L.pitch : nullptr;
         L.SRC = (l == 1) ? base + 18 * L.pitch : nullptr;
         std::vector<double> stc((size_t)std::max(Ul, 1) * kStcStride, 0.0);
         for (int q = 0; q < Ul; ++q) {

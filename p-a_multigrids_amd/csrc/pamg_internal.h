@@ -203,6 +203,11 @@ struct pamg_handle {
     hipEvent_t ev_fine = nullptr, ev_coarse = nullptr;
     // RHSN of every level holds the restriction of the finer level's current residual
     bool rhsn_valid = true;
+    // op = 1, cycle 0, inside vcycle_face_pp (PAMG_FACE_RR): a streaming level l >= 2 folds its restrictor into the pass
+    // that computes its residual (into level l+1's RHSN_alt, swapped in at the next cycle's restriction point);
+    // pp_folded[l]: level l+1's RHSN_alt holds the restriction of level l's latest residual (face_restrict_prev)
+    bool pp_fold = false;
+    bool pp_folded[pamg::kMaxLevels + 1] = {};
     bool mesh_ready = false;
     std::string err;
     pamg::Timing timing;
